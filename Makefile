@@ -1,0 +1,41 @@
+# Top-level build: product libraries (HIP for gfx950 + host C++) and the
+# oracle (test infrastructure).  No cmake/ninja needed.
+#
+#   make            -> dealii-ns-gls_amd/lib/libglsmesh.so, libglsamd.so, oracle/liboracle.so
+#   make mesh|amd|oracle
+#   make clean
+
+PKG      := dealii-ns-gls_amd
+LIBDIR   := $(PKG)/lib
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+ARCH     ?= gfx950
+
+CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
+HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics \
+            -Wall -Wno-unused-parameter -Wno-unused-function
+
+MESH_SRC := $(PKG)/host/mesh.cc
+AMD_SRC  := $(wildcard $(PKG)/csrc/*.hip) $(wildcard $(PKG)/csrc/*.cc)
+AMD_HDR  := $(wildcard $(PKG)/csrc/*.h) $(wildcard $(PKG)/csrc/*.cuh) include/gls_op.h
+
+all: mesh amd oracle
+
+mesh: $(LIBDIR)/libglsmesh.so
+amd: $(LIBDIR)/libglsamd.so
+oracle:
+	$(MAKE) -C oracle
+
+$(LIBDIR)/libglsmesh.so: $(MESH_SRC) include/gls_mesh.h
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(CXXFLAGS) -shared -o $@ $(MESH_SRC)
+
+$(LIBDIR)/libglsamd.so: $(AMD_SRC) $(AMD_HDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(AMD_SRC)
+
+clean:
+	rm -f $(LIBDIR)/*.so
+	$(MAKE) -C oracle clean
+
+.PHONY: all mesh amd oracle clean

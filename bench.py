@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""bench.py — vmult DoF/s + achieved HBM-roofline fraction of the matrix-free
+GLS Navier–Stokes operator on MI355X (BASELINE.json metric).
+
+Workload (N = 1): input_hoffmann_3D_Re3900.json — 3D flow past a cylinder,
+Q2/Q2 (FESystem(FE_Q(2), 4)), QGauss(3), MappingQ2, 2 global refinements
+(25,600 cells, 878,592 DoFs), Newton-Jacobian (increment-form) operator in
+FP64, BDF2 with dt = 2.5e-4, synthetic inputs of SURVEY §8d.  One "step" =
+one operator apply (vmult) on inputs already resident in HBM.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--nref R]
+For N > 1 launch with torch.distributed.run (one rank per GPU); cells are
+partitioned into contiguous x-slabs, ghost DoFs exchanged over RCCL.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dealii-ns-gls_amd", "python"))
+
+import numpy as np  # noqa: E402
+
+import glsinputs as gi  # noqa: E402
+import glsmesh as gm  # noqa: E402
+
+HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
+DECK = "input_hoffmann_3D_Re3900.json"
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(case_mesh, cmask, params, weights, u_star, hist, src, n_dofs, budget_s=12.0):
+    """Oracle (CPU restatement, 'port') timed on the host cores: bounded
+    sample of the same workload (whole vmults of the same mesh)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    orc.set_threads(threads)
+    om = orc.OracleMesh(case_mesh, cmask)
+    o = orc.Oracle(om, **params)
+    o.set_linearization_point(u_star)
+    if params["order"] > 0:
+        o.set_previous_solution(hist, weights)
+    o.vmult(src)  # warm-up
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        o.vmult(src)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el > budget_s or reps >= 50:
+            break
+    return dict(value=n_dofs * reps / el, unit="DoF/s", cores=threads, kind="port",
+                sample=f"{reps} full FP64 Newton vmults of the same Re3900 mesh "
+                       f"({n_dofs} DoFs), oracle/gls_oracle.c with {threads} OpenMP threads, "
+                       f"{el:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--nref", type=int, default=None)
+    ap.add_argument("--precision", default="f64")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import glsamd
+    d = gm.read_deck(os.path.join(gm.DECK_DIR, DECK))
+    n_ref = d.n_refinements if args.nref is None else args.nref
+    t0 = time.time()
+    mesh = d.mesh(n_ref)
+    vel, p, slip = d.boundary_descriptor()
+    cmask = mesh.constraint_mask(vel, p, slip)
+    params, weights = d.operator_parameters(2.5e-4)
+    n_dofs = mesh.n_dofs
+    src_h = gi.src_vector(n_dofs)
+    u_star = gi.linearization_point(mesh.n_nodes, mesh.dim, d.u_max)
+    hist = gi.history(u_star, params["order"])
+    log(f"[bench] mesh {mesh.n_cells} cells, {n_dofs} DoFs ({time.time() - t0:.1f}s)")
+
+    if world > 1:
+        import glsdist
+        runner = glsdist.DistributedOperator(mesh, cmask, args.precision, dist, rank, world)
+        runner.setup(params, u_star, hist, weights)
+        src = runner.scatter_global(src_h)
+        dst = runner.new_vector()
+        apply_fn = lambda: runner.vmult(dst, src)  # noqa: E731
+        kernel_fn = None
+        local_cells = runner.n_local_cells
+        op = runner.op
+    else:
+        op = glsamd.NavierStokesOperator(mesh, cmask, args.precision)
+        op.set_parameters(**params)
+        op.set_linearization_point(u_star)
+        if params["order"] > 0:
+            op.set_previous_solution(hist, weights)
+        src = op._dev(src_h)
+        dst = op.initialize_dof_vector()
+        local_cells = op.n_cells
+
+        def apply_fn():
+            op.vmult(dst, src)
+
+        def kernel_fn(ev0, ev1):
+            op.vmult_init(dst, src)
+            ev0.record()
+            op.vmult_cells(dst, src, 0, op.n_cells)
+            ev1.record()
+
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        apply_fn()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        apply_fn()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t_start
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms = el / args.steps * 1e3
+    value = n_dofs * args.steps / el
+
+    # per-launch duration of the dominant kernel (cell-loop kernel), HIP
+    # events on the stream it is launched on (torch's current stream)
+    kernel_ms = None
+    if kernel_fn is not None:
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        for e0, e1 in evs:
+            kernel_fn(e0, e1)
+        torch.cuda.synchronize()
+        kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+    bytes_per_vmult = op.vmult_bytes()
+    n_gen, n_cart = op.geometry_counts()
+    out = None
+    if rank == 0:
+        if kernel_ms is None:
+            kernel_ms = ms
+        achieved = bytes_per_vmult / (kernel_ms * 1e-3)
+        traffic = None
+        tf = os.environ.get("GLS_TRAFFIC_JSON")
+        if tf and os.path.exists(tf):
+            with open(tf) as f:
+                traffic = json.load(f).get("bytes_per_launch")
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(mesh, cmask, params, weights, u_star, hist, src_h, n_dofs,
+                                   args.cpu_budget)
+            except Exception as e:  # baseline is reported, never fatal
+                cpu = dict(value=None, unit="DoF/s", cores=0, kind="port", sample=f"failed: {e}")
+        out = {
+            "metric": "vmult DoF/s (3D cylinder Re=3900 Q2, FP64 Newton-Jacobian GLS operator)",
+            "value": value,
+            "unit": "DoF/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64" if args.precision == "f64" else "f32",
+            "data": "synthetic (SURVEY §8d splitmix64 inputs on the generated cylinder mesh)",
+            "config": {"workload": f"{DECK} r{n_ref}: {mesh.n_cells} cells, {n_dofs} DoFs, "
+                                   f"Q2/Q2, MappingQ2, BDF2, increment form",
+                       "cells": mesh.n_cells, "dofs": n_dofs, "cells_per_gpu": local_cells,
+                       "general_geometry_cells": n_gen, "cartesian_cells": n_cart,
+                       "parallelism": f"cells x-slab partitioned over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
+                         "kernel": "gls::k_apply<3,2,double,MODE_NEWTON>",
+                         "kernel_ms": kernel_ms, "algorithmic_bytes": bytes_per_vmult},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

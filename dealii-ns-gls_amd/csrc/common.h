@@ -1,0 +1,48 @@
+// common.h — shared host helpers of libglsamd.so (error handling, 1D basis).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace gls
+{
+void set_error(const std::string &s);
+
+#define HIP_THROW(expr)                                                                      \
+  do                                                                                         \
+    {                                                                                        \
+      const hipError_t e_ = (expr);                                                          \
+      if (e_ != hipSuccess)                                                                  \
+        throw std::runtime_error(std::string(#expr) + ": " + hipGetErrorString(e_));         \
+    }                                                                                        \
+  while (0)
+
+// every C-ABI function body is wrapped in these: exceptions -> status 1 +
+// thread-local message (the reference's AssertThrow becomes a status code)
+#define GLS_TRY \
+  try           \
+    {
+#define GLS_CATCH                                 \
+  }                                               \
+  catch (const std::exception &ex_)               \
+    {                                             \
+      gls::set_error(ex_.what());                 \
+      return 1;                                   \
+    }                                             \
+  return 0;
+
+// FE_Q(k) on Gauss-Lobatto points, QGauss(k+1), on [0,1]
+struct Basis1D
+{
+  int                 n = 0;
+  std::vector<double> nodes, qp, qw;
+  std::vector<double> S;  // S[q*n+i]  = phi_i(x_q)
+  std::vector<double> D;  // D[q*n+i]  = phi_i'(x_q)
+  std::vector<double> Dq; // Dq[q*n+j] = l_j'(x_q), l_j Lagrange on Gauss points
+  explicit Basis1D(int k);
+};
+
+} // namespace gls

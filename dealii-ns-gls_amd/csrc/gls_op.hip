@@ -1,0 +1,855 @@
+// gls_op.hip — host side of the C-ABI (include/gls_op.h): operator setup
+// (MatrixFree-style compressed geometry, packed cell→node indices with the
+// constrained-component bits, per-q tables), and the launch functions for the
+// vmult / residual / diagonal / table-producer kernels of kernels.h.
+#include "../../include/gls_op.h"
+#include "common.h"
+#include "kernels.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+using namespace gls;
+
+namespace gls
+{
+thread_local std::string g_err;
+
+void
+set_error(const std::string &s)
+{
+  g_err = s;
+}
+
+// ------------------------------------------------------------ 1D basis (host)
+Basis1D::Basis1D(int k)
+{
+  n = k + 1;
+  if (k == 1)
+    nodes = {0.0, 1.0};
+  else if (k == 2)
+    nodes = {0.0, 0.5, 1.0};
+  else if (k == 3)
+    nodes = {0.0, 0.5 - std::sqrt(5.0) / 10.0, 0.5 + std::sqrt(5.0) / 10.0, 1.0};
+  else
+    throw std::runtime_error("degree > 3 not supported");
+  // Gauss-Legendre on [0,1]
+  qp.resize(n);
+  qw.resize(n);
+  for (int i = 0; i < n; ++i)
+    {
+      double z = std::cos(M_PI * (i + 0.75) / (n + 0.5)), pp = 0;
+      for (int it = 0; it < 100; ++it)
+        {
+          double p1 = 1, p2 = 0;
+          for (int j = 1; j <= n; ++j)
+            {
+              const double p3 = p2;
+              p2              = p1;
+              p1              = ((2.0 * j - 1.0) * z * p2 - (j - 1.0) * p3) / j;
+            }
+          pp              = n * (z * p1 - p2) / (z * z - 1.0);
+          const double z1 = z;
+          z               = z1 - p1 / pp;
+          if (std::abs(z - z1) < 1e-16)
+            break;
+        }
+      qp[n - 1 - i] = 0.5 * (1.0 + z);
+      qw[n - 1 - i] = 1.0 / ((1.0 - z * z) * pp * pp);
+    }
+  auto lagrange = [](const std::vector<double> &x, int i, double t, double &val, double &der) {
+    const int m = (int)x.size();
+    val = 1, der = 0;
+    for (int j = 0; j < m; ++j)
+      if (j != i)
+        {
+          double prod = 1.0 / (x[i] - x[j]);
+          for (int l = 0; l < m; ++l)
+            if (l != i && l != j)
+              prod *= (t - x[l]) / (x[i] - x[l]);
+          der += prod;
+          val *= (t - x[j]) / (x[i] - x[j]);
+        }
+  };
+  S.assign(n * n, 0);
+  D.assign(n * n, 0);
+  Dq.assign(n * n, 0);
+  for (int q = 0; q < n; ++q)
+    for (int i = 0; i < n; ++i)
+      {
+        double v, d;
+        lagrange(nodes, i, qp[q], v, d);
+        S[q * n + i] = v;
+        D[q * n + i] = d;
+        lagrange(qp, i, qp[q], v, d);
+        Dq[q * n + i] = d;
+      }
+}
+
+} // namespace gls
+
+// ------------------------------------------------------------ operator state
+struct glsOp_
+{
+  int     dim = 3, degree = 2, prec = GLS_F64;
+  int64_t n_cells = 0, n_nodes = 0, n_owned_nodes = 0, n_dofs = 0, n_owned_dofs = 0;
+  int     nq = 0, nf = 0;
+  Basis1D basis{1};
+
+  glsOpParams prm{};
+  bool        have_lin = false, have_prev = false, have_old_grad = false;
+
+  int64_t n_gen = 0, n_cart = 0;
+  // device buffers
+  uint32_t *d_nodes    = nullptr;
+  uint32_t *d_cell_geo = nullptr;
+  void     *d_geo_cart = nullptr;
+  void     *d_geo_gen  = nullptr;
+  void     *d_tab      = nullptr;
+  void     *d_cellwise = nullptr;
+  void     *d_old_grad = nullptr;
+  void     *d_hq       = nullptr;
+  void     *d_hmin     = nullptr;
+  void     *d_tmp      = nullptr;
+  uint32_t *d_cbits    = nullptr;
+  int       device     = 0;
+
+  size_t
+  tsize() const
+  {
+    return prec == GLS_F64 ? 8 : 4;
+  }
+};
+
+namespace
+{
+template <typename T>
+void
+upload(void **dptr, const std::vector<T> &h)
+{
+  HIP_THROW(hipMalloc(dptr, std::max<size_t>(1, h.size() * sizeof(T))));
+  if (!h.empty())
+    HIP_THROW(hipMemcpy(*dptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+}
+
+template <typename T>
+std::vector<T>
+convert(const std::vector<double> &v)
+{
+  return std::vector<T>(v.begin(), v.end());
+}
+
+// geometry of one cell at all q: J[d][a] = dx_d / dxi_a by sum factorisation
+void
+cell_jacobians(int dim, const Basis1D &b, const double *X /* [nloc][dim] */,
+               std::vector<double> &J /* [nq][dim][dim] */)
+{
+  const int n = b.n, nq = dim == 3 ? n * n * n : n * n;
+  J.assign((size_t)nq * dim * dim, 0.0);
+  for (int q = 0; q < nq; ++q)
+    {
+      const int qa[3] = {q % n, (q / n) % n, dim == 3 ? q / (n * n) : 0};
+      for (int i = 0; i < nq; ++i)
+        {
+          const int ia[3] = {i % n, (i / n) % n, dim == 3 ? i / (n * n) : 0};
+          double    sv[3], dv[3];
+          for (int a = 0; a < dim; ++a)
+            {
+              sv[a] = b.S[qa[a] * n + ia[a]];
+              dv[a] = b.D[qa[a] * n + ia[a]];
+            }
+          for (int a = 0; a < dim; ++a)
+            {
+              double w = 1;
+              for (int bb = 0; bb < dim; ++bb)
+                w *= (bb == a) ? dv[bb] : sv[bb];
+              if (w == 0.0)
+                continue;
+              for (int d = 0; d < dim; ++d)
+                J[(q * dim + d) * dim + a] += X[i * dim + d] * w;
+            }
+        }
+    }
+}
+
+void
+invert(int dim, const double *J, double *inv, double &det)
+{
+  if (dim == 2)
+    {
+      det    = J[0] * J[3] - J[1] * J[2];
+      inv[0] = J[3] / det, inv[1] = -J[1] / det, inv[2] = -J[2] / det, inv[3] = J[0] / det;
+    }
+  else
+    {
+      det = J[0] * (J[4] * J[8] - J[5] * J[7]) - J[1] * (J[3] * J[8] - J[5] * J[6]) +
+            J[2] * (J[3] * J[7] - J[4] * J[6]);
+      inv[0] = (J[4] * J[8] - J[5] * J[7]) / det;
+      inv[1] = (J[2] * J[7] - J[1] * J[8]) / det;
+      inv[2] = (J[1] * J[5] - J[2] * J[4]) / det;
+      inv[3] = (J[5] * J[6] - J[3] * J[8]) / det;
+      inv[4] = (J[0] * J[8] - J[2] * J[6]) / det;
+      inv[5] = (J[2] * J[3] - J[0] * J[5]) / det;
+      inv[6] = (J[3] * J[7] - J[4] * J[6]) / det;
+      inv[7] = (J[1] * J[6] - J[0] * J[7]) / det;
+      inv[8] = (J[0] * J[4] - J[1] * J[3]) / det;
+    }
+}
+
+template <typename T, int n>
+Shape<T, n>
+make_shape(const Basis1D &b)
+{
+  Shape<T, n> s;
+  for (int q = 0; q < n; ++q)
+    {
+      for (int i = 0; i < n; ++i)
+        {
+          s.S[q][i]  = (T)b.S[q * n + i];
+          s.Dq[q][i] = (T)b.Dq[q * n + i];
+        }
+      s.w[q] = (T)b.qw[q];
+    }
+  return s;
+}
+
+// ------------------------------------------------------------ dispatch
+template <int dim, int k, typename T>
+struct Impl
+{
+  static constexpr int n  = k + 1;
+  static constexpr int nq = ipow(n, dim);
+
+  static ApplyArgs<T, dim, n>
+  args(const glsOp_ *op)
+  {
+    ApplyArgs<T, dim, n> a;
+    a.nodes         = op->d_nodes;
+    a.cell_geo      = op->d_cell_geo;
+    a.geo_cart      = (const T *)op->d_geo_cart;
+    a.n_cart        = op->n_cart;
+    a.geo_gen       = (const T *)op->d_geo_gen;
+    a.gen_stride    = op->n_gen * nq;
+    a.tab           = (const T *)op->d_tab;
+    a.tab_stride    = op->n_cells * nq;
+    a.cellwise      = (const T *)op->d_cellwise;
+    a.n_cells       = op->n_cells;
+    a.old_grad      = (const T *)op->d_old_grad;
+    a.dst           = nullptr;
+    a.src           = nullptr;
+    a.cell_begin    = 0;
+    a.cell_end      = op->n_cells;
+    a.nu            = (T)op->prm.nu;
+    a.w0            = (T)op->prm.w0;
+    a.theta         = (T)op->prm.theta;
+    a.td            = ((op->prm.flags & GLS_CONSIDER_TIME_DERIVATIVE) && op->prm.order > 0) ? 1 : 0;
+    a.cw            = (op->prm.flags & GLS_CELL_WISE_STAB) ? 1 : 0;
+    a.have_prev     = op->have_prev ? 1 : 0;
+    a.have_old_grad = (op->have_old_grad && op->prm.theta != 1.0) ? 1 : 0;
+    a.diag_ndof     = nq * (dim + 1);
+    a.sh            = make_shape<T, n>(op->basis);
+    return a;
+  }
+
+  static void
+  apply(const glsOp_ *op, int mode, bool diag, void *dst, const void *src, int64_t b, int64_t e,
+        hipStream_t s)
+  {
+    if (e <= b)
+      return;
+    auto a       = args(op);
+    a.dst        = (T *)dst;
+    a.src        = (const T *)src;
+    a.cell_begin = b;
+    a.cell_end   = e;
+    constexpr int CPB = BLOCK / nq;
+    const int64_t nv  = (e - b) * (diag ? (int64_t)nq * (dim + 1) : 1);
+    const dim3    grid((unsigned)((nv + CPB - 1) / CPB));
+#define GLS_LAUNCH(M, DG) hipLaunchKernelGGL((k_apply<dim, k, T, M, DG>), grid, dim3(BLOCK), 0, s, a)
+    if (diag)
+      {
+        if (mode == MODE_NEWTON)
+          GLS_LAUNCH(MODE_NEWTON, true);
+        else
+          GLS_LAUNCH(MODE_FIXED, true);
+      }
+    else if (mode == MODE_NEWTON)
+      GLS_LAUNCH(MODE_NEWTON, false);
+    else if (mode == MODE_FIXED)
+      GLS_LAUNCH(MODE_FIXED, false);
+    else
+      GLS_LAUNCH(MODE_RESIDUAL, false);
+#undef GLS_LAUNCH
+    HIP_THROW(hipGetLastError());
+  }
+
+  static void
+  produce(const glsOp_ *op, int what, const void *vec, hipStream_t s)
+  {
+    ProducerArgs<T, dim, n> a;
+    a.nodes      = op->d_nodes;
+    a.cell_geo   = op->d_cell_geo;
+    a.geo_cart   = (const T *)op->d_geo_cart;
+    a.n_cart     = op->n_cart;
+    a.geo_gen    = (const T *)op->d_geo_gen;
+    a.gen_stride = op->n_gen * nq;
+    a.tab        = (T *)op->d_tab;
+    a.tab_stride = op->n_cells * nq;
+    a.cellwise   = (T *)op->d_cellwise;
+    a.n_cells    = op->n_cells;
+    a.old_grad   = (T *)op->d_old_grad;
+    a.vec        = (const T *)vec;
+    a.h_q        = (const T *)op->d_hq;
+    a.h_min      = (const T *)op->d_hmin;
+    a.nu         = (T)op->prm.nu;
+    a.c1         = (T)op->prm.c1;
+    a.c2         = (T)op->prm.c2;
+    a.stau       = (T)(op->prm.dt == 0.0 ? 0.0 : 1.0 / op->prm.dt);
+    a.what       = what;
+    a.sh         = make_shape<T, n>(op->basis);
+    constexpr int CPB = BLOCK / nq;
+    const dim3    grid((unsigned)((op->n_cells + CPB - 1) / CPB));
+    hipLaunchKernelGGL((k_produce<dim, k, T>), grid, dim3(BLOCK), 0, s, a);
+    HIP_THROW(hipGetLastError());
+  }
+};
+
+using ApplyFn   = void (*)(const glsOp_ *, int, bool, void *, const void *, int64_t, int64_t,
+                         hipStream_t);
+using ProduceFn = void (*)(const glsOp_ *, int, const void *, hipStream_t);
+
+template <typename T>
+void
+select_t(int dim, int k, ApplyFn &af, ProduceFn &pf)
+{
+  af = nullptr;
+  pf = nullptr;
+#define GLS_CASE(D, K)                  \
+  if (dim == D && k == K)               \
+    {                                   \
+      af = &Impl<D, K, T>::apply;       \
+      pf = &Impl<D, K, T>::produce;     \
+    }
+  GLS_CASE(2, 1)
+  GLS_CASE(2, 2)
+  GLS_CASE(2, 3)
+  GLS_CASE(3, 1)
+  GLS_CASE(3, 2)
+  GLS_CASE(3, 3)
+#undef GLS_CASE
+}
+
+void
+select(const glsOp_ *op, ApplyFn &af, ProduceFn &pf)
+{
+  if (op->prec == GLS_F64)
+    select_t<double>(op->dim, op->degree, af, pf);
+  else
+    select_t<float>(op->dim, op->degree, af, pf);
+  if (!af)
+    throw std::runtime_error("no kernel instantiation for this (dim, degree)");
+}
+
+int
+vmult_mode(const glsOp_ *op)
+{
+  return (op->prm.flags & GLS_INCREMENT_FORM) ? MODE_NEWTON : MODE_FIXED;
+}
+
+dim3
+grid1d(int64_t n)
+{
+  return dim3((unsigned)((n + 255) / 256));
+}
+
+template <typename T>
+void
+launch_init(const glsOp_ *op, void *dst, const void *src, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_init_dst<T>, grid1d(op->n_dofs), dim3(256), 0, s, (T *)dst,
+                     (const T *)src, op->d_cbits, op->n_owned_dofs, op->n_dofs);
+  HIP_THROW(hipGetLastError());
+}
+
+void
+init_dst(const glsOp_ *op, void *dst, const void *src, hipStream_t s)
+{
+  if (op->prec == GLS_F64)
+    launch_init<double>(op, dst, src, s);
+  else
+    launch_init<float>(op, dst, src, s);
+}
+
+} // namespace
+
+// ------------------------------------------------------------ C-ABI
+extern "C" {
+
+const char *
+gls_last_error(void)
+{
+  return gls::g_err.c_str();
+}
+
+glsStatus
+gls_op_create(const glsOpDesc *d, glsOp *out)
+{
+  GLS_TRY
+  if (!d || !out)
+    throw std::runtime_error("gls_op_create: null argument");
+  if ((d->dim != 2 && d->dim != 3) || d->degree < 1 || d->degree > 3 ||
+      (d->precision != GLS_F64 && d->precision != GLS_F32) || d->n_cells < 0 || d->n_nodes < 0 ||
+      d->n_owned_nodes < 0 || d->n_owned_nodes > d->n_nodes || !d->cell_nodes ||
+      !d->node_coords || !d->node_cmask || !d->cell_measure || !d->cell_hmin)
+    throw std::runtime_error("gls_op_create: invalid descriptor");
+  if (d->n_nodes >= (int64_t)NODE_MASK)
+    throw std::runtime_error("gls_op_create: too many local nodes for 28-bit node indices");
+  auto *op          = new glsOp_();
+  op->dim           = d->dim;
+  op->degree        = d->degree;
+  op->prec          = d->precision;
+  op->n_cells       = d->n_cells;
+  op->n_nodes       = d->n_nodes;
+  op->n_owned_nodes = d->n_owned_nodes;
+  op->n_dofs        = d->n_nodes * (d->dim + 1);
+  op->n_owned_dofs  = d->n_owned_nodes * (d->dim + 1);
+  op->basis         = Basis1D(d->degree);
+  const int dim = d->dim, n = d->degree + 1;
+  op->nq            = dim == 3 ? n * n * n : n * n;
+  op->nf            = 2 + 3 * dim + dim * dim;
+  HIP_THROW(hipGetDevice(&op->device));
+  const int nq = op->nq;
+
+  // packed node indices with constrained-component bits (read_dof_values /
+  // distribute_local_to_global resolve homogeneous Dirichlet constraints)
+  std::vector<uint32_t> nodes((size_t)d->n_cells * nq);
+  for (size_t i = 0; i < nodes.size(); ++i)
+    {
+      const uint32_t nd = d->cell_nodes[i];
+      if ((int64_t)nd >= d->n_nodes)
+        throw std::runtime_error("gls_op_create: node index out of range");
+      nodes[i] = nd | ((uint32_t)(d->node_cmask[nd] & 0xF) << 28);
+    }
+  upload((void **)&op->d_nodes, nodes);
+
+  // constrained dof bitmask on the owned range (identity rows)
+  std::vector<uint32_t> cbits((size_t)(op->n_owned_dofs + 31) / 32 + 1, 0u);
+  for (int64_t nd = 0; nd < d->n_owned_nodes; ++nd)
+    for (int c = 0; c <= dim; ++c)
+      if ((d->node_cmask[nd] >> c) & 1)
+        {
+          const int64_t i = nd * (dim + 1) + c;
+          cbits[i >> 5] |= 1u << (i & 31);
+        }
+  upload((void **)&op->d_cbits, cbits);
+
+  // MatrixFree-style geometry: Cartesian cells (constant diagonal J) store
+  // dim+1 numbers, all others JxW + J^{-1} per quadrature point
+  std::vector<uint32_t> cell_geo((size_t)d->n_cells);
+  std::vector<double>   cart, gen; // [field][index] filled below
+  std::vector<double>   cart_rows, gen_rows;
+  std::vector<double>   X((size_t)nq * dim), J;
+  int64_t               n_cart = 0, n_gen = 0;
+  for (int64_t c = 0; c < d->n_cells; ++c)
+    {
+      for (int i = 0; i < nq; ++i)
+        for (int e = 0; e < dim; ++e)
+          X[i * dim + e] = d->node_coords[(size_t)d->cell_nodes[c * nq + i] * dim + e];
+      cell_jacobians(dim, op->basis, X.data(), J);
+      double scale = 0;
+      for (int e = 0; e < dim; ++e)
+        scale = std::max(scale, std::abs(J[e * dim + e]));
+      bool cartesian = true;
+      for (int q = 0; q < nq && cartesian; ++q)
+        for (int i = 0; i < dim * dim; ++i)
+          {
+            const double v  = J[q * dim * dim + i];
+            const bool   dg = (i / dim) == (i % dim);
+            if ((!dg && std::abs(v) > 1e-12 * scale) ||
+                std::abs(v - J[i]) > 1e-12 * scale)
+              {
+                cartesian = false;
+                break;
+              }
+          }
+      if (cartesian)
+        {
+          cell_geo[c] = (uint32_t)n_cart++;
+          double det  = 1;
+          for (int e = 0; e < dim; ++e)
+            {
+              cart_rows.push_back(1.0 / J[e * dim + e]);
+              det *= J[e * dim + e];
+            }
+          cart_rows.push_back(det);
+        }
+      else
+        {
+          cell_geo[c] = GEO_GENERAL | (uint32_t)n_gen++;
+          for (int q = 0; q < nq; ++q)
+            {
+              double inv[9], det;
+              invert(dim, &J[(size_t)q * dim * dim], inv, det);
+              const int qa[3] = {q % n, (q / n) % n, dim == 3 ? q / (n * n) : 0};
+              double    w     = 1;
+              for (int a = 0; a < dim; ++a)
+                w *= op->basis.qw[qa[a]];
+              gen_rows.push_back(det * w);
+              for (int i = 0; i < dim * dim; ++i)
+                gen_rows.push_back(inv[i]);
+            }
+        }
+    }
+  op->n_cart = n_cart;
+  op->n_gen  = n_gen;
+  // transpose rows -> SoA [field][index]
+  const int ncf = dim + 1, ngf = 1 + dim * dim;
+  cart.resize((size_t)ncf * n_cart);
+  for (int64_t i = 0; i < n_cart; ++i)
+    for (int f = 0; f < ncf; ++f)
+      cart[(size_t)f * n_cart + i] = cart_rows[(size_t)i * ncf + f];
+  gen.resize((size_t)ngf * n_gen * nq);
+  for (int64_t i = 0; i < n_gen * nq; ++i)
+    for (int f = 0; f < ngf; ++f)
+      gen[(size_t)f * n_gen * nq + i] = gen_rows[(size_t)i * ngf + f];
+  upload((void **)&op->d_cell_geo, cell_geo);
+
+  std::vector<double> hq((size_t)d->n_cells), hmin((size_t)d->n_cells);
+  for (int64_t c = 0; c < d->n_cells; ++c)
+    {
+      const double hk = d->cell_measure[c];
+      hq[c]   = dim == 2 ? std::sqrt(4. * hk / M_PI) / d->degree :
+                           std::pow(6 * hk / M_PI, 1. / 3.) / d->degree;
+      hmin[c] = d->cell_hmin[c];
+    }
+  if (op->prec == GLS_F64)
+    {
+      upload(&op->d_geo_cart, cart);
+      upload(&op->d_geo_gen, gen);
+      upload(&op->d_hq, hq);
+      upload(&op->d_hmin, hmin);
+    }
+  else
+    {
+      upload(&op->d_geo_cart, convert<float>(cart));
+      upload(&op->d_geo_gen, convert<float>(gen));
+      upload(&op->d_hq, convert<float>(hq));
+      upload(&op->d_hmin, convert<float>(hmin));
+    }
+  const size_t ts = op->tsize();
+  HIP_THROW(hipMalloc(&op->d_tab, std::max<size_t>(1, (size_t)op->nf * d->n_cells * nq * ts)));
+  HIP_THROW(hipMemset(op->d_tab, 0, std::max<size_t>(1, (size_t)op->nf * d->n_cells * nq * ts)));
+  HIP_THROW(hipMalloc(&op->d_cellwise, std::max<size_t>(1, 2 * (size_t)d->n_cells * ts)));
+  HIP_THROW(hipMemset(op->d_cellwise, 0, std::max<size_t>(1, 2 * (size_t)d->n_cells * ts)));
+  HIP_THROW(hipMalloc(&op->d_tmp, std::max<size_t>(1, (size_t)op->n_dofs * ts)));
+  op->prm.nu    = 1.0;
+  op->prm.theta = 1.0;
+  op->prm.dt    = 1.0;
+  *out          = op;
+  GLS_CATCH
+}
+
+void
+gls_op_destroy(glsOp op)
+{
+  if (!op)
+    return;
+  void *bufs[] = {op->d_nodes, op->d_cell_geo, op->d_geo_cart, op->d_geo_gen, op->d_tab,
+                  op->d_cellwise, op->d_old_grad, op->d_hq, op->d_hmin, op->d_tmp, op->d_cbits};
+  for (void *b : bufs)
+    if (b)
+      (void)hipFree(b);
+  delete op;
+}
+
+glsStatus
+gls_op_set_parameters(glsOp op, const glsOpParams *prm)
+{
+  GLS_TRY
+  if (!op || !prm)
+    throw std::runtime_error("gls_op_set_parameters: null argument");
+  // operator_ns.cc:126-129: theta == 1 required with a stabilised time derivative
+  const bool td = (prm->flags & GLS_CONSIDER_TIME_DERIVATIVE) && prm->order > 0;
+  if (td && prm->theta != 1.0)
+    throw std::runtime_error("consider_time_derivative requires theta == 1 "
+                             "(operator_ns.cc:126-129)");
+  op->prm = *prm;
+  GLS_CATCH
+}
+
+int64_t
+gls_op_m(glsOp op)
+{
+  return op ? op->n_dofs : 0;
+}
+
+int
+gls_op_precision(glsOp op)
+{
+  return op ? op->prec : -1;
+}
+
+glsStatus
+gls_op_set_linearization_point(glsOp op, const void *vec, void *stream)
+{
+  GLS_TRY
+  if (!op || !vec)
+    throw std::runtime_error("gls_op_set_linearization_point: null argument");
+  ApplyFn   af;
+  ProduceFn pf;
+  select(op, af, pf);
+  pf(op, 0, vec, (hipStream_t)stream);
+  op->have_lin = true;
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_set_previous_solution(glsOp op, const void *const *hist, int n_hist,
+                             const double *weights, void *stream)
+{
+  GLS_TRY
+  if (!op)
+    throw std::runtime_error("gls_op_set_previous_solution: null operator");
+  const int order = op->prm.order;
+  if (order == 0)
+    return 0; // operator_ns.cc:243-244
+  if (!hist || !weights || n_hist < order + 1 || order > 3)
+    throw std::runtime_error("gls_op_set_previous_solution: need order+1 history vectors");
+  ApplyFn     af;
+  ProduceFn   pf;
+  hipStream_t s = (hipStream_t)stream;
+  select(op, af, pf);
+  const void *x[4] = {nullptr, nullptr, nullptr, nullptr};
+  double      w[4] = {0, 0, 0, 0};
+  for (int i = 1; i <= order; ++i)
+    {
+      x[i - 1] = hist[i];
+      w[i - 1] = weights[i];
+    }
+  if (op->prec == GLS_F64)
+    hipLaunchKernelGGL(k_lincomb<double>, grid1d(op->n_dofs), dim3(256), 0, s,
+                       (double *)op->d_tmp, (const double *)x[0], (const double *)x[1],
+                       (const double *)x[2], (const double *)x[3], w[0], w[1], w[2], w[3],
+                       op->n_dofs);
+  else
+    hipLaunchKernelGGL(k_lincomb<float>, grid1d(op->n_dofs), dim3(256), 0, s,
+                       (float *)op->d_tmp, (const float *)x[0], (const float *)x[1],
+                       (const float *)x[2], (const float *)x[3], w[0], w[1], w[2], w[3],
+                       op->n_dofs);
+  HIP_THROW(hipGetLastError());
+  pf(op, 1, op->d_tmp, s);
+  op->have_prev = true;
+  if (op->prm.theta != 1.0)
+    {
+      if (!op->d_old_grad)
+        {
+          const size_t sz = (size_t)(op->dim * op->dim + op->dim) * op->n_cells * op->nq * op->tsize();
+          HIP_THROW(hipMalloc(&op->d_old_grad, std::max<size_t>(1, sz)));
+        }
+      pf(op, 2, hist[1], s);
+      op->have_old_grad = true;
+    }
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_vmult_init(glsOp op, void *dst, const void *src, void *stream)
+{
+  GLS_TRY
+  if (!op || !dst || !src)
+    throw std::runtime_error("gls_op_vmult_init: null argument");
+  init_dst(op, dst, src, (hipStream_t)stream);
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_vmult_cells(glsOp op, void *dst, const void *src, int64_t b, int64_t e, void *stream)
+{
+  GLS_TRY
+  if (!op || !dst || !src)
+    throw std::runtime_error("gls_op_vmult_cells: null argument");
+  if (!op->have_lin)
+    throw std::runtime_error("vmult before set_linearization_point");
+  if (b < 0 || e > op->n_cells || b > e)
+    throw std::runtime_error("gls_op_vmult_cells: bad cell range");
+  ApplyFn   af;
+  ProduceFn pf;
+  select(op, af, pf);
+  af(op, vmult_mode(op), false, dst, src, b, e, (hipStream_t)stream);
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_vmult(glsOp op, void *dst, const void *src, void *stream)
+{
+  GLS_TRY
+  if (!op || !dst || !src)
+    throw std::runtime_error("gls_op_vmult: null argument");
+  if (dst == src)
+    throw std::runtime_error("gls_op_vmult: dst and src must not alias");
+  if (!op->have_lin)
+    throw std::runtime_error("vmult before set_linearization_point");
+  ApplyFn   af;
+  ProduceFn pf;
+  select(op, af, pf);
+  hipStream_t s = (hipStream_t)stream;
+  init_dst(op, dst, src, s);
+  af(op, vmult_mode(op), false, dst, src, 0, op->n_cells, s);
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_evaluate_residual(glsOp op, void *dst, const void *src, void *stream)
+{
+  GLS_TRY
+  if (!op || !dst || !src || dst == src)
+    throw std::runtime_error("gls_op_evaluate_residual: bad arguments");
+  if (!op->have_lin)
+    throw std::runtime_error("evaluate_residual before set_linearization_point");
+  ApplyFn   af;
+  ProduceFn pf;
+  select(op, af, pf);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_THROW(hipMemsetAsync(dst, 0, (size_t)op->n_dofs * op->tsize(), s));
+  af(op, MODE_RESIDUAL, false, dst, src, 0, op->n_cells, s);
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_compute_inverse_diagonal(glsOp op, void *diag, void *stream)
+{
+  GLS_TRY
+  if (!op || !diag)
+    throw std::runtime_error("gls_op_compute_inverse_diagonal: null argument");
+  if (!op->have_lin)
+    throw std::runtime_error("compute_inverse_diagonal before set_linearization_point");
+  ApplyFn   af;
+  ProduceFn pf;
+  select(op, af, pf);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_THROW(hipMemsetAsync(diag, 0, (size_t)op->n_dofs * op->tsize(), s));
+  af(op, vmult_mode(op), true, diag, diag, 0, op->n_cells, s);
+  if (op->prec == GLS_F64)
+    hipLaunchKernelGGL(k_invert_diag<double>, grid1d(op->n_dofs), dim3(256), 0, s,
+                       (double *)diag, op->d_cbits, op->n_owned_dofs, op->n_dofs);
+  else
+    hipLaunchKernelGGL(k_invert_diag<float>, grid1d(op->n_dofs), dim3(256), 0, s, (float *)diag,
+                       op->d_cbits, op->n_owned_dofs, op->n_dofs);
+  HIP_THROW(hipGetLastError());
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_upload_tables(glsOp op, const double *tables, const double *cellwise)
+{
+  GLS_TRY
+  if (!op || !tables)
+    throw std::runtime_error("gls_op_upload_tables: null argument");
+  const int64_t       m = op->n_cells * op->nq;
+  std::vector<double> soa((size_t)op->nf * m);
+  for (int64_t i = 0; i < m; ++i)
+    for (int f = 0; f < op->nf; ++f)
+      soa[(size_t)f * m + i] = tables[(size_t)i * op->nf + f];
+  std::vector<double> cw((size_t)2 * op->n_cells, 0.0);
+  if (cellwise)
+    for (int64_t c = 0; c < op->n_cells; ++c)
+      {
+        cw[c]               = cellwise[2 * c];
+        cw[op->n_cells + c] = cellwise[2 * c + 1];
+      }
+  if (op->prec == GLS_F64)
+    {
+      HIP_THROW(hipMemcpy(op->d_tab, soa.data(), soa.size() * 8, hipMemcpyHostToDevice));
+      HIP_THROW(hipMemcpy(op->d_cellwise, cw.data(), cw.size() * 8, hipMemcpyHostToDevice));
+    }
+  else
+    {
+      auto sf = convert<float>(soa);
+      auto cf = convert<float>(cw);
+      HIP_THROW(hipMemcpy(op->d_tab, sf.data(), sf.size() * 4, hipMemcpyHostToDevice));
+      HIP_THROW(hipMemcpy(op->d_cellwise, cf.data(), cf.size() * 4, hipMemcpyHostToDevice));
+    }
+  op->have_lin  = true;
+  op->have_prev = op->prm.order > 0;
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_download_tables(glsOp op, double *tables, double *cellwise)
+{
+  GLS_TRY
+  if (!op)
+    throw std::runtime_error("gls_op_download_tables: null argument");
+  HIP_THROW(hipDeviceSynchronize());
+  const int64_t       m = op->n_cells * op->nq;
+  std::vector<double> soa((size_t)op->nf * m), cw((size_t)2 * op->n_cells);
+  if (op->prec == GLS_F64)
+    {
+      HIP_THROW(hipMemcpy(soa.data(), op->d_tab, soa.size() * 8, hipMemcpyDeviceToHost));
+      HIP_THROW(hipMemcpy(cw.data(), op->d_cellwise, cw.size() * 8, hipMemcpyDeviceToHost));
+    }
+  else
+    {
+      std::vector<float> sf(soa.size()), cf(cw.size());
+      HIP_THROW(hipMemcpy(sf.data(), op->d_tab, sf.size() * 4, hipMemcpyDeviceToHost));
+      HIP_THROW(hipMemcpy(cf.data(), op->d_cellwise, cf.size() * 4, hipMemcpyDeviceToHost));
+      soa.assign(sf.begin(), sf.end());
+      cw.assign(cf.begin(), cf.end());
+    }
+  if (tables)
+    for (int64_t i = 0; i < m; ++i)
+      for (int f = 0; f < op->nf; ++f)
+        tables[(size_t)i * op->nf + f] = soa[(size_t)f * m + i];
+  if (cellwise)
+    for (int64_t c = 0; c < op->n_cells; ++c)
+      {
+        cellwise[2 * c]     = cw[c];
+        cellwise[2 * c + 1] = cw[op->n_cells + c];
+      }
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_geometry_counts(glsOp op, int64_t *n_general, int64_t *n_cartesian)
+{
+  GLS_TRY
+  if (!op)
+    throw std::runtime_error("gls_op_geometry_counts: null argument");
+  if (n_general)
+    *n_general = op->n_gen;
+  if (n_cartesian)
+    *n_cartesian = op->n_cart;
+  GLS_CATCH
+}
+
+double
+gls_op_vmult_bytes(glsOp op)
+{
+  if (!op)
+    return 0;
+  // B_tab = s 2N + s C nq n_tab + s [n_gen nq (dim^2+1) +
+  //                     n_cart (dim+1)] + 4 C nq
+  const double s   = (double)op->tsize();
+  const int    dim = op->dim;
+  const bool   td  = (op->prm.flags & GLS_CONSIDER_TIME_DERIVATIVE) && op->prm.order > 0;
+  int          n_tab;
+  if (op->prm.flags & GLS_INCREMENT_FORM)
+    n_tab = 2 + dim + dim * dim + dim + (td ? dim : 0);
+  else
+    n_tab = 2 + dim;
+  if (op->prm.flags & GLS_CELL_WISE_STAB)
+    n_tab -= 2;
+  const double C = (double)op->n_cells, nq = (double)op->nq;
+  double b = s * 2.0 * (double)op->n_dofs + s * C * nq * n_tab +
+             s * ((double)op->n_gen * nq * (dim * dim + 1) + (double)op->n_cart * (dim + 1)) +
+             4.0 * C * nq;
+  if (op->prm.flags & GLS_CELL_WISE_STAB)
+    b += s * 2.0 * C;
+  return b;
+}
+
+} // extern "C"

@@ -1,0 +1,801 @@
+// kernels.h — HIP/CDNA4 (gfx950) kernels of the matrix-free GLS
+// Navier–Stokes operator.  Included by gls_op.hip only.
+//
+// Thread mapping: one thread per (cell, quadrature point); since FE_Q(k) has
+// (k+1)^dim nodes and QGauss(k+1) has (k+1)^dim points, the same thread also
+// owns the cell's node with the same lexicographic index.  A 256-thread
+// workgroup holds CPB = 256 / (k+1)^dim cells (3D Q2: 9 cells, 243 lanes).
+// Sum factorisation (deal.II's FEEvaluation::evaluate/integrate, called at
+// operator_ns.cc:962-963,1064-1065,1074-1075,1179-1180) runs as 1D
+// contractions through LDS: values by S (shape values at Gauss points),
+// gradients by the collocation derivative Dq at the Gauss points, integrate
+// by the transposes.  The q-point physics is do_vmult_cell,
+// operator_ns.cc:949-1182 (Newton branch :1067-1181, fixed-point/residual
+// branch :955-1066).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gls
+{
+constexpr uint32_t NODE_MASK  = 0x0FFFFFFFu;
+constexpr int      BLOCK      = 256;
+constexpr uint32_t GEO_GENERAL = 0x80000000u;
+
+constexpr int
+ipow(int n, int d)
+{
+  return d == 0 ? 1 : n * ipow(n, d - 1);
+}
+
+enum Mode
+{
+  MODE_NEWTON   = 0, // vmult, increment form (Newton Jacobian)
+  MODE_FIXED    = 1, // vmult, fixed-point form (!increment_form)
+  MODE_RESIDUAL = 2  // evaluate_residual (read plain, negate)
+};
+
+// table field offsets (SoA, [field][cell * nq + q])
+template <int dim>
+struct Fields
+{
+  static constexpr int D1 = 0, D2 = 1, U = 2, GU = 2 + dim, GP = 2 + dim + dim * dim,
+                       UT = 2 + 2 * dim + dim * dim, N = 2 + 3 * dim + dim * dim;
+};
+
+template <typename T, int n>
+struct Shape
+{
+  T S[n][n];  // S[q][i]  = phi_i(x_q)          (nodal basis at Gauss points)
+  T Dq[n][n]; // Dq[q][j] = l_j'(x_q)           (collocation derivative)
+  T w[n];     // 1D Gauss weights on [0,1]
+};
+
+template <typename T, int dim, int n>
+struct ApplyArgs
+{
+  const uint32_t *nodes;    // [cells][nq] node | cmask << 28
+  const uint32_t *cell_geo; // GEO_GENERAL | index, or cartesian index
+  const T        *geo_cart; // [dim + 1][n_cart]: invJ diagonal, det J
+  int64_t         n_cart;
+  const T        *geo_gen;  // [1 + dim*dim][n_gen * nq]: JxW, invJ[a][e]
+  int64_t         gen_stride;
+  const T        *tab;      // [Fields::N][n_cells * nq]
+  int64_t         tab_stride;
+  const T        *cellwise; // [2][n_cells]
+  int64_t         n_cells;
+  const T        *old_grad; // [dim*dim + dim][n_cells * nq]
+  T              *dst;
+  const T        *src;
+  int64_t         cell_begin, cell_end;
+  T               nu, w0, theta;
+  int             td, cw, have_prev, have_old_grad;
+  int             diag_ndof;
+  Shape<T, n>     sh;
+};
+
+// ------------------------------------------------------------ helpers
+template <typename T, int nc>
+__device__ __forceinline__ void
+load_node(const T *__restrict__ v, uint32_t node, T (&u)[nc])
+{
+#pragma unroll
+  for (int c = 0; c < nc; ++c)
+    u[c] = v[(size_t)node * nc + c];
+}
+
+template <>
+__device__ __forceinline__ void
+load_node<double, 4>(const double *__restrict__ v, uint32_t node, double (&u)[4])
+{
+  const double2 *p = reinterpret_cast<const double2 *>(v + (size_t)node * 4);
+  const double2  a = p[0], b = p[1];
+  u[0] = a.x, u[1] = a.y, u[2] = b.x, u[3] = b.y;
+}
+
+template <>
+__device__ __forceinline__ void
+load_node<float, 4>(const float *__restrict__ v, uint32_t node, float (&u)[4])
+{
+  const float4 a = *reinterpret_cast<const float4 *>(v + (size_t)node * 4);
+  u[0] = a.x, u[1] = a.y, u[2] = a.z, u[3] = a.w;
+}
+
+// 1D contraction along an axis with stride `s` (n points):
+//   forward:   out[p] = sum_j M[pa][j] in[base + j s]
+//   transpose: out[p] = sum_j M[j][pa] in[base + j s]
+template <int n, bool TR, typename T>
+__device__ __forceinline__ T
+contract(const T *in, const T (*M)[n], int pa, int base, int s)
+{
+  T acc = 0;
+#pragma unroll
+  for (int j = 0; j < n; ++j)
+    acc += (TR ? M[j][pa] : M[pa][j]) * in[base + j * s];
+  return acc;
+}
+
+// ------------------------------------------------------------ q-point physics
+// do_vmult_cell, operator_ns.cc:949-1182; u/p/gu/gp are trial values and
+// REAL-space gradients at the q point; output value / gradient coefficients
+// (before JxW and J^{-T}).
+template <int dim, typename T, int MODE>
+__device__ __forceinline__ void
+qpoint_physics(const T *u, T p, const T (*gu)[dim],
+               const T *gp, const T *U, const T (*GU)[dim], const T *GP, const T *UT,
+               const T *oldg, T d1, T d2, T nu, T w0, T theta, int td, int have_prev,
+               int have_old_grad, T *vr, T (*gr)[dim])
+{
+#pragma unroll
+  for (int c = 0; c <= dim; ++c)
+    {
+      vr[c] = 0;
+#pragma unroll
+      for (int e = 0; e < dim; ++e)
+        gr[c][e] = 0;
+    }
+  if (MODE == MODE_NEWTON)
+    {
+      // Newton increment branch, operator_ns.cc:1067-1181
+      T ut[dim], sgu[dim], ugs[dim], sgs[dim], divu = 0;
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        {
+          ut[d] = u[d] * w0;
+          divu += gu[d][d];
+          sgu[d] = ugs[d] = sgs[d] = 0;
+#pragma unroll
+          for (int e = 0; e < dim; ++e)
+            {
+              sgu[d] += gu[d][e] * U[e];
+              ugs[d] += GU[d][e] * u[e];
+              sgs[d] += GU[d][e] * U[e];
+            }
+        }
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        {
+          vr[d] = ut[d] + sgu[d] + ugs[d];
+          gr[d][d] += gu[d][d] * (T(2) * nu) - p;
+        }
+#pragma unroll
+      for (int e = 0; e < dim; ++e)
+#pragma unroll
+        for (int d = e + 1; d < dim; ++d)
+          {
+            const T tmp = (gu[d][e] + gu[e][d]) * nu;
+            gr[d][e] += tmp;
+            gr[e][d] += tmp;
+          }
+      T r0[dim], r1[dim];
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        {
+          r0[d] = d1 * ((td ? ut[d] : T(0)) + gp[d] + sgu[d] + ugs[d]);
+          r1[d] = d1 * ((td ? (U[d] * w0 + UT[d]) : T(0)) + GP[d] + sgs[d]);
+        }
+#pragma unroll
+      for (int d0 = 0; d0 < dim; ++d0)
+#pragma unroll
+        for (int e = 0; e < dim; ++e)
+          gr[d0][e] += U[e] * r0[d0] + u[e] * r1[d0];
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        gr[d][d] += d2 * divu;
+      vr[dim] = divu;
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        gr[dim][d] = r0[d];
+    }
+  else
+    {
+      // fixed-point / residual branch, operator_ns.cc:955-1066
+      const bool R = MODE == MODE_RESIDUAL;
+      T          ut[dim], gb[dim][dim], gpb[dim];
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        {
+          ut[d]  = u[d] * w0 + ((R && have_prev) ? UT[d] : T(0));
+          gpb[d] = theta * gp[d];
+#pragma unroll
+          for (int e = 0; e < dim; ++e)
+            gb[d][e] = theta * gu[d][e];
+        }
+      if (R && have_old_grad)
+        {
+#pragma unroll
+          for (int d = 0; d < dim; ++d)
+            {
+#pragma unroll
+              for (int e = 0; e < dim; ++e)
+                gb[d][e] += (T(1) - theta) * oldg[d * dim + e];
+              gpb[d] += (T(1) - theta) * oldg[dim * dim + d];
+            }
+        }
+      T divb = 0, sgb[dim];
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        {
+          divb += gb[d][d];
+          sgb[d] = 0;
+#pragma unroll
+          for (int e = 0; e < dim; ++e)
+            sgb[d] += gb[d][e] * U[e];
+        }
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        {
+          vr[d] = ut[d] + sgb[d];
+          gr[d][d] += gb[d][d] * (T(2) * nu) - p;
+        }
+#pragma unroll
+      for (int e = 0; e < dim; ++e)
+#pragma unroll
+        for (int d = e + 1; d < dim; ++d)
+          {
+            const T tmp = (gb[d][e] + gb[e][d]) * nu;
+            gr[d][e] += tmp;
+            gr[e][d] += tmp;
+          }
+      T r0[dim];
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        r0[d] = d1 * ((td ? ut[d] : T(0)) + gpb[d] + sgb[d]);
+#pragma unroll
+      for (int d0 = 0; d0 < dim; ++d0)
+#pragma unroll
+        for (int e = 0; e < dim; ++e)
+          gr[d0][e] += U[e] * r0[d0];
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        gr[d][d] += d2 * divb;
+      vr[dim] = divb;
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        gr[dim][d] = d1 * ((td ? ut[d] : T(0)) + gp[d] + sgb[d]);
+    }
+}
+
+// ------------------------------------------------------------ geometry
+template <int dim, int n, typename T>
+struct QGeo
+{
+  T JxW;
+  T inv[dim][dim]; // d xi_a / d x_e
+};
+
+template <int dim, int n, typename T, typename Args>
+__device__ __forceinline__ void
+load_geometry(const Args &a, int64_t cell, int p, int px, int py, int pz,
+              const T *sw, QGeo<dim, n, T> &g)
+{
+  constexpr int  nq = ipow(n, dim);
+  const uint32_t cg = a.cell_geo[cell];
+  if (cg & GEO_GENERAL)
+    {
+      const int64_t idx = (int64_t)(cg & ~GEO_GENERAL) * nq + p;
+      g.JxW             = a.geo_gen[idx];
+#pragma unroll
+      for (int i = 0; i < dim; ++i)
+#pragma unroll
+        for (int e = 0; e < dim; ++e)
+          g.inv[i][e] = a.geo_gen[(1 + i * dim + e) * a.gen_stride + idx];
+    }
+  else
+    {
+      const int64_t idx = cg;
+#pragma unroll
+      for (int i = 0; i < dim; ++i)
+#pragma unroll
+        for (int e = 0; e < dim; ++e)
+          g.inv[i][e] = (i == e) ? a.geo_cart[i * a.n_cart + idx] : T(0);
+      T w = sw[px] * sw[py];
+      if (dim == 3)
+        w *= sw[pz];
+      g.JxW = a.geo_cart[dim * a.n_cart + idx] * w;
+    }
+}
+
+// ------------------------------------------------------------ apply kernel
+// MODE: Newton / fixed-point vmult or residual.  DIAG: each virtual cell is
+// (cell, local dof j) with a unit-vector input; only the diagonal entry is
+// accumulated (MatrixFreeTools::compute_diagonal, operator_ns.cc:209-218).
+template <int dim, int k, typename T, int MODE, bool DIAG>
+__global__ void __launch_bounds__(BLOCK)
+  k_apply(ApplyArgs<T, dim, k + 1> a)
+{
+  constexpr int n    = k + 1;
+  constexpr int nq   = ipow(n, dim);
+  constexpr int nc   = dim + 1;
+  constexpr int CPB  = BLOCK / nq;
+  constexpr int LDSC = nc * nq * (dim > 2 ? dim : 2);
+  using F            = Fields<dim>;
+
+  __shared__ T smem[CPB * LDSC];
+  __shared__ T sS[n][n], sD[n][n], sw[n];
+
+  const int t = threadIdx.x;
+  if (t < n * n)
+    {
+      sS[t / n][t % n] = a.sh.S[t / n][t % n];
+      sD[t / n][t % n] = a.sh.Dq[t / n][t % n];
+    }
+  if (t < n)
+    sw[t] = a.sh.w[t];
+
+  const int     lc       = t / nq;
+  const int     p        = t - lc * nq;
+  const bool    in_block = lc < CPB;
+  const int64_t vcell    = (int64_t)blockIdx.x * CPB + lc;
+  int64_t       cell;
+  int           jdiag = 0;
+  if (DIAG)
+    {
+      cell  = a.cell_begin + vcell / a.diag_ndof;
+      jdiag = (int)(vcell % a.diag_ndof);
+    }
+  else
+    cell = a.cell_begin + vcell;
+  const bool active = in_block && cell < a.cell_end;
+  T         *A      = smem + (in_block ? lc : 0) * LDSC;
+  T         *B      = A + nc * nq;
+  const int  px     = p % n;
+  const int  py     = (p / n) % n;
+  const int  pz     = dim == 3 ? p / (n * n) : 0;
+  const int  pa[3]  = {px, py, pz};
+  const int  st[3]  = {1, n, n * n};
+
+  // ---- gather (read_dof_values / read_dof_values_plain)
+  uint32_t node = 0, cm = 0;
+  T        u[nc];
+  if (active)
+    {
+      const uint32_t packed = a.nodes[cell * nq + p];
+      node                  = packed & NODE_MASK;
+      cm                    = packed >> 28;
+    }
+  if (DIAG)
+    {
+#pragma unroll
+      for (int c = 0; c < nc; ++c)
+        u[c] = (active && p == jdiag / nc && c == jdiag % nc) ? T(1) : T(0);
+    }
+  else if (active)
+    {
+      load_node<T, nc>(a.src, node, u);
+      if (MODE != MODE_RESIDUAL)
+#pragma unroll
+        for (int c = 0; c < nc; ++c)
+          if ((cm >> c) & 1)
+            u[c] = 0;
+    }
+  else
+    {
+#pragma unroll
+      for (int c = 0; c < nc; ++c)
+        u[c] = 0;
+    }
+  if (in_block)
+#pragma unroll
+    for (int c = 0; c < nc; ++c)
+      A[c * nq + p] = u[c];
+  __syncthreads();
+
+  // ---- evaluate: values at q (dim sweeps with S)
+  T *in = A, *out = B;
+#pragma unroll
+  for (int ax = 0; ax < dim; ++ax)
+    {
+      if (in_block)
+#pragma unroll
+        for (int c = 0; c < nc; ++c)
+          out[c * nq + p] =
+            contract<n, false>(in + c * nq, sS, pa[ax], p - pa[ax] * st[ax], st[ax]);
+      __syncthreads();
+      T *tmp = in;
+      in     = out;
+      out    = tmp;
+    }
+  // `in` holds the values at the quadrature points
+  T val[nc], gref[nc][dim];
+  if (in_block)
+#pragma unroll
+    for (int c = 0; c < nc; ++c)
+      {
+        val[c] = in[c * nq + p];
+#pragma unroll
+        for (int ax = 0; ax < dim; ++ax)
+          gref[c][ax] = contract<n, false>(in + c * nq, sD, pa[ax], p - pa[ax] * st[ax], st[ax]);
+      }
+  __syncthreads();
+
+  // ---- q-point physics
+  T vhat[nc], ghat[nc][dim];
+#pragma unroll
+  for (int c = 0; c < nc; ++c)
+    {
+      vhat[c] = 0;
+#pragma unroll
+      for (int ax = 0; ax < dim; ++ax)
+        ghat[c][ax] = 0;
+    }
+  if (active)
+    {
+      QGeo<dim, n, T> g;
+      load_geometry<dim, n, T>(a, cell, p, px, py, pz, sw, g);
+      T gu[dim][dim], gp[dim];
+#pragma unroll
+      for (int c = 0; c < nc; ++c)
+#pragma unroll
+        for (int e = 0; e < dim; ++e)
+          {
+            T s = 0;
+#pragma unroll
+            for (int i = 0; i < dim; ++i)
+              s += g.inv[i][e] * gref[c][i];
+            if (c < dim)
+              gu[c][e] = s;
+            else
+              gp[e] = s;
+          }
+      const int64_t q  = cell * nq + p;
+      const int64_t ts = a.tab_stride;
+      T             U[dim], GU[dim][dim], GP[dim], UT[dim], oldg[dim * dim + dim];
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        {
+          U[d] = a.tab[(F::U + d) * ts + q];
+#pragma unroll
+          for (int e = 0; e < dim; ++e)
+            GU[d][e] = MODE == MODE_NEWTON ? a.tab[(F::GU + d * dim + e) * ts + q] : T(0);
+          GP[d] = MODE == MODE_NEWTON ? a.tab[(F::GP + d) * ts + q] : T(0);
+          UT[d] = ((MODE == MODE_NEWTON && a.td) || (MODE == MODE_RESIDUAL && a.have_prev)) ?
+                    a.tab[(F::UT + d) * ts + q] :
+                    T(0);
+        }
+#pragma unroll
+      for (int i = 0; i < dim * dim + dim; ++i)
+        oldg[i] = (MODE == MODE_RESIDUAL && a.have_old_grad) ? a.old_grad[i * ts + q] : T(0);
+      const T d1 = a.cw ? a.cellwise[cell] : a.tab[F::D1 * ts + q];
+      const T d2 = a.cw ? a.cellwise[a.n_cells + cell] : a.tab[F::D2 * ts + q];
+      T       vr[nc], gr[nc][dim];
+      qpoint_physics<dim, T, MODE>(val, val[dim], gu, gp, U, GU, GP, UT, oldg, d1, d2,
+                                   a.nu, a.w0, a.theta, a.td, a.have_prev, a.have_old_grad, vr,
+                                   gr);
+      // submit_value / submit_gradient: JxW and J^{-T}
+#pragma unroll
+      for (int c = 0; c < nc; ++c)
+        {
+          vhat[c] = vr[c] * g.JxW;
+#pragma unroll
+          for (int i = 0; i < dim; ++i)
+            {
+              T s = 0;
+#pragma unroll
+              for (int e = 0; e < dim; ++e)
+                s += g.inv[i][e] * gr[c][e];
+              ghat[c][i] = s * g.JxW;
+            }
+        }
+    }
+  // ---- integrate: gradient part via Dq^T, then S^T sweeps
+  if (in_block)
+#pragma unroll
+    for (int c = 0; c < nc; ++c)
+#pragma unroll
+      for (int ax = 0; ax < dim; ++ax)
+        A[(c * dim + ax) * nq + p] = ghat[c][ax];
+  __syncthreads();
+  T wq[nc];
+  if (in_block)
+#pragma unroll
+    for (int c = 0; c < nc; ++c)
+      {
+        T s = vhat[c];
+#pragma unroll
+        for (int ax = 0; ax < dim; ++ax)
+          s += contract<n, true>(A + (c * dim + ax) * nq, sD, pa[ax], p - pa[ax] * st[ax], st[ax]);
+        wq[c] = s;
+      }
+  __syncthreads();
+  if (in_block)
+#pragma unroll
+    for (int c = 0; c < nc; ++c)
+      A[c * nq + p] = wq[c];
+  __syncthreads();
+  in  = A;
+  out = B;
+#pragma unroll
+  for (int ax = dim - 1; ax >= 0; --ax)
+    {
+      if (in_block)
+#pragma unroll
+        for (int c = 0; c < nc; ++c)
+          out[c * nq + p] =
+            contract<n, true>(in + c * nq, sS, pa[ax], p - pa[ax] * st[ax], st[ax]);
+      __syncthreads();
+      T *tmp = in;
+      in     = out;
+      out    = tmp;
+    }
+
+  // ---- scatter (distribute_local_to_global, constrained dofs skipped)
+  if (!active)
+    return;
+  if (DIAG)
+    {
+      const int c = jdiag % nc;
+      if (p == jdiag / nc && !((cm >> c) & 1))
+        unsafeAtomicAdd(a.dst + (size_t)node * nc + c, in[c * nq + p]);
+    }
+  else
+    {
+#pragma unroll
+      for (int c = 0; c < nc; ++c)
+        if (!((cm >> c) & 1))
+          {
+            const T r = in[c * nq + p];
+            unsafeAtomicAdd(a.dst + (size_t)node * nc + c, MODE == MODE_RESIDUAL ? -r : r);
+          }
+    }
+}
+
+// ------------------------------------------------------------ producers
+// set_linearization_point (operator_ns.cc:570-620) fused with
+// compute_penalty_parameters (:322-421): u*, grad u*, grad p* at q and the
+// q-wise / cell-wise delta_1, delta_2.
+template <typename T, int dim, int n>
+struct ProducerArgs
+{
+  const uint32_t *nodes;
+  const uint32_t *cell_geo;
+  const T        *geo_cart;
+  int64_t         n_cart;
+  const T        *geo_gen;
+  int64_t         gen_stride;
+  T              *tab;
+  int64_t         tab_stride;
+  T              *cellwise;
+  int64_t         n_cells;
+  T              *old_grad;
+  const T        *vec;
+  const T        *h_q;   // [n_cells] (6|K|/pi)^(1/3)/k or sqrt(4|K|/pi)/k
+  const T        *h_min; // [n_cells] minimum vertex distance
+  T               nu, c1, c2, stau;
+  int             what; // 0: linearization point, 1: Ut_old, 2: old gradients
+  Shape<T, n>     sh;
+};
+
+template <int dim, int k, typename T>
+__global__ void __launch_bounds__(BLOCK)
+  k_produce(ProducerArgs<T, dim, k + 1> a)
+{
+  constexpr int n    = k + 1;
+  constexpr int nq   = ipow(n, dim);
+  constexpr int nc   = dim + 1;
+  constexpr int CPB  = BLOCK / nq;
+  constexpr int LDSC = 2 * nc * nq;
+  using F            = Fields<dim>;
+
+  __shared__ T smem[CPB * LDSC];
+  __shared__ T sS[n][n], sD[n][n], sw[n];
+  __shared__ T umax[CPB];
+
+  const int t = threadIdx.x;
+  if (t < n * n)
+    {
+      sS[t / n][t % n] = a.sh.S[t / n][t % n];
+      sD[t / n][t % n] = a.sh.Dq[t / n][t % n];
+    }
+  if (t < n)
+    sw[t] = a.sh.w[t];
+  const int     lc       = t / nq;
+  const int     p        = t - lc * nq;
+  const bool    in_block = lc < CPB;
+  const int64_t cell     = (int64_t)blockIdx.x * CPB + lc;
+  const bool    active   = in_block && cell < a.n_cells;
+  T            *A        = smem + (in_block ? lc : 0) * LDSC;
+  T            *B        = A + nc * nq;
+  const int     px = p % n, py = (p / n) % n, pz = dim == 3 ? p / (n * n) : 0;
+  const int     pa[3] = {px, py, pz};
+  const int     st[3] = {1, n, n * n};
+
+  T u[nc];
+#pragma unroll
+  for (int c = 0; c < nc; ++c)
+    u[c] = 0;
+  if (active)
+    load_node<T, nc>(a.vec, a.nodes[cell * nq + p] & NODE_MASK, u); // read plain
+  if (in_block)
+#pragma unroll
+    for (int c = 0; c < nc; ++c)
+      A[c * nq + p] = u[c];
+  __syncthreads();
+  T *in = A, *out = B;
+#pragma unroll
+  for (int ax = 0; ax < dim; ++ax)
+    {
+      if (in_block)
+#pragma unroll
+        for (int c = 0; c < nc; ++c)
+          out[c * nq + p] =
+            contract<n, false>(in + c * nq, sS, pa[ax], p - pa[ax] * st[ax], st[ax]);
+      __syncthreads();
+      T *tmp = in;
+      in     = out;
+      out    = tmp;
+    }
+  T val[nc], gref[nc][dim];
+  if (in_block)
+#pragma unroll
+    for (int c = 0; c < nc; ++c)
+      {
+        val[c] = in[c * nq + p];
+#pragma unroll
+        for (int ax = 0; ax < dim; ++ax)
+          gref[c][ax] = contract<n, false>(in + c * nq, sD, pa[ax], p - pa[ax] * st[ax], st[ax]);
+      }
+  const int64_t q  = cell * nq + p;
+  const int64_t ts = a.tab_stride;
+  T             unorm = 0;
+  if (active)
+    {
+      if (a.what == 1)
+        {
+          // set_previous_solution: u_time_derivative_old (:262-271)
+#pragma unroll
+          for (int d = 0; d < dim; ++d)
+            a.tab[(F::UT + d) * ts + q] = val[d];
+        }
+      else
+        {
+          QGeo<dim, n, T> g;
+          ApplyArgs<T, dim, n> ga;
+          ga.cell_geo   = a.cell_geo;
+          ga.geo_cart   = a.geo_cart;
+          ga.n_cart     = a.n_cart;
+          ga.geo_gen    = a.geo_gen;
+          ga.gen_stride = a.gen_stride;
+          load_geometry<dim, n, T>(ga, cell, p, px, py, pz, sw, g);
+          T gr[nc][dim];
+#pragma unroll
+          for (int c = 0; c < nc; ++c)
+#pragma unroll
+            for (int e = 0; e < dim; ++e)
+              {
+                T s = 0;
+#pragma unroll
+                for (int i = 0; i < dim; ++i)
+                  s += g.inv[i][e] * gref[c][i];
+                gr[c][e] = s;
+              }
+          if (a.what == 2)
+            {
+              // theta != 1: u_old_gradient, p_old_gradient (:273-316)
+#pragma unroll
+              for (int d = 0; d < dim; ++d)
+                {
+#pragma unroll
+                  for (int e = 0; e < dim; ++e)
+                    a.old_grad[(d * dim + e) * ts + q] = gr[d][e];
+                  a.old_grad[(dim * dim + d) * ts + q] = gr[dim][d];
+                }
+            }
+          else
+            {
+              T u2 = 0;
+#pragma unroll
+              for (int d = 0; d < dim; ++d)
+                {
+                  a.tab[(F::U + d) * ts + q] = val[d];
+#pragma unroll
+                  for (int e = 0; e < dim; ++e)
+                    a.tab[(F::GU + d * dim + e) * ts + q] = gr[d][e];
+                  a.tab[(F::GP + d) * ts + q] = gr[dim][d];
+                  u2 += val[d] * val[d];
+                }
+              unorm = sqrt(u2);
+              // q-wise stabilisation, operator_ns.cc:394-420
+              const T h      = a.h_q[cell];
+              const T umag2  = T(1e-12) + u2;
+              const T fac    = T(4) * a.nu / (h * h);
+              a.tab[F::D1 * ts + q] =
+                T(1) / sqrt(a.stau * a.stau + T(4) * umag2 / h / h + T(9) * fac * fac);
+              a.tab[F::D2 * ts + q] = sqrt(umag2) * h * T(0.5);
+            }
+        }
+    }
+  if (a.what != 0)
+    return;
+  // cell-wise stabilisation (:365-388): u_max over the cell's q points
+  __syncthreads();
+  if (in_block)
+    A[p] = unorm;
+  __syncthreads();
+  if (active && p == 0)
+    {
+      T m = 0;
+      for (int i = 0; i < nq; ++i)
+        m = A[i] > m ? A[i] : m;
+      umax[lc]  = m;
+      const T h = a.h_min[cell];
+      T       d1, d2;
+      if (a.nu < h)
+        {
+          d1 = a.c1 / sqrt(a.stau * a.stau + m * m / (h * h));
+          d2 = a.c2 * h;
+        }
+      else
+        {
+          d1 = a.c1 * h * h;
+          d2 = a.c2 * h * h;
+        }
+      a.cellwise[cell]             = d1;
+      a.cellwise[a.n_cells + cell] = d2;
+    }
+}
+
+// ------------------------------------------------------------ vector kernels
+// dst[i] = constrained(i) ? src[i] : 0 (owned), 0 (ghost)  — cell_loop's
+// zero_dst plus the identity rows of vmult (operator_ns.cc:719-721)
+template <typename T>
+__global__ void
+k_init_dst(T *__restrict__ dst, const T *__restrict__ src, const uint32_t *__restrict__ cbits,
+           int64_t n_owned, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  T v = 0;
+  if (i < n_owned && ((cbits[i >> 5] >> (i & 31)) & 1))
+    v = src[i];
+  dst[i] = v;
+}
+
+template <typename T>
+__global__ void
+k_fill(T *__restrict__ dst, T v, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    dst[i] = v;
+}
+
+// y = sum_j w_j x_j (j < 4)
+template <typename T>
+__global__ void
+k_lincomb(T *__restrict__ y, const T *x0, const T *x1, const T *x2, const T *x3, double w0,
+          double w1, double w2, double w3, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  T s = 0;
+  if (x0)
+    s += T(w0) * x0[i];
+  if (x1)
+    s += T(w1) * x1[i];
+  if (x2)
+    s += T(w2) * x2[i];
+  if (x3)
+    s += T(w3) * x3[i];
+  y[i] = s;
+}
+
+// compute_inverse_diagonal finalisation (:220-224): constrained -> 1, then
+// d <- |d| > 1e-10 ? 1/d : 1
+template <typename T>
+__global__ void
+k_invert_diag(T *__restrict__ d, const uint32_t *__restrict__ cbits, int64_t n_owned, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  T v = d[i];
+  if (i < n_owned && ((cbits[i >> 5] >> (i & 31)) & 1))
+    v = 1;
+  d[i] = (fabs((double)v) > 1.0e-10) ? T(1) / v : T(1);
+}
+
+} // namespace gls

@@ -1,0 +1,232 @@
+"""ctypes binding of libglsamd.so (include/gls_op.h) — Python mirror of the
+reference's OperatorBase<Number> interface (include/operator_base.h:13-73)
+for the matrix-free GLS Navier–Stokes operator on MI355X.
+
+Vectors are torch tensors on the GPU (torch is plumbing: device memory and
+streams); every compute call goes through the HIP kernels of libglsamd.so.
+There is no CPU fallback: a missing library or GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.normpath(os.path.join(_HERE, "..", "lib"))
+_lib = None
+
+GLS_F64, GLS_F32 = 0, 1
+GLS_INCREMENT_FORM, GLS_CONSIDER_TIME_DERIVATIVE, GLS_CELL_WISE_STAB = 1, 2, 4
+
+# exported symbols of include/gls_op.h (checked by tests/test_abi.py)
+EXPORTS = [
+    "gls_op_create", "gls_op_destroy", "gls_op_set_parameters", "gls_op_m",
+    "gls_op_precision", "gls_op_set_linearization_point", "gls_op_set_previous_solution",
+    "gls_op_vmult", "gls_op_vmult_cells", "gls_op_vmult_init", "gls_op_evaluate_residual",
+    "gls_op_compute_inverse_diagonal", "gls_op_upload_tables", "gls_op_download_tables",
+    "gls_op_geometry_counts", "gls_op_vmult_bytes", "gls_mg_create", "gls_mg_destroy",
+    "gls_mg_setup", "gls_mg_get_relaxation", "gls_mg_vcycle", "gls_mg_prolongate_add",
+    "gls_mg_restrict_add", "gls_mg_interpolate", "gls_mg_smooth", "gls_last_error",
+]
+
+
+class OpDesc(C.Structure):
+    _fields_ = [("dim", C.c_int), ("degree", C.c_int), ("precision", C.c_int),
+                ("n_cells", C.c_int64), ("n_nodes", C.c_int64), ("n_owned_nodes", C.c_int64),
+                ("cell_nodes", C.c_void_p), ("node_coords", C.c_void_p),
+                ("node_cmask", C.c_void_p), ("cell_measure", C.c_void_p),
+                ("cell_hmin", C.c_void_p)]
+
+
+class OpParams(C.Structure):
+    _fields_ = [("nu", C.c_double), ("c1", C.c_double), ("c2", C.c_double),
+                ("theta", C.c_double), ("w0", C.c_double), ("dt", C.c_double),
+                ("order", C.c_int), ("flags", C.c_int)]
+
+
+class MGDesc(C.Structure):
+    _fields_ = [("n_levels", C.c_int), ("smoothing_n_iterations", C.c_int),
+                ("smoothing_eig_n_iterations", C.c_int), ("smoothing_range", C.c_double),
+                ("coarse_n_iterations", C.c_int)]
+
+
+def lib_path():
+    return os.path.join(LIBDIR, "libglsamd.so")
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = lib_path()
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make amd` (or __graft_entry__.build())")
+        L = C.CDLL(path)
+        vp, i64 = C.c_void_p, C.c_int64
+        L.gls_op_create.argtypes = [C.POINTER(OpDesc), C.POINTER(vp)]
+        L.gls_op_destroy.argtypes = [vp]
+        L.gls_op_set_parameters.argtypes = [vp, C.POINTER(OpParams)]
+        L.gls_op_m.argtypes = [vp]
+        L.gls_op_m.restype = i64
+        L.gls_op_precision.argtypes = [vp]
+        L.gls_op_set_linearization_point.argtypes = [vp, vp, vp]
+        L.gls_op_set_previous_solution.argtypes = [vp, vp, C.c_int, vp, vp]
+        L.gls_op_vmult.argtypes = [vp, vp, vp, vp]
+        L.gls_op_vmult_cells.argtypes = [vp, vp, vp, i64, i64, vp]
+        L.gls_op_vmult_init.argtypes = [vp, vp, vp, vp]
+        L.gls_op_evaluate_residual.argtypes = [vp, vp, vp, vp]
+        L.gls_op_compute_inverse_diagonal.argtypes = [vp, vp, vp]
+        L.gls_op_upload_tables.argtypes = [vp, vp, vp]
+        L.gls_op_download_tables.argtypes = [vp, vp, vp]
+        L.gls_op_geometry_counts.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)]
+        L.gls_op_vmult_bytes.argtypes = [vp]
+        L.gls_op_vmult_bytes.restype = C.c_double
+        L.gls_mg_create.argtypes = [C.POINTER(MGDesc), vp, vp, C.POINTER(vp)]
+        L.gls_mg_destroy.argtypes = [vp]
+        L.gls_mg_setup.argtypes = [vp, vp]
+        L.gls_mg_get_relaxation.argtypes = [vp, C.c_int, C.POINTER(C.c_double),
+                                            C.POINTER(C.c_double)]
+        L.gls_mg_vcycle.argtypes = [vp, vp, vp, vp]
+        for f in ("gls_mg_prolongate_add", "gls_mg_restrict_add", "gls_mg_interpolate"):
+            getattr(L, f).argtypes = [vp, C.c_int, vp, vp, vp]
+        L.gls_mg_smooth.argtypes = [vp, C.c_int, vp, vp, C.c_int, vp]
+        L.gls_last_error.restype = C.c_char_p
+        _lib = L
+    return _lib
+
+
+class GlsError(RuntimeError):
+    pass
+
+
+def _check(rc):
+    if rc != 0:
+        raise GlsError(lib().gls_last_error().decode())
+
+
+def _stream():
+    import torch
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr())
+
+
+class NavierStokesOperator:
+    """Mirror of NavierStokesOperator<dim, Number> (operator_ns.h:17-189) over
+    the HIP C-ABI.  precision: "f64" (fine level, Number=double) or "f32"
+    (MG levels, MGNumber=float, config.h:6-7)."""
+
+    def __init__(self, mesh, cmask, precision="f64", cells=None, n_owned_nodes=None):
+        import torch
+        if not torch.cuda.is_available():
+            raise GlsError("NavierStokesOperator needs a GPU (no CPU fallback by design)")
+        self.mesh = mesh
+        self.dim = mesh.dim
+        self.degree = mesh.degree
+        self.prec = GLS_F64 if precision in ("f64", "double", GLS_F64) else GLS_F32
+        self.dtype = torch.float64 if self.prec == GLS_F64 else torch.float32
+        cell_nodes = mesh.cell_nodes if cells is None else mesh.cell_nodes[cells]
+        meas, hmin = mesh.cell_measure()
+        if cells is not None:
+            meas, hmin = meas[cells], hmin[cells]
+        self._keep = [np.ascontiguousarray(cell_nodes, dtype=np.uint32),
+                      np.ascontiguousarray(mesh.coords, dtype=np.float64),
+                      np.ascontiguousarray(cmask, dtype=np.uint8),
+                      np.ascontiguousarray(meas), np.ascontiguousarray(hmin)]
+        k = self._keep
+        self.n_cells = k[0].shape[0]
+        d = OpDesc(self.dim, self.degree, self.prec, self.n_cells, mesh.n_nodes,
+                   mesh.n_nodes if n_owned_nodes is None else n_owned_nodes,
+                   k[0].ctypes.data, k[1].ctypes.data, k[2].ctypes.data, k[3].ctypes.data,
+                   k[4].ctypes.data)
+        h = C.c_void_p()
+        _check(lib().gls_op_create(C.byref(d), C.byref(h)))
+        self.h = h
+        self.n_dofs = lib().gls_op_m(h)
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().gls_op_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    # --- OperatorBase-like API
+    def m(self):
+        return self.n_dofs
+
+    def set_parameters(self, nu, c1=1.0, c2=1.0, theta=1.0, w0=0.0, dt=1.0, order=0,
+                       increment_form=True, consider_time_derivative=False,
+                       cell_wise_stabilization=False):
+        flags = ((GLS_INCREMENT_FORM if increment_form else 0)
+                 | (GLS_CONSIDER_TIME_DERIVATIVE if consider_time_derivative else 0)
+                 | (GLS_CELL_WISE_STAB if cell_wise_stabilization else 0))
+        self.params = OpParams(nu, c1, c2, theta, w0, dt, order, flags)
+        _check(lib().gls_op_set_parameters(self.h, C.byref(self.params)))
+
+    def initialize_dof_vector(self):
+        import torch
+        return torch.zeros(self.n_dofs, dtype=self.dtype, device="cuda")
+
+    def _dev(self, v):
+        import torch
+        if isinstance(v, np.ndarray):
+            v = torch.from_numpy(v)
+        return v.to(device="cuda", dtype=self.dtype).contiguous()
+
+    def set_linearization_point(self, vec):
+        v = self._dev(vec)
+        _check(lib().gls_op_set_linearization_point(self.h, _ptr(v), _stream()))
+
+    def set_previous_solution(self, history, weights):
+        hs = [self._dev(h) for h in history]
+        ptrs = (C.c_void_p * len(hs))(*[h.data_ptr() for h in hs])
+        w = np.ascontiguousarray(weights, dtype=np.float64)
+        _check(lib().gls_op_set_previous_solution(self.h, C.cast(ptrs, C.c_void_p), len(hs),
+                                                  w.ctypes.data, _stream()))
+        self._hist_keep = hs
+
+    def vmult(self, dst, src):
+        _check(lib().gls_op_vmult(self.h, _ptr(dst), _ptr(src), _stream()))
+        return dst
+
+    def vmult_init(self, dst, src):
+        _check(lib().gls_op_vmult_init(self.h, _ptr(dst), _ptr(src), _stream()))
+
+    def vmult_cells(self, dst, src, begin, end):
+        _check(lib().gls_op_vmult_cells(self.h, _ptr(dst), _ptr(src), int(begin), int(end),
+                                        _stream()))
+
+    def evaluate_residual(self, dst, src):
+        _check(lib().gls_op_evaluate_residual(self.h, _ptr(dst), _ptr(src), _stream()))
+        return dst
+
+    def compute_inverse_diagonal(self, diag):
+        _check(lib().gls_op_compute_inverse_diagonal(self.h, _ptr(diag), _stream()))
+        return diag
+
+    def download_tables(self):
+        nq = (self.degree + 1) ** self.dim
+        nf = 2 + 3 * self.dim + self.dim ** 2
+        t = np.empty((self.n_cells, nq, nf))
+        cw = np.empty((self.n_cells, 2))
+        _check(lib().gls_op_download_tables(self.h, t.ctypes.data, cw.ctypes.data))
+        return t, cw
+
+    def upload_tables(self, tables, cellwise=None):
+        t = np.ascontiguousarray(tables, dtype=np.float64)
+        cw = None if cellwise is None else np.ascontiguousarray(cellwise, dtype=np.float64)
+        _check(lib().gls_op_upload_tables(self.h, t.ctypes.data,
+                                          None if cw is None else cw.ctypes.data))
+
+    def geometry_counts(self):
+        g, c = C.c_int64(), C.c_int64()
+        _check(lib().gls_op_geometry_counts(self.h, C.byref(g), C.byref(c)))
+        return g.value, c.value
+
+    def vmult_bytes(self):
+        return lib().gls_op_vmult_bytes(self.h)

@@ -1,0 +1,250 @@
+"""ctypes binding of libglsmesh.so (include/gls_mesh.h) + the deck reader.
+
+Problem setup for the hot path: the refined cylinder / hyper-cube meshes of
+the five BASELINE decks, their Q_k node numbering, boundary ids and the
+constrained-component masks of the boundary descriptor.  See
+include/gls_mesh.h for the reference lines each function restates.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.normpath(os.path.join(_HERE, "..", "lib"))
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(LIBDIR, "libglsmesh.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make mesh` (or __graft_entry__.build())")
+        L = C.CDLL(path)
+        vp = C.c_void_p
+        L.gls_mesh_cylinder.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
+                                        C.c_double, C.c_double, C.c_double, C.POINTER(vp)]
+        L.gls_mesh_hypercube.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
+        L.gls_mesh_destroy.argtypes = [vp]
+        for name in ("gls_mesh_dim", "gls_mesh_degree"):
+            getattr(L, name).argtypes = [vp]
+            getattr(L, name).restype = C.c_int
+        for name in ("gls_mesh_n_cells", "gls_mesh_n_nodes", "gls_mesh_n_coarse_cells"):
+            getattr(L, name).argtypes = [vp]
+            getattr(L, name).restype = C.c_int64
+        for name in ("gls_mesh_cell_nodes", "gls_mesh_node_coords", "gls_mesh_node_boundary",
+                     "gls_mesh_cell_coarse"):
+            getattr(L, name).argtypes = [vp]
+            getattr(L, name).restype = vp
+        L.gls_mesh_constraint_mask.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, vp]
+        L.gls_mesh_child_lattice.argtypes = [vp, vp, vp]
+        L.gls_mesh_cell_measure.argtypes = [vp, vp, vp]
+        L.gls_mesh_last_error.restype = C.c_char_p
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(lib().gls_mesh_last_error().decode())
+
+
+def _view(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    ct = np.ctypeslib.as_ctypes_type(dtype)
+    arr = np.ctypeslib.as_array((ct * n).from_address(ptr))
+    return arr.copy()
+
+
+class Mesh:
+    """A refined mesh with Q_k node numbering (dof = node*(dim+1)+comp)."""
+
+    def __init__(self, handle, kind, params):
+        self._h = C.c_void_p(handle)
+        self.kind = kind
+        self.params = params
+        L = lib()
+        self.dim = L.gls_mesh_dim(self._h)
+        self.degree = L.gls_mesh_degree(self.h)
+        self.n_cells = L.gls_mesh_n_cells(self._h)
+        self.n_nodes = L.gls_mesh_n_nodes(self._h)
+        self.n_coarse_cells = L.gls_mesh_n_coarse_cells(self._h)
+        self.nloc = (self.degree + 1) ** self.dim
+        self.cell_nodes = _view(L.gls_mesh_cell_nodes(self._h), self.n_cells * self.nloc,
+                                np.uint32).reshape(self.n_cells, self.nloc)
+        self.coords = _view(L.gls_mesh_node_coords(self._h), self.n_nodes * self.dim,
+                            np.float64).reshape(self.n_nodes, self.dim)
+        self.node_boundary = _view(L.gls_mesh_node_boundary(self._h), self.n_nodes, np.uint32)
+        self.cell_coarse = _view(L.gls_mesh_cell_coarse(self._h), self.n_cells, np.int32)
+
+    @property
+    def h(self):
+        return self._h
+
+    @property
+    def n_dofs(self):
+        return self.n_nodes * (self.dim + 1)
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().gls_mesh_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def constraint_mask(self, vel_ids=(), p_ids=(), slip_ids=()):
+        out = np.zeros(self.n_nodes, dtype=np.uint8)
+        bits = lambda ids: sum(1 << int(i) for i in ids)
+        _check(lib().gls_mesh_constraint_mask(self._h, bits(vel_ids), bits(p_ids),
+                                              bits(slip_ids), out.ctypes.data))
+        return out
+
+    def cell_measure(self):
+        meas = np.zeros(self.n_cells)
+        hmin = np.zeros(self.n_cells)
+        _check(lib().gls_mesh_cell_measure(self._h, meas.ctypes.data, hmin.ctypes.data))
+        return meas, hmin
+
+    def child_lattice(self, fine: "Mesh"):
+        L = 2 * self.degree + 1
+        out = np.zeros((self.n_cells, L ** self.dim), dtype=np.uint32)
+        _check(lib().gls_mesh_child_lattice(self._h, fine._h, out.ctypes.data))
+        return out
+
+
+def cylinder(dim, degree, n_ref, length=None, height=0.41, position=None, diameter=0.1,
+             shift=0.005):
+    """Channel with cylinder (grid_cylinder.h; defaults simulation.cc:210-215)."""
+    if length is None:
+        length = 2.2 if dim == 2 else 2.5
+    if position is None:
+        position = 0.2 if dim == 2 else 0.5
+    h = C.c_void_p()
+    _check(lib().gls_mesh_cylinder(dim, degree, n_ref, length, height, position, diameter,
+                                   shift, C.byref(h)))
+    return Mesh(h.value, "cylinder", dict(dim=dim, degree=degree, n_ref=n_ref, length=length,
+                                          height=height, position=position,
+                                          diameter=diameter, shift=shift))
+
+
+def hypercube(dim, degree, n_ref):
+    h = C.c_void_p()
+    _check(lib().gls_mesh_hypercube(dim, degree, n_ref, C.byref(h)))
+    return Mesh(h.value, "hypercube", dict(dim=dim, degree=degree, n_ref=n_ref))
+
+
+# --------------------------------------------------------------------- decks
+DECK_DIR = os.path.normpath(os.path.join(_HERE, "..", "..", "tests", "decks"))
+
+
+@dataclass
+class Deck:
+    """Parameters of one input deck that reach the hot path (defaults as
+    Parameters main.cc:66-118 and SimulationCylinder simulation.cc:198-222)."""
+    name: str
+    dim: int = 2
+    fe_degree: int = 1
+    n_refinements: int = 0
+    simulation: str = "cylinder"
+    time_integration: str = "bdf"
+    bdf_order: int = 2
+    theta: float = 1.0
+    c1: float = 1.0
+    c2: float = 1.0
+    nu: float = 0.001
+    consider_time_derivative: bool = True
+    cell_wise_stabilization: bool = False
+    nonlinear_solver: str = "Newton"
+    no_slip_cylinder: bool = True
+    no_slip_wall: bool = True
+    cylinder_shift: float = 0.005
+    u_max: float = 1.0
+    raw: dict = field(default_factory=dict)
+
+    @property
+    def increment_form(self):
+        # main.cc:331
+        return self.nonlinear_solver == "Newton"
+
+    def boundary_descriptor(self):
+        """(vel_ids, p_ids, slip_ids) of constraints_homogeneous
+        (simulation.cc:378-431 + main.cc:259-291)."""
+        if self.simulation != "cylinder":
+            raise NotImplementedError(f"simulation {self.simulation!r} (SURVEY §8f next-4)")
+        vel = [0]  # inflow: inhomogeneous DBC, zero in constraints_homogeneous
+        slip = []
+        walls = list(range(3, 3 + 2 * self.dim))
+        (vel if self.no_slip_wall else slip).extend(walls)
+        (vel if self.no_slip_cylinder else slip).append(2)
+        p = [1]  # outflow: homogeneous "NBC" constrains the pressure
+        return vel, p, slip
+
+    def time_integrator(self, dt=2.5e-4, n_steps=None):
+        """(theta, weights[0..order], order, current_dt) of the deck's
+        TimeIntegratorData after `n_steps` constant-dt updates (default: order,
+        i.e. full order reached) — time_integration.cc:10-178."""
+        if self.time_integration == "none":
+            return 1.0, [0.0], 0, 1.0
+        if self.time_integration == "theta":
+            return self.theta, [1.0 / dt, -1.0 / dt], 1, dt
+        order = self.bdf_order
+        n_steps = order if n_steps is None else n_steps
+        dts = [dt if i < n_steps else 0.0 for i in range(order)]
+        w = [0.0] * (order + 1)
+        eff = sum(1 for x in dts if x > 0)
+        d = dts
+        if eff == 3:
+            w[1] = -(d[0] + d[1]) * (d[0] + d[1] + d[2]) / (d[0] * d[1] * (d[1] + d[2]))
+            w[2] = d[0] * (d[0] + d[1] + d[2]) / (d[1] * d[2] * (d[0] + d[1]))
+            w[3] = -d[0] * (d[0] + d[1]) / (d[2] * (d[1] + d[2]) * (d[0] + d[1] + d[2]))
+            w[0] = -(w[1] + w[2] + w[3])
+        elif eff == 2:
+            w[0] = (2 * d[0] + d[1]) / (d[0] * (d[0] + d[1]))
+            w[1] = -(d[0] + d[1]) / (d[0] * d[1])
+            w[2] = d[0] / (d[1] * (d[0] + d[1]))
+        elif eff == 1:
+            w[0], w[1] = 1.0 / d[0], -1.0 / d[0]
+        return 1.0, w, order, d[0]
+
+    def operator_parameters(self, dt=2.5e-4):
+        """Keyword arguments for NavierStokesOperator.set_parameters / Oracle."""
+        theta, w, order, cdt = self.time_integrator(dt)
+        return dict(nu=self.nu, c1=self.c1, c2=self.c2, theta=theta, w0=w[0], dt=cdt,
+                    order=order, increment_form=self.increment_form,
+                    consider_time_derivative=self.consider_time_derivative,
+                    cell_wise_stabilization=self.cell_wise_stabilization), w
+
+    def mesh(self, n_ref=None):
+        n_ref = self.n_refinements if n_ref is None else n_ref
+        return cylinder(self.dim, self.fe_degree, n_ref, shift=self.cylinder_shift)
+
+
+def read_deck(path):
+    with open(path) as f:
+        raw = json.load(f)
+    d = Deck(name=os.path.basename(path), raw=raw)
+    d.dim = int(raw.get("dim", 2))
+    d.fe_degree = int(raw.get("fe degree", 1))
+    d.n_refinements = int(raw.get("n global refinements", 0))
+    d.simulation = raw.get("simulation name", "channel")
+    d.time_integration = raw.get("time intration", "theta")
+    d.bdf_order = int(raw.get("bdf order", 1))
+    d.theta = float(raw.get("theta", 0.5))
+    d.c1 = float(raw.get("c1", 4.0))
+    d.c2 = float(raw.get("c2", 2.0))
+    d.nu = float(raw.get("nu", 0.1))
+    d.consider_time_derivative = bool(raw.get("consider time derivative", False))
+    d.cell_wise_stabilization = bool(raw.get("cell wise stabilization", True))
+    d.nonlinear_solver = raw.get("nonlinear solver", "linearized")
+    d.no_slip_cylinder = bool(raw.get("simulation no slip cylinder", True))
+    d.no_slip_wall = bool(raw.get("simulation no slip wall", True))
+    d.cylinder_shift = float(raw.get("simulation geometry cylinder shift", 0.005))
+    d.u_max = float(raw.get("simulation u max", 1.0))
+    return d

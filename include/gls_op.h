@@ -1,0 +1,185 @@
+/*
+ * gls_op.h — C-ABI of the MI355X (gfx950) matrix-free GLS Navier–Stokes
+ * operator and its geometric-multigrid pieces (libglsamd.so).
+ *
+ * This is the drop-in boundary for the reference's hot path.  Each entry
+ * point replaces one member of the reference's operator / preconditioner
+ * interface (peterrum/dealii-ns-gls @ 2025-05-23):
+ *
+ *   gls_op_create                    NavierStokesOperator ctor
+ *                                      include/operator_ns.h:24-41, .cc:68-153
+ *                                      (+ MatrixFree::reinit of the cell
+ *                                      geometry, .cc:110-121)
+ *   gls_op_set_parameters            the scalars the ctor / TimeIntegratorData
+ *                                      feed the kernel (nu, c1, c2, theta,
+ *                                      primary weight, dt, order, flags)
+ *                                      operator_ns.h:102-114,
+ *                                      time_integration.h:10-36
+ *   gls_op_set_linearization_point   OperatorBase::set_linearization_point
+ *                                      operator_base.h:38-39, .cc:570-620
+ *                                      (+ compute_penalty_parameters :322-421)
+ *   gls_op_set_previous_solution     OperatorBase::set_previous_solution
+ *                                      operator_base.h:35-36, .cc:234-320
+ *   gls_op_vmult                     OperatorBase::vmult
+ *                                      operator_base.h:47-48, .cc:684-732
+ *   gls_op_vmult_cells /
+ *   gls_op_vmult_finish              the two halves of vmult around the ghost
+ *                                      exchange (deal.II cell_loop with
+ *                                      compress(add), .cc:702-721) for
+ *                                      multi-GPU overlap
+ *   gls_op_evaluate_residual         OperatorBase::evaluate_residual
+ *                                      operator_base.h:44-46, .cc:648-682
+ *   gls_op_compute_inverse_diagonal  OperatorBase::compute_inverse_diagonal
+ *                                      operator_base.h:29-30, .cc:195-225
+ *   gls_op_m                         OperatorBase::m  operator_base.h:23-24
+ *   gls_op_upload_tables /
+ *   gls_op_download_tables           host-produced / inspected per-q tables
+ *                                      (u_star_value ... operator_ns.h:120-132)
+ *   gls_mg_*                         PreconditionerGMG (multigrid.h:61-141):
+ *                                      relaxation smoother (multigrid.cc:281-351),
+ *                                      MGTwoLevelTransfer (main.cc:538-563),
+ *                                      V-cycle apply (multigrid.cc:202-220)
+ *
+ * Conventions
+ *   - Vectors are DEVICE pointers in the operator's precision (double for
+ *     GLS_F64, float for GLS_F32), local layout [owned | ghost] with
+ *     dof = node * (dim + 1) + component (component dim = pressure).
+ *   - `stream` is a hipStream_t (NULL = legacy default stream).  Calls are
+ *     stream-ordered and not thread safe per handle (as the reference: one
+ *     host thread per rank, mutable state, operator_ns.h:181-188).
+ *   - Every function returns 0 on success; nonzero status = error, with a
+ *     thread-local message from gls_last_error() (the C++ facade turns it
+ *     into an exception, mirroring AssertThrow).
+ */
+#ifndef GLS_OP_H
+#define GLS_OP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct glsOp_ *glsOp;
+typedef struct glsMG_ *glsMG;
+typedef int            glsStatus;
+
+enum glsPrecision
+{
+  GLS_F64 = 0,
+  GLS_F32 = 1
+};
+
+enum glsFlags
+{
+  GLS_INCREMENT_FORM           = 1, /* Newton: increment_form, main.cc:331    */
+  GLS_CONSIDER_TIME_DERIVATIVE = 2, /* consider_time_derivative (ctor arg)    */
+  GLS_CELL_WISE_STAB           = 4  /* cell_wise_stabilization (ctor arg)     */
+};
+
+typedef struct
+{
+  int             dim;        /* 2 or 3                                       */
+  int             degree;     /* Q_k, k in {1,2,3}                            */
+  int             precision;  /* glsPrecision                                 */
+  int64_t         n_cells;    /* locally processed cells                      */
+  int64_t         n_nodes;    /* local nodes [owned | ghost]                  */
+  int64_t         n_owned_nodes; /* owned prefix; identity rows only there    */
+  const uint32_t *cell_nodes; /* host [n_cells][(k+1)^dim] lexicographic      */
+  const double   *node_coords;/* host [n_nodes][dim] MappingQ_k support pts   */
+  const uint8_t  *node_cmask; /* host [n_nodes] constrained component bits    */
+  const double   *cell_measure;     /* host [n_cells] vertex measure |K|      */
+  const double   *cell_hmin;        /* host [n_cells] min vertex distance     */
+} glsOpDesc;
+
+typedef struct
+{
+  double nu, c1, c2;
+  double theta;  /* TimeIntegratorData::get_theta()                          */
+  double w0;     /* get_primary_weight()                                      */
+  double dt;     /* get_current_dt()  (stau = dt == 0 ? 0 : 1/dt)             */
+  int    order;  /* get_order()                                               */
+  int    flags;  /* glsFlags                                                  */
+} glsOpParams;
+
+glsStatus gls_op_create(const glsOpDesc *desc, glsOp *out);
+void      gls_op_destroy(glsOp op);
+glsStatus gls_op_set_parameters(glsOp op, const glsOpParams *prm);
+int64_t   gls_op_m(glsOp op); /* number of local dofs */
+int       gls_op_precision(glsOp op);
+
+glsStatus gls_op_set_linearization_point(glsOp op, const void *vec, void *stream);
+/* vec_old = sum_{i=1..order} weights[i] * history[i]  (history[0] unused) */
+glsStatus gls_op_set_previous_solution(glsOp op, const void *const *history,
+                                       int n_history, const double *weights,
+                                       void *stream);
+
+glsStatus gls_op_vmult(glsOp op, void *dst, const void *src, void *stream);
+/* cells [cell_begin, cell_end): dst += cell contributions (no zeroing) */
+glsStatus gls_op_vmult_cells(glsOp op, void *dst, const void *src,
+                             int64_t cell_begin, int64_t cell_end,
+                             void *stream);
+/* dst[i] = constrained(i) ? src[i] : 0 on the owned dofs, 0 on ghosts */
+glsStatus gls_op_vmult_init(glsOp op, void *dst, const void *src, void *stream);
+
+glsStatus gls_op_evaluate_residual(glsOp op, void *dst, const void *src,
+                                   void *stream);
+glsStatus gls_op_compute_inverse_diagonal(glsOp op, void *inv_diag,
+                                          void *stream);
+
+/* canonical host layout [cell][q][field] (fields: delta1, delta2, U(dim),
+ * gradU(dim*dim), gradP(dim), Ut_old(dim)) + cellwise [cell][2] */
+glsStatus gls_op_upload_tables(glsOp op, const double *tables,
+                               const double *cellwise);
+glsStatus gls_op_download_tables(glsOp op, double *tables, double *cellwise);
+
+/* number of cells whose geometry is stored per quadrature point (general)
+ * and per cell (Cartesian) — MatrixFree-style compressed geometry */
+glsStatus gls_op_geometry_counts(glsOp op, int64_t *n_general,
+                                 int64_t *n_cartesian);
+/* algorithmic bytes of one vmult (SURVEY §8d B_tab) */
+double gls_op_vmult_bytes(glsOp op);
+
+/* ------------------------------------------------------------ multigrid */
+typedef struct
+{
+  int    n_levels;             /* levels 0 (coarse) .. n_levels-1 (fine)     */
+  int    smoothing_n_iterations;       /* 5   multigrid.h:31                 */
+  int    smoothing_eig_n_iterations;   /* 20  multigrid.h:32                 */
+  double smoothing_range;              /* 20  multigrid.h:30                 */
+  int    coarse_n_iterations;  /* coarse solver: relaxation sweeps (0 =
+                                  identity); see DESIGN.md                   */
+} glsMGDesc;
+
+/* levels[l] are level operators (same precision); child[l] for l >= 1 is the
+ * host child lattice of level l-1 cells into level l nodes
+ * (gls_mesh_child_lattice), n_cells(l-1) * (2k+1)^dim entries. */
+glsStatus gls_mg_create(const glsMGDesc *desc, const glsOp *levels,
+                        const uint32_t *const *child, glsMG *out);
+void      gls_mg_destroy(glsMG mg);
+/* PreconditionerGMG::initialize (multigrid.cc:247-370): inverse diagonals
+ * and power-iteration relaxation factors on every level */
+glsStatus gls_mg_setup(glsMG mg, void *stream);
+glsStatus gls_mg_get_relaxation(glsMG mg, int level, double *omega,
+                                double *lambda_max);
+/* one V-cycle on the finest level: dst = V(src) (PreconditionMG::vmult) */
+glsStatus gls_mg_vcycle(glsMG mg, void *dst, const void *src, void *stream);
+/* transfer on level pair (l-1, l): prolongate_and_add / restrict_and_add */
+glsStatus gls_mg_prolongate_add(glsMG mg, int level, void *dst_fine,
+                                const void *src_coarse, void *stream);
+glsStatus gls_mg_restrict_add(glsMG mg, int level, void *dst_coarse,
+                              const void *src_fine, void *stream);
+/* interpolate_to_mg: nodal injection level l -> l-1 */
+glsStatus gls_mg_interpolate(glsMG mg, int level, void *dst_coarse,
+                             const void *src_fine, void *stream);
+/* PreconditionRelaxation::vmult (zero start) / step on one level */
+glsStatus gls_mg_smooth(glsMG mg, int level, void *x, const void *b,
+                        int zero_initial_guess, void *stream);
+
+const char *gls_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

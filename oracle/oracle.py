@@ -1,0 +1,182 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of oracle/liboracle.so.
+
+The CPU restatement of the reference hot path (see gls_oracle.h for the
+reference lines it follows and its parity status: pinned by KAT-1..6,
+"parity unpinned" against the reference binary, which cannot be built here).
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+
+class _Mesh(C.Structure):
+    _fields_ = [("dim", C.c_int), ("degree", C.c_int), ("n_cells", C.c_int64),
+                ("n_nodes", C.c_int64), ("cell_nodes", C.c_void_p), ("coords", C.c_void_p),
+                ("cmask", C.c_void_p), ("cell_measure", C.c_void_p), ("cell_hmin", C.c_void_p)]
+
+
+class _Params(C.Structure):
+    _fields_ = [("nu", C.c_double), ("c1", C.c_double), ("c2", C.c_double),
+                ("theta", C.c_double), ("w0", C.c_double), ("dt", C.c_double),
+                ("order", C.c_int), ("consider_time_derivative", C.c_int),
+                ("increment_form", C.c_int), ("cell_wise_stabilization", C.c_int)]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C oracle`")
+        L = C.CDLL(path)
+        vp = C.c_void_p
+        L.orc_create.argtypes = [C.POINTER(_Mesh), C.POINTER(_Params)]
+        L.orc_create.restype = vp
+        L.orc_destroy.argtypes = [vp]
+        L.orc_set_threads.argtypes = [C.c_int]
+        L.orc_set_linearization_point.argtypes = [vp, vp]
+        L.orc_set_previous_solution.argtypes = [vp, vp, C.c_int, vp]
+        L.orc_vmult.argtypes = [vp, vp, vp]
+        L.orc_evaluate_residual.argtypes = [vp, vp, vp]
+        L.orc_compute_inverse_diagonal.argtypes = [vp, vp]
+        L.orc_cell_matrix.argtypes = [vp, C.c_int64, vp]
+        L.orc_get_tables.argtypes = [vp, vp, vp]
+        L.orc_get_tables.restype = C.c_int
+        L.orc_get_geometry.argtypes = [vp, vp]
+        L.orc_bdf_weights.argtypes = [C.c_int, vp, vp]
+        L.orc_bdf_weights.restype = C.c_int
+        for f in ("orc_prolongate_add", "orc_restrict_add", "orc_interpolate"):
+            getattr(L, f).argtypes = [vp, vp, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def set_threads(n):
+    lib().orc_set_threads(int(n))
+
+
+def _p(a):
+    return a.ctypes.data
+
+
+class OracleMesh:
+    """Holds the numpy arrays alive for an orc_mesh struct."""
+
+    def __init__(self, mesh, cmask):
+        self.dim = mesh.dim
+        self.degree = mesh.degree
+        self.n_nodes = mesh.n_nodes
+        self.n_cells = mesh.n_cells
+        self.cell_nodes = np.ascontiguousarray(mesh.cell_nodes, dtype=np.uint32)
+        self.coords = np.ascontiguousarray(mesh.coords, dtype=np.float64)
+        self.cmask = np.ascontiguousarray(cmask, dtype=np.uint8)
+        meas, hmin = mesh.cell_measure()
+        self.measure = np.ascontiguousarray(meas)
+        self.hmin = np.ascontiguousarray(hmin)
+        self.s = _Mesh(self.dim, self.degree, self.n_cells, self.n_nodes, _p(self.cell_nodes),
+                       _p(self.coords), _p(self.cmask), _p(self.measure), _p(self.hmin))
+
+    @property
+    def n_dofs(self):
+        return self.n_nodes * (self.dim + 1)
+
+
+class Oracle:
+    """CPU NavierStokesOperator restatement on one mesh (double precision)."""
+
+    def __init__(self, omesh: OracleMesh, nu, c1=1.0, c2=1.0, theta=1.0, w0=0.0, dt=1.0,
+                 order=0, consider_time_derivative=False, increment_form=True,
+                 cell_wise_stabilization=False):
+        self.m = omesh
+        self.prm = _Params(nu, c1, c2, theta, w0, dt, order, int(consider_time_derivative),
+                           int(increment_form), int(cell_wise_stabilization))
+        self.h = lib().orc_create(C.byref(omesh.s), C.byref(self.prm))
+        if not self.h:
+            raise RuntimeError("orc_create failed")
+        self.nq = (omesh.degree + 1) ** omesh.dim
+
+    def __del__(self):
+        try:
+            lib().orc_destroy(self.h)
+        except Exception:
+            pass
+
+    def set_linearization_point(self, vec):
+        vec = np.ascontiguousarray(vec, dtype=np.float64)
+        lib().orc_set_linearization_point(self.h, _p(vec))
+
+    def set_previous_solution(self, history, weights):
+        hist = [np.ascontiguousarray(h, dtype=np.float64) for h in history]
+        ptrs = (C.c_void_p * len(hist))(*[_p(h) for h in hist])
+        w = np.ascontiguousarray(weights, dtype=np.float64)
+        lib().orc_set_previous_solution(self.h, C.cast(ptrs, C.c_void_p), len(hist), _p(w))
+
+    def vmult(self, src):
+        src = np.ascontiguousarray(src, dtype=np.float64)
+        dst = np.empty_like(src)
+        lib().orc_vmult(self.h, _p(dst), _p(src))
+        return dst
+
+    def evaluate_residual(self, src):
+        src = np.ascontiguousarray(src, dtype=np.float64)
+        dst = np.empty_like(src)
+        lib().orc_evaluate_residual(self.h, _p(dst), _p(src))
+        return dst
+
+    def inverse_diagonal(self):
+        d = np.empty(self.m.n_dofs)
+        lib().orc_compute_inverse_diagonal(self.h, _p(d))
+        return d
+
+    def cell_matrix(self, cell):
+        nd = self.nq * (self.m.dim + 1)
+        A = np.empty((nd, nd))
+        lib().orc_cell_matrix(self.h, int(cell), _p(A))
+        return A
+
+    def tables(self):
+        dim = self.m.dim
+        nf = 2 + 3 * dim + dim * dim
+        t = np.empty((self.m.n_cells, self.nq, nf))
+        cw = np.empty((self.m.n_cells, 2))
+        lib().orc_get_tables(self.h, _p(t), _p(cw))
+        return t, cw
+
+    def geometry(self):
+        dim = self.m.dim
+        g = np.empty((self.m.n_cells, self.nq, 1 + dim * dim))
+        lib().orc_get_geometry(self.h, _p(g))
+        return g
+
+
+def bdf_weights(order, dts):
+    dt = np.zeros(max(order, 1))
+    dt[:len(dts)] = dts[:order]
+    w = np.zeros(order + 1)
+    lib().orc_bdf_weights(order, _p(dt), _p(w))
+    return w
+
+
+def prolongate_add(cm: OracleMesh, fm: OracleMesh, child, dst_f, src_c):
+    child = np.ascontiguousarray(child, dtype=np.uint32)
+    src_c = np.ascontiguousarray(src_c, dtype=np.float64)
+    lib().orc_prolongate_add(C.byref(cm.s), C.byref(fm.s), _p(child), _p(dst_f), _p(src_c))
+
+
+def restrict_add(cm: OracleMesh, fm: OracleMesh, child, dst_c, src_f):
+    child = np.ascontiguousarray(child, dtype=np.uint32)
+    src_f = np.ascontiguousarray(src_f, dtype=np.float64)
+    lib().orc_restrict_add(C.byref(cm.s), C.byref(fm.s), _p(child), _p(dst_c), _p(src_f))
+
+
+def interpolate(cm: OracleMesh, fm: OracleMesh, child, dst_c, src_f):
+    child = np.ascontiguousarray(child, dtype=np.uint32)
+    src_f = np.ascontiguousarray(src_f, dtype=np.float64)
+    lib().orc_interpolate(C.byref(cm.s), C.byref(fm.s), _p(child), _p(dst_c), _p(src_f))
