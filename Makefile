@@ -39,3 +39,9 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all mesh amd oracle clean
+
+# diagnostic ablation builds (timing only, wrong results by design)
+abl:
+	@mkdir -p $(LIBDIR)/abl
+	for v in 1 2 4 8 14; do $(HIPCC) $(HIPFLAGS) -DGLS_ABL=$$v -shared -o $(LIBDIR)/abl/libglsamd_abl$$v.so $(AMD_SRC) & done; wait
+.PHONY: abl

@@ -266,7 +266,7 @@ struct Impl
     a.src        = (const T *)src;
     a.cell_begin = b;
     a.cell_end   = e;
-    constexpr int CPB = BLOCK / nq;
+    constexpr int CPB = (64 / nq > 0 ? 64 / nq : 1) * (BLOCK / 64);
     const int64_t nv  = (e - b) * (diag ? (int64_t)nq * (dim + 1) : 1);
     const dim3    grid((unsigned)((nv + CPB - 1) / CPB));
 #define GLS_LAUNCH(M, DG) hipLaunchKernelGGL((k_apply<dim, k, T, M, DG>), grid, dim3(BLOCK), 0, s, a)

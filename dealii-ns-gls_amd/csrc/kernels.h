@@ -17,6 +17,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// GLS_ABL: diagnostic-only ablation builds (never the product library):
+//   1 plain (racy) read-modify-write instead of atomics, 2 no scatter,
+//   4 no table/geometry loads, 8 no gather
+#ifndef GLS_ABL
+#define GLS_ABL 0
+#endif
+
 namespace gls
 {
 constexpr uint32_t NODE_MASK  = 0x0FFFFFFFu;
@@ -298,6 +305,19 @@ load_geometry(const Args &a, int64_t cell, int p, int px, int py, int pz,
 }
 
 // ------------------------------------------------------------ apply kernel
+// Wave-local cell packing: each wavefront owns CPW = 64 / (k+1)^dim whole
+// cells (3D Q2: 2 cells = 54 lanes), so every sum-factorisation exchange is
+// ordered by a wavefront-scope fence instead of a workgroup barrier.  The
+// per-q tables and geometry are loaded into registers right after the
+// gather, so their HBM latency overlaps the evaluate sweeps.
+__device__ __forceinline__ void
+wave_sync()
+{
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // MODE: Newton / fixed-point vmult or residual.  DIAG: each virtual cell is
 // (cell, local dof j) with a unit-vector input; only the diagonal entry is
 // accumulated (MatrixFreeTools::compute_diagonal, operator_ns.cc:209-218).
@@ -308,9 +328,12 @@ __global__ void __launch_bounds__(BLOCK)
   constexpr int n    = k + 1;
   constexpr int nq   = ipow(n, dim);
   constexpr int nc   = dim + 1;
-  constexpr int CPB  = BLOCK / nq;
+  constexpr int CPW  = 64 / nq > 0 ? 64 / nq : 1;
+  constexpr int WPB  = BLOCK / 64;
+  constexpr int CPB  = CPW * WPB;
   constexpr int LDSC = nc * nq * (dim > 2 ? dim : 2);
   using F            = Fields<dim>;
+  static_assert(nq <= 64, "one cell must fit a wavefront");
 
   __shared__ T smem[CPB * LDSC];
   __shared__ T sS[n][n], sD[n][n], sw[n];
@@ -324,10 +347,13 @@ __global__ void __launch_bounds__(BLOCK)
   if (t < n)
     sw[t] = a.sh.w[t];
 
-  const int     lc       = t / nq;
-  const int     p        = t - lc * nq;
-  const bool    in_block = lc < CPB;
-  const int64_t vcell    = (int64_t)blockIdx.x * CPB + lc;
+  const int     wave    = t >> 6;
+  const int     lane    = t & 63;
+  const int     slot    = lane / nq;
+  const int     p       = lane - slot * nq;
+  const bool    in_wave = slot < CPW;
+  const int     lc      = wave * CPW + (in_wave ? slot : 0);
+  const int64_t vcell   = (int64_t)blockIdx.x * CPB + lc;
   int64_t       cell;
   int           jdiag = 0;
   if (DIAG)
@@ -337,8 +363,8 @@ __global__ void __launch_bounds__(BLOCK)
     }
   else
     cell = a.cell_begin + vcell;
-  const bool active = in_block && cell < a.cell_end;
-  T         *A      = smem + (in_block ? lc : 0) * LDSC;
+  const bool active = in_wave && cell < a.cell_end;
+  T         *A      = smem + lc * LDSC;
   T         *B      = A + nc * nq;
   const int  px     = p % n;
   const int  py     = (p / n) % n;
@@ -349,11 +375,110 @@ __global__ void __launch_bounds__(BLOCK)
   // ---- gather (read_dof_values / read_dof_values_plain)
   uint32_t node = 0, cm = 0;
   T        u[nc];
+#pragma unroll
+  for (int c = 0; c < nc; ++c)
+    u[c] = 0;
   if (active)
     {
       const uint32_t packed = a.nodes[cell * nq + p];
       node                  = packed & NODE_MASK;
       cm                    = packed >> 28;
+      if (!DIAG && !(GLS_ABL & 8))
+        load_node<T, nc>(a.src, node, u);
+      if (GLS_ABL & 8)
+#pragma unroll
+        for (int c = 0; c < nc; ++c)
+          u[c] = T(0.001) * (p + c);
+    }
+
+  // ---- prefetch geometry and per-q tables (consumed after evaluate)
+  const int64_t   q  = cell * nq + p;
+  const int64_t   ts = a.tab_stride;
+  QGeo<dim, n, T> g;
+  T               U[dim], GU[dim][dim], GP[dim], UT[dim], oldg[dim * dim + dim], d1 = 0, d2 = 0;
+  g.JxW = 0;
+#pragma unroll
+  for (int i = 0; i < dim; ++i)
+    {
+#pragma unroll
+      for (int e = 0; e < dim; ++e)
+        {
+          g.inv[i][e] = 0;
+          GU[i][e]    = 0;
+        }
+      U[i] = GP[i] = UT[i] = 0;
+    }
+#pragma unroll
+  for (int i = 0; i < dim * dim + dim; ++i)
+    oldg[i] = 0;
+  if (active && (GLS_ABL & 4))
+    {
+      g.JxW = T(1e-6);
+#pragma unroll
+      for (int i = 0; i < dim; ++i)
+        {
+          g.inv[i][i] = T(10) + p;
+          U[i]        = T(1) + i;
+        }
+      d1 = T(1e-4) * p;
+      d2 = T(1e-3);
+    }
+  if (active && !(GLS_ABL & 4))
+    {
+      const uint32_t cg = a.cell_geo[cell];
+      if (cg & GEO_GENERAL)
+        {
+          const int64_t idx = (int64_t)(cg & ~GEO_GENERAL) * nq + p;
+          g.JxW             = a.geo_gen[idx];
+#pragma unroll
+          for (int i = 0; i < dim; ++i)
+#pragma unroll
+            for (int e = 0; e < dim; ++e)
+              g.inv[i][e] = a.geo_gen[(1 + i * dim + e) * a.gen_stride + idx];
+        }
+      else
+        {
+#pragma unroll
+          for (int i = 0; i < dim; ++i)
+            g.inv[i][i] = a.geo_cart[i * a.n_cart + cg];
+          g.JxW = a.geo_cart[dim * a.n_cart + cg]; // det J, times weight below
+        }
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        {
+          U[d] = a.tab[(F::U + d) * ts + q];
+          if (MODE == MODE_NEWTON)
+            {
+#pragma unroll
+              for (int e = 0; e < dim; ++e)
+                GU[d][e] = a.tab[(F::GU + d * dim + e) * ts + q];
+              GP[d] = a.tab[(F::GP + d) * ts + q];
+            }
+          if ((MODE == MODE_NEWTON && a.td) || (MODE == MODE_RESIDUAL && a.have_prev))
+            UT[d] = a.tab[(F::UT + d) * ts + q];
+        }
+      if (MODE == MODE_RESIDUAL && a.have_old_grad)
+#pragma unroll
+        for (int i = 0; i < dim * dim + dim; ++i)
+          oldg[i] = a.old_grad[i * ts + q];
+      if (a.cw)
+        {
+          d1 = a.cellwise[cell];
+          d2 = a.cellwise[a.n_cells + cell];
+        }
+      else
+        {
+          d1 = a.tab[F::D1 * ts + q];
+          d2 = a.tab[F::D2 * ts + q];
+        }
+      if (!(cg & GEO_GENERAL))
+        {
+          T w = 1;
+#pragma unroll
+          for (int d = 0; d < dim; ++d)
+            w *= a.sh.w[pa[d]];
+          g.JxW *= w;
+        }
     }
   if (DIAG)
     {
@@ -361,160 +486,111 @@ __global__ void __launch_bounds__(BLOCK)
       for (int c = 0; c < nc; ++c)
         u[c] = (active && p == jdiag / nc && c == jdiag % nc) ? T(1) : T(0);
     }
-  else if (active)
-    {
-      load_node<T, nc>(a.src, node, u);
-      if (MODE != MODE_RESIDUAL)
-#pragma unroll
-        for (int c = 0; c < nc; ++c)
-          if ((cm >> c) & 1)
-            u[c] = 0;
-    }
-  else
+  else if (MODE != MODE_RESIDUAL)
     {
 #pragma unroll
       for (int c = 0; c < nc; ++c)
-        u[c] = 0;
+        if ((cm >> c) & 1)
+          u[c] = 0;
     }
-  if (in_block)
+  __syncthreads(); // shape tables in LDS
+  if (in_wave)
 #pragma unroll
     for (int c = 0; c < nc; ++c)
       A[c * nq + p] = u[c];
-  __syncthreads();
+  wave_sync();
 
   // ---- evaluate: values at q (dim sweeps with S)
   T *in = A, *out = B;
 #pragma unroll
   for (int ax = 0; ax < dim; ++ax)
     {
-      if (in_block)
+      if (in_wave)
 #pragma unroll
         for (int c = 0; c < nc; ++c)
           out[c * nq + p] =
             contract<n, false>(in + c * nq, sS, pa[ax], p - pa[ax] * st[ax], st[ax]);
-      __syncthreads();
+      wave_sync();
       T *tmp = in;
       in     = out;
       out    = tmp;
     }
-  // `in` holds the values at the quadrature points
   T val[nc], gref[nc][dim];
-  if (in_block)
-#pragma unroll
-    for (int c = 0; c < nc; ++c)
-      {
-        val[c] = in[c * nq + p];
-#pragma unroll
-        for (int ax = 0; ax < dim; ++ax)
-          gref[c][ax] = contract<n, false>(in + c * nq, sD, pa[ax], p - pa[ax] * st[ax], st[ax]);
-      }
-  __syncthreads();
-
-  // ---- q-point physics
-  T vhat[nc], ghat[nc][dim];
 #pragma unroll
   for (int c = 0; c < nc; ++c)
     {
-      vhat[c] = 0;
+      val[c] = in[c * nq + p];
 #pragma unroll
       for (int ax = 0; ax < dim; ++ax)
-        ghat[c][ax] = 0;
+        gref[c][ax] = contract<n, false>(in + c * nq, sD, pa[ax], p - pa[ax] * st[ax], st[ax]);
     }
-  if (active)
+  wave_sync();
+
+  // ---- q-point physics
+  T gu[dim][dim], gp[dim];
+#pragma unroll
+  for (int c = 0; c < nc; ++c)
+#pragma unroll
+    for (int e = 0; e < dim; ++e)
+      {
+        T s = 0;
+#pragma unroll
+        for (int i = 0; i < dim; ++i)
+          s += g.inv[i][e] * gref[c][i];
+        if (c < dim)
+          gu[c][e] = s;
+        else
+          gp[e] = s;
+      }
+  T vr[nc], gr[nc][dim];
+  qpoint_physics<dim, T, MODE>(val, val[dim], gu, gp, U, GU, GP, UT, oldg, d1, d2, a.nu, a.w0,
+                               a.theta, a.td, a.have_prev, a.have_old_grad, vr, gr);
+  // submit_value / submit_gradient (JxW, J^{-T}); inactive lanes have JxW 0
+  T vhat[nc];
+#pragma unroll
+  for (int c = 0; c < nc; ++c)
     {
-      QGeo<dim, n, T> g;
-      load_geometry<dim, n, T>(a, cell, p, px, py, pz, sw, g);
-      T gu[dim][dim], gp[dim];
+      vhat[c] = vr[c] * g.JxW;
 #pragma unroll
-      for (int c = 0; c < nc; ++c)
-#pragma unroll
-        for (int e = 0; e < dim; ++e)
-          {
-            T s = 0;
-#pragma unroll
-            for (int i = 0; i < dim; ++i)
-              s += g.inv[i][e] * gref[c][i];
-            if (c < dim)
-              gu[c][e] = s;
-            else
-              gp[e] = s;
-          }
-      const int64_t q  = cell * nq + p;
-      const int64_t ts = a.tab_stride;
-      T             U[dim], GU[dim][dim], GP[dim], UT[dim], oldg[dim * dim + dim];
-#pragma unroll
-      for (int d = 0; d < dim; ++d)
+      for (int i = 0; i < dim; ++i)
         {
-          U[d] = a.tab[(F::U + d) * ts + q];
+          T s = 0;
 #pragma unroll
           for (int e = 0; e < dim; ++e)
-            GU[d][e] = MODE == MODE_NEWTON ? a.tab[(F::GU + d * dim + e) * ts + q] : T(0);
-          GP[d] = MODE == MODE_NEWTON ? a.tab[(F::GP + d) * ts + q] : T(0);
-          UT[d] = ((MODE == MODE_NEWTON && a.td) || (MODE == MODE_RESIDUAL && a.have_prev)) ?
-                    a.tab[(F::UT + d) * ts + q] :
-                    T(0);
-        }
-#pragma unroll
-      for (int i = 0; i < dim * dim + dim; ++i)
-        oldg[i] = (MODE == MODE_RESIDUAL && a.have_old_grad) ? a.old_grad[i * ts + q] : T(0);
-      const T d1 = a.cw ? a.cellwise[cell] : a.tab[F::D1 * ts + q];
-      const T d2 = a.cw ? a.cellwise[a.n_cells + cell] : a.tab[F::D2 * ts + q];
-      T       vr[nc], gr[nc][dim];
-      qpoint_physics<dim, T, MODE>(val, val[dim], gu, gp, U, GU, GP, UT, oldg, d1, d2,
-                                   a.nu, a.w0, a.theta, a.td, a.have_prev, a.have_old_grad, vr,
-                                   gr);
-      // submit_value / submit_gradient: JxW and J^{-T}
-#pragma unroll
-      for (int c = 0; c < nc; ++c)
-        {
-          vhat[c] = vr[c] * g.JxW;
-#pragma unroll
-          for (int i = 0; i < dim; ++i)
-            {
-              T s = 0;
-#pragma unroll
-              for (int e = 0; e < dim; ++e)
-                s += g.inv[i][e] * gr[c][e];
-              ghat[c][i] = s * g.JxW;
-            }
+            s += g.inv[i][e] * gr[c][e];
+          if (in_wave)
+            A[(c * dim + i) * nq + p] = s * g.JxW;
         }
     }
+  wave_sync();
   // ---- integrate: gradient part via Dq^T, then S^T sweeps
-  if (in_block)
+  T wq[nc];
 #pragma unroll
-    for (int c = 0; c < nc; ++c)
+  for (int c = 0; c < nc; ++c)
+    {
+      T s = vhat[c];
 #pragma unroll
       for (int ax = 0; ax < dim; ++ax)
-        A[(c * dim + ax) * nq + p] = ghat[c][ax];
-  __syncthreads();
-  T wq[nc];
-  if (in_block)
-#pragma unroll
-    for (int c = 0; c < nc; ++c)
-      {
-        T s = vhat[c];
-#pragma unroll
-        for (int ax = 0; ax < dim; ++ax)
-          s += contract<n, true>(A + (c * dim + ax) * nq, sD, pa[ax], p - pa[ax] * st[ax], st[ax]);
-        wq[c] = s;
-      }
-  __syncthreads();
-  if (in_block)
+        s += contract<n, true>(A + (c * dim + ax) * nq, sD, pa[ax], p - pa[ax] * st[ax], st[ax]);
+      wq[c] = s;
+    }
+  wave_sync();
+  if (in_wave)
 #pragma unroll
     for (int c = 0; c < nc; ++c)
       A[c * nq + p] = wq[c];
-  __syncthreads();
+  wave_sync();
   in  = A;
   out = B;
 #pragma unroll
   for (int ax = dim - 1; ax >= 0; --ax)
     {
-      if (in_block)
+      if (in_wave)
 #pragma unroll
         for (int c = 0; c < nc; ++c)
           out[c * nq + p] =
             contract<n, true>(in + c * nq, sS, pa[ax], p - pa[ax] * st[ax], st[ax]);
-      __syncthreads();
+      wave_sync();
       T *tmp = in;
       in     = out;
       out    = tmp;
@@ -536,7 +612,12 @@ __global__ void __launch_bounds__(BLOCK)
         if (!((cm >> c) & 1))
           {
             const T r = in[c * nq + p];
-            unsafeAtomicAdd(a.dst + (size_t)node * nc + c, MODE == MODE_RESIDUAL ? -r : r);
+            if (GLS_ABL & 2)
+              asm volatile("" ::"v"(r));
+            else if (GLS_ABL & 1)
+              a.dst[(size_t)node * nc + c] += r;
+            else
+              unsafeAtomicAdd(a.dst + (size_t)node * nc + c, MODE == MODE_RESIDUAL ? -r : r);
           }
     }
 }

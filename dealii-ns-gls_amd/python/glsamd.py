@@ -59,7 +59,7 @@ def lib_path():
 def lib():
     global _lib
     if _lib is None:
-        path = lib_path()
+        path = os.environ.get("GLS_AMD_LIB") or lib_path()
         if not os.path.exists(path):
             raise RuntimeError(f"{path} missing: run `make amd` (or __graft_entry__.build())")
         L = C.CDLL(path)
