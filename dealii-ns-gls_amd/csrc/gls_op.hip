@@ -3,6 +3,7 @@
 // constrained-component bits, per-q tables), and the launch functions for the
 // vmult / residual / diagonal / table-producer kernels of kernels.h.
 #include "../../include/gls_op.h"
+#include "brick.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -118,6 +119,16 @@ struct glsOp_
   uint32_t *d_cbits    = nullptr;
   int       device     = 0;
 
+  // brick decomposition (csrc/brick.h)
+  bool      use_brick = false;
+  int       bx = 1, by = 1, bz = 1, L = 0, Lx = 0, Ly = 0;
+  int64_t   n_bricks = 0, n_slots = 0, n_shared = 0;
+  uint32_t *d_brick_nodes  = nullptr;
+  uint32_t *d_brick_target = nullptr;
+  uint32_t *d_shared_nodes = nullptr;
+  uint32_t *d_shared_off   = nullptr;
+  void     *d_partial      = nullptr;
+
   size_t
   tsize() const
   {
@@ -141,6 +152,127 @@ std::vector<T>
 convert(const std::vector<double> &v)
 {
   return std::vector<T>(v.begin(), v.end());
+}
+
+// host twin of gls::qindex (kernels.h): [plane][cell][line] position of q
+// point p of `cell`
+int64_t
+host_qindex(int dim, int n, int64_t cell, int p, int64_t ncell)
+{
+  const int lpc = dim == 3 ? n * n : n;
+  return ((int64_t)(p / lpc) * ncell + cell) * lpc + (p % lpc);
+}
+
+// Brick decomposition: node lattice per brick, exclusive vs shared nodes,
+// partial slots and the CSR that k_shared_reduce walks.
+void
+build_bricks(glsOp_ *op, const glsOpDesc *d)
+{
+  const int dim = op->dim, k = op->degree, n = k + 1;
+  const int bx = d->brick[0], by = d->brick[1], bz = dim == 3 ? d->brick[2] : 1;
+  if (bx <= 0 || by <= 0 || bz <= 0)
+    return;
+  const int64_t cpb = (int64_t)bx * by * bz;
+  if (d->n_cells % cpb != 0)
+    throw std::runtime_error("gls_op_create: n_cells is not a multiple of the brick size");
+  const int Lx = k * bx + 1, Ly = k * by + 1, Lz = dim == 3 ? k * bz + 1 : 1;
+  const int L  = Lx * Ly * Lz;
+  const int side_max = k * (dim == 3 ? 4 : 8) + 1;
+  const int lmax     = dim == 3 ? side_max * side_max * side_max : side_max * side_max;
+  if (L > lmax || lmax > 729 || (dim == 3 && (bx > 4 || by > 4 || bz > 4)) ||
+      (dim == 2 && (bx > 8 || by > 8)))
+    return; // lattice does not fit the brick kernel's LDS: per-cell path
+  const int64_t nb = d->n_cells / cpb;
+  const int     nq = op->nq;
+  std::vector<uint32_t> bnodes((size_t)nb * L, UINT32_MAX);
+  for (int64_t b = 0; b < nb; ++b)
+    for (int64_t lc = 0; lc < cpb; ++lc)
+      {
+        const int     cx = (int)(lc % bx), cy = (int)((lc / bx) % by), cz = (int)(lc / (bx * by));
+        const int64_t cell = b * cpb + lc;
+        for (int p = 0; p < nq; ++p)
+          {
+            const int i = p % n, j = (p / n) % n, l = dim == 3 ? p / (n * n) : 0;
+            const int li = (cx * k + i) + Lx * ((cy * k + j) + Ly * (cz * k + l));
+            const uint32_t node = d->cell_nodes[cell * nq + p];
+            uint32_t      &s    = bnodes[(size_t)b * L + li];
+            if (s == UINT32_MAX)
+              s = node;
+            else if (s != node)
+              throw std::runtime_error("gls_op_create: cells do not form the declared bricks "
+                                       "(shared lattice nodes differ)");
+          }
+      }
+  // brick multiplicity of each node
+  std::vector<uint32_t> mult((size_t)d->n_nodes, 0), last((size_t)d->n_nodes, UINT32_MAX);
+  for (int64_t b = 0; b < nb; ++b)
+    for (int i = 0; i < L; ++i)
+      {
+        const uint32_t node = bnodes[(size_t)b * L + i];
+        if (last[node] != (uint32_t)b)
+          {
+            last[node] = (uint32_t)b;
+            mult[node]++;
+          }
+      }
+  // targets: exclusive owned nodes -> node id; every other node is "shared":
+  // its per-brick partials occupy a contiguous slot range [off[s], off[s+1])
+  // in node order, so k_shared_reduce reads one contiguous run per node.
+  // Owned nodes no brick touches get an empty range (identity / zero row).
+  std::vector<uint32_t> target((size_t)nb * L);
+  std::vector<int64_t>  shared_index((size_t)d->n_nodes, -1);
+  std::vector<uint32_t> shared_nodes;
+  for (int64_t node = 0; node < d->n_nodes; ++node)
+    {
+      const bool owned  = node < d->n_owned_nodes;
+      const bool shared = mult[node] > 1                 // brick boundary
+                          || (!owned && mult[node] > 0)  // ghost partial sums
+                          || (owned && mult[node] == 0); // untouched owned row
+      if (shared)
+        {
+          shared_index[node] = (int64_t)shared_nodes.size();
+          shared_nodes.push_back((uint32_t)node);
+        }
+    }
+  std::vector<uint32_t> off(shared_nodes.size() + 1, 0);
+  for (size_t s = 0; s < shared_nodes.size(); ++s)
+    off[s + 1] = off[s] + mult[shared_nodes[s]];
+  const uint64_t n_slot_total = off.back();
+  if (n_slot_total >= SHARED_BIT)
+    throw std::runtime_error("gls_op_create: too many partial slots");
+  std::vector<uint32_t> fill(shared_nodes.size(), 0);
+  for (int64_t b = 0; b < nb; ++b)
+    {
+      // a node appears once per brick lattice
+      for (int i = 0; i < L; ++i)
+        {
+          const uint32_t node = bnodes[(size_t)b * L + i];
+          const int64_t  s    = shared_index[node];
+          if (s < 0)
+            target[(size_t)b * L + i] = node;
+          else
+            target[(size_t)b * L + i] = SHARED_BIT | (off[s] + fill[s]++);
+        }
+    }
+  const uint32_t slot = (uint32_t)n_slot_total;
+  // packed node | cmask for the gather and the reduction
+  for (auto &v : bnodes)
+    v |= (uint32_t)(d->node_cmask[v] & 0xF) << 28;
+  for (auto &v : shared_nodes)
+    v |= (uint32_t)(d->node_cmask[v] & 0xF) << 28;
+
+  op->use_brick = true;
+  op->bx = bx, op->by = by, op->bz = bz;
+  op->L = L, op->Lx = Lx, op->Ly = Ly;
+  op->n_bricks = nb;
+  op->n_slots  = slot;
+  op->n_shared = (int64_t)shared_nodes.size();
+  upload((void **)&op->d_brick_nodes, bnodes);
+  upload((void **)&op->d_brick_target, target);
+  upload((void **)&op->d_shared_nodes, shared_nodes);
+  upload((void **)&op->d_shared_off, off);
+  HIP_THROW(hipMalloc(&op->d_partial,
+                      std::max<size_t>(1, (size_t)slot * (dim + 1) * op->tsize())));
 }
 
 // geometry of one cell at all q: J[d][a] = dx_d / dxi_a by sum factorisation
@@ -287,6 +419,69 @@ struct Impl
     HIP_THROW(hipGetLastError());
   }
 
+  // brick kernel + shared-node reduction: dst fully (over)written
+  static void
+  brick(const glsOp_ *op, int mode, void *dst, const void *src, hipStream_t s)
+  {
+    if constexpr (BrickLattice<dim, k>::fits)
+      {
+        BrickArgs<T, dim, n> a;
+        a.brick_nodes   = op->d_brick_nodes;
+        a.brick_target  = op->d_brick_target;
+        a.cell_geo      = op->d_cell_geo;
+        a.geo_cart      = (const T *)op->d_geo_cart;
+        a.n_cart        = op->n_cart;
+        a.geo_gen       = (const T *)op->d_geo_gen;
+        a.n_gen         = op->n_gen;
+        a.tab           = (const T *)op->d_tab;
+        a.n_cells       = op->n_cells;
+        a.cellwise      = (const T *)op->d_cellwise;
+        a.old_grad      = (const T *)op->d_old_grad;
+        a.dst           = (T *)dst;
+        a.src           = (const T *)src;
+        a.partial       = (T *)op->d_partial;
+        a.brick_begin   = 0;
+        a.brick_end     = op->n_bricks;
+        a.bx            = op->bx;
+        a.by            = op->by;
+        a.bz            = op->bz;
+        a.L             = op->L;
+        a.Lx            = op->Lx;
+        a.Ly            = op->Ly;
+        a.nu            = (T)op->prm.nu;
+        a.w0            = (T)op->prm.w0;
+        a.theta         = (T)op->prm.theta;
+        a.td            = ((op->prm.flags & GLS_CONSIDER_TIME_DERIVATIVE) && op->prm.order > 0);
+        a.cw            = (op->prm.flags & GLS_CELL_WISE_STAB) ? 1 : 0;
+        a.have_prev     = op->have_prev ? 1 : 0;
+        a.have_old_grad = (op->have_old_grad && op->prm.theta != 1.0) ? 1 : 0;
+        a.sh            = make_shape<T, n>(op->basis);
+        const dim3 grid((unsigned)op->n_bricks);
+        if (mode == MODE_NEWTON)
+          hipLaunchKernelGGL((k_brick<dim, k, T, MODE_NEWTON>), grid, dim3(BLOCK), 0, s, a);
+        else if (mode == MODE_FIXED)
+          hipLaunchKernelGGL((k_brick<dim, k, T, MODE_FIXED>), grid, dim3(BLOCK), 0, s, a);
+        else
+          hipLaunchKernelGGL((k_brick<dim, k, T, MODE_RESIDUAL>), grid, dim3(BLOCK), 0, s, a);
+        HIP_THROW(hipGetLastError());
+        if (op->n_shared > 0)
+          {
+            const dim3 g2((unsigned)((op->n_shared * (dim + 1) + 255) / 256));
+            if (mode == MODE_RESIDUAL)
+              hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, true>), g2, dim3(256), 0, s,
+                                 (T *)dst, (const T *)src, (const T *)op->d_partial,
+                                 op->d_shared_nodes, op->d_shared_off, op->n_shared);
+            else
+              hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, false>), g2, dim3(256), 0, s,
+                                 (T *)dst, (const T *)src, (const T *)op->d_partial,
+                                 op->d_shared_nodes, op->d_shared_off, op->n_shared);
+            HIP_THROW(hipGetLastError());
+          }
+      }
+    else
+      throw std::runtime_error("brick kernel not available for this (dim, degree)");
+  }
+
   static void
   produce(const glsOp_ *op, int what, const void *vec, hipStream_t s)
   {
@@ -352,6 +547,32 @@ select(const glsOp_ *op, ApplyFn &af, ProduceFn &pf)
     select_t<float>(op->dim, op->degree, af, pf);
   if (!af)
     throw std::runtime_error("no kernel instantiation for this (dim, degree)");
+}
+
+using BrickFn = void (*)(const glsOp_ *, int, void *, const void *, hipStream_t);
+
+template <typename T>
+BrickFn
+select_brick_t(int dim, int k)
+{
+#define GLS_CASE(D, K)     \
+  if (dim == D && k == K)  \
+    return &Impl<D, K, T>::brick;
+  GLS_CASE(2, 1)
+  GLS_CASE(2, 2)
+  GLS_CASE(2, 3)
+  GLS_CASE(3, 1)
+  GLS_CASE(3, 2)
+  GLS_CASE(3, 3)
+#undef GLS_CASE
+  return nullptr;
+}
+
+BrickFn
+select_brick(const glsOp_ *op)
+{
+  return op->prec == GLS_F64 ? select_brick_t<double>(op->dim, op->degree) :
+                               select_brick_t<float>(op->dim, op->degree);
 }
 
 int
@@ -513,10 +734,13 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
     for (int f = 0; f < ncf; ++f)
       cart[(size_t)f * n_cart + i] = cart_rows[(size_t)i * ncf + f];
   gen.resize((size_t)ngf * n_gen * nq);
-  for (int64_t i = 0; i < n_gen * nq; ++i)
-    for (int f = 0; f < ngf; ++f)
-      gen[(size_t)f * n_gen * nq + i] = gen_rows[(size_t)i * ngf + f];
+  for (int64_t g = 0; g < n_gen; ++g)
+    for (int q = 0; q < nq; ++q)
+      for (int f = 0; f < ngf; ++f)
+        gen[(size_t)f * n_gen * nq + host_qindex(dim, n, g, q, n_gen)] =
+          gen_rows[((size_t)g * nq + q) * ngf + f];
   upload((void **)&op->d_cell_geo, cell_geo);
+  build_bricks(op, d);
 
   std::vector<double> hq((size_t)d->n_cells), hmin((size_t)d->n_cells);
   for (int64_t c = 0; c < d->n_cells; ++c)
@@ -558,8 +782,11 @@ gls_op_destroy(glsOp op)
 {
   if (!op)
     return;
-  void *bufs[] = {op->d_nodes, op->d_cell_geo, op->d_geo_cart, op->d_geo_gen, op->d_tab,
-                  op->d_cellwise, op->d_old_grad, op->d_hq, op->d_hmin, op->d_tmp, op->d_cbits};
+  void *bufs[] = {op->d_nodes,        op->d_cell_geo,     op->d_geo_cart,     op->d_geo_gen,
+                  op->d_tab,          op->d_cellwise,     op->d_old_grad,     op->d_hq,
+                  op->d_hmin,         op->d_tmp,          op->d_cbits,        op->d_brick_nodes,
+                  op->d_brick_target, op->d_shared_nodes, op->d_shared_off,
+                  op->d_partial};
   for (void *b : bufs)
     if (b)
       (void)hipFree(b);
@@ -697,8 +924,13 @@ gls_op_vmult(glsOp op, void *dst, const void *src, void *stream)
   ProduceFn pf;
   select(op, af, pf);
   hipStream_t s = (hipStream_t)stream;
-  init_dst(op, dst, src, s);
-  af(op, vmult_mode(op), false, dst, src, 0, op->n_cells, s);
+  if (op->use_brick)
+    select_brick(op)(op, vmult_mode(op), dst, src, s);
+  else
+    {
+      init_dst(op, dst, src, s);
+      af(op, vmult_mode(op), false, dst, src, 0, op->n_cells, s);
+    }
   GLS_CATCH
 }
 
@@ -714,8 +946,13 @@ gls_op_evaluate_residual(glsOp op, void *dst, const void *src, void *stream)
   ProduceFn pf;
   select(op, af, pf);
   hipStream_t s = (hipStream_t)stream;
-  HIP_THROW(hipMemsetAsync(dst, 0, (size_t)op->n_dofs * op->tsize(), s));
-  af(op, MODE_RESIDUAL, false, dst, src, 0, op->n_cells, s);
+  if (op->use_brick)
+    select_brick(op)(op, MODE_RESIDUAL, dst, src, s);
+  else
+    {
+      HIP_THROW(hipMemsetAsync(dst, 0, (size_t)op->n_dofs * op->tsize(), s));
+      af(op, MODE_RESIDUAL, false, dst, src, 0, op->n_cells, s);
+    }
   GLS_CATCH
 }
 
@@ -751,9 +988,11 @@ gls_op_upload_tables(glsOp op, const double *tables, const double *cellwise)
     throw std::runtime_error("gls_op_upload_tables: null argument");
   const int64_t       m = op->n_cells * op->nq;
   std::vector<double> soa((size_t)op->nf * m);
-  for (int64_t i = 0; i < m; ++i)
-    for (int f = 0; f < op->nf; ++f)
-      soa[(size_t)f * m + i] = tables[(size_t)i * op->nf + f];
+  for (int64_t c = 0; c < op->n_cells; ++c)
+    for (int q = 0; q < op->nq; ++q)
+      for (int f = 0; f < op->nf; ++f)
+        soa[(size_t)f * m + host_qindex(op->dim, op->degree + 1, c, q, op->n_cells)] =
+          tables[((size_t)c * op->nq + q) * op->nf + f];
   std::vector<double> cw((size_t)2 * op->n_cells, 0.0);
   if (cellwise)
     for (int64_t c = 0; c < op->n_cells; ++c)
@@ -801,9 +1040,11 @@ gls_op_download_tables(glsOp op, double *tables, double *cellwise)
       cw.assign(cf.begin(), cf.end());
     }
   if (tables)
-    for (int64_t i = 0; i < m; ++i)
-      for (int f = 0; f < op->nf; ++f)
-        tables[(size_t)i * op->nf + f] = soa[(size_t)f * m + i];
+    for (int64_t c = 0; c < op->n_cells; ++c)
+      for (int q = 0; q < op->nq; ++q)
+        for (int f = 0; f < op->nf; ++f)
+          tables[((size_t)c * op->nq + q) * op->nf + f] =
+            soa[(size_t)f * m + host_qindex(op->dim, op->degree + 1, c, q, op->n_cells)];
   if (cellwise)
     for (int64_t c = 0; c < op->n_cells; ++c)
       {

@@ -36,6 +36,18 @@ ipow(int n, int d)
   return d == 0 ? 1 : n * ipow(n, d - 1);
 }
 
+// Per-quadrature-point arrays (tables, general geometry) are stored
+// [field][plane][cell][line]: q point p = line + LPC * plane with
+// LPC = (k+1)^(dim-1), so the lanes that own one quadrature plane of
+// consecutive cells read consecutive addresses (csrc/brick.h thread map).
+template <int dim, int n>
+__device__ __forceinline__ int64_t
+qindex(int64_t cell, int p, int64_t ncell)
+{
+  constexpr int LPC = ipow(n, dim - 1);
+  return ((int64_t)(p / LPC) * ncell + cell) * LPC + (p % LPC);
+}
+
 enum Mode
 {
   MODE_NEWTON   = 0, // vmult, increment form (Newton Jacobian)
@@ -281,7 +293,7 @@ load_geometry(const Args &a, int64_t cell, int p, int px, int py, int pz,
   const uint32_t cg = a.cell_geo[cell];
   if (cg & GEO_GENERAL)
     {
-      const int64_t idx = (int64_t)(cg & ~GEO_GENERAL) * nq + p;
+      const int64_t idx = qindex<dim, n>(cg & ~GEO_GENERAL, p, a.gen_stride / nq);
       g.JxW             = a.geo_gen[idx];
 #pragma unroll
       for (int i = 0; i < dim; ++i)
@@ -392,7 +404,7 @@ __global__ void __launch_bounds__(BLOCK)
     }
 
   // ---- prefetch geometry and per-q tables (consumed after evaluate)
-  const int64_t   q  = cell * nq + p;
+  const int64_t   q  = qindex<dim, n>(cell, p, a.n_cells);
   const int64_t   ts = a.tab_stride;
   QGeo<dim, n, T> g;
   T               U[dim], GU[dim][dim], GP[dim], UT[dim], oldg[dim * dim + dim], d1 = 0, d2 = 0;
@@ -428,7 +440,7 @@ __global__ void __launch_bounds__(BLOCK)
       const uint32_t cg = a.cell_geo[cell];
       if (cg & GEO_GENERAL)
         {
-          const int64_t idx = (int64_t)(cg & ~GEO_GENERAL) * nq + p;
+          const int64_t idx = qindex<dim, n>(cg & ~GEO_GENERAL, p, a.gen_stride / nq);
           g.JxW             = a.geo_gen[idx];
 #pragma unroll
           for (int i = 0; i < dim; ++i)
@@ -717,7 +729,7 @@ __global__ void __launch_bounds__(BLOCK)
         for (int ax = 0; ax < dim; ++ax)
           gref[c][ax] = contract<n, false>(in + c * nq, sD, pa[ax], p - pa[ax] * st[ax], st[ax]);
       }
-  const int64_t q  = cell * nq + p;
+  const int64_t q  = qindex<dim, n>(cell, p, a.n_cells);
   const int64_t ts = a.tab_stride;
   T             unorm = 0;
   if (active)

@@ -400,6 +400,51 @@ compute_face_bids(CoarseMesh &cm, double length, double height, double pos,
       }
 }
 
+// ------------------------------------------------------------ cell order
+// Inside a coarse cell refined to nsub^dim cells, cells are ordered
+// brick-major: bricks of b[d] = min(nsub, BRICK[d]) cells per direction in
+// lexicographic order, cells lexicographic inside a brick.  The operator
+// processes one brick per workgroup (see csrc/brick.h); 3D bricks are
+// 4 x 4 x 2 cells so that the headline mesh (400 coarse cells, r = 2) yields
+// 800 workgroups for the 256 CUs.
+inline void
+brick_dims(int nsub, int dim, int b[3])
+{
+  const int B[3] = {dim == 3 ? 4 : 8, dim == 3 ? 4 : 8, dim == 3 ? 2 : 1};
+  for (int d = 0; d < 3; ++d)
+    b[d] = (d < dim) ? (nsub < B[d] ? nsub : B[d]) : 1;
+}
+
+inline int64_t
+local_cell_index(int cx, int cy, int cz, int nsub, int dim)
+{
+  int b[3];
+  brick_dims(nsub, dim, b);
+  const int     nbx = nsub / b[0], nby = nsub / b[1];
+  const int64_t brick =
+    (cx / b[0]) + (int64_t)nbx * ((cy / b[1]) + (int64_t)nby * (dim == 3 ? (cz / b[2]) : 0));
+  const int64_t inner =
+    (cx % b[0]) + (int64_t)b[0] * ((cy % b[1]) + (int64_t)b[1] * (dim == 3 ? (cz % b[2]) : 0));
+  return brick * ((int64_t)b[0] * b[1] * b[2]) + inner;
+}
+
+inline void
+local_cell_coords(int64_t r, int nsub, int dim, int &cx, int &cy, int &cz)
+{
+  int b[3];
+  brick_dims(nsub, dim, b);
+  const int     nbx = nsub / b[0], nby = nsub / b[1];
+  const int64_t cpb   = (int64_t)b[0] * b[1] * b[2];
+  const int64_t brick = r / cpb, inner = r % cpb;
+  const int     bx = (int)(brick % nbx), by = (int)((brick / nbx) % nby),
+            bz = dim == 3 ? (int)(brick / ((int64_t)nbx * nby)) : 0;
+  const int ix = (int)(inner % b[0]), iy = (int)((inner / b[0]) % b[1]),
+            iz = dim == 3 ? (int)(inner / ((int64_t)b[0] * b[1])) : 0;
+  cx = bx * b[0] + ix;
+  cy = by * b[1] + iy;
+  cz = bz * b[2] + iz;
+}
+
 // ------------------------------------------------------------ fine mesh
 struct KeyHash
 {
@@ -592,12 +637,13 @@ build_fine(const CoarseMesh &cm, int degree, int n_ref, const CurvedSurface &cs)
       };
 
       const int64_t cbase = (int64_t)c * cells_per_coarse;
-      const int     sz    = dim == 3 ? nsub : 1;
-      for (int cz = 0; cz < sz; ++cz)
-        for (int cy = 0; cy < nsub; ++cy)
-          for (int cx = 0; cx < nsub; ++cx)
+      // brick-major cell order (see local_cell_index); node numbers follow
+      // first appearance in that order, so a brick's nodes are clustered
+      for (int64_t r = 0; r < cells_per_coarse; ++r)
             {
-              const int64_t cell = cbase + cx + (int64_t)nsub * (cy + (int64_t)nsub * cz);
+              int cx, cy, cz;
+              local_cell_coords(r, nsub, dim, cx, cy, cz);
+              const int64_t cell = cbase + r;
               m->cell_coarse[cell] = (int32_t)c;
               uint32_t *cn         = &m->cell_nodes[(size_t)cell * nloc];
               int       q          = 0;
@@ -865,6 +911,18 @@ gls_mesh_constraint_mask(const glsMesh *m, uint32_t vel_ids, uint32_t p_ids,
 }
 
 int
+gls_mesh_brick(const glsMesh *m, int *dims)
+{
+  if (!m || !dims)
+    {
+      g_err = "gls_mesh_brick: null argument";
+      return 1;
+    }
+  brick_dims(1 << m->n_ref, m->dim, dims);
+  return 0;
+}
+
+int
 gls_mesh_child_lattice(const glsMesh *coarse, const glsMesh *fine,
                        uint32_t *out)
 {
@@ -889,11 +947,9 @@ gls_mesh_child_lattice(const glsMesh *coarse, const glsMesh *fine,
   const int     nlat  = L * L * Lz;
   for (int64_t cell = 0; cell < coarse->n_cells; ++cell)
     {
-      const int64_t c   = cell / cpcC;
-      int64_t       r   = cell % cpcC;
-      const int     cx  = (int)(r % nsc);
-      const int     cy  = (int)((r / nsc) % nsc);
-      const int     cz  = dim == 3 ? (int)(r / ((int64_t)nsc * nsc)) : 0;
+      const int64_t c = cell / cpcC;
+      int           cx, cy, cz;
+      local_cell_coords(cell % cpcC, nsc, dim, cx, cy, cz);
       for (int l = 0; l < Lz; ++l)
         for (int j = 0; j < L; ++j)
           for (int i = 0; i < L; ++i)
@@ -901,8 +957,8 @@ gls_mesh_child_lattice(const glsMesh *coarse, const glsMesh *fine,
               const int ai = std::min(i / k, 1), aj = std::min(j / k, 1),
                         al = dim == 3 ? std::min(l / k, 1) : 0;
               const int64_t fcell =
-                c * cpcF + (2 * cx + ai) +
-                (int64_t)nsf * ((2 * cy + aj) + (int64_t)nsf * (dim == 3 ? (2 * cz + al) : 0));
+                c * cpcF + local_cell_index(2 * cx + ai, 2 * cy + aj,
+                                            dim == 3 ? 2 * cz + al : 0, nsf, dim);
               const int li = i - ai * k, lj = j - aj * k, ll = dim == 3 ? l - al * k : 0;
               const int q  = li + kp * (lj + kp * ll);
               out[cell * nlat + i + L * (j + L * l)] =

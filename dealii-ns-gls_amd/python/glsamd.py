@@ -37,7 +37,7 @@ class OpDesc(C.Structure):
                 ("n_cells", C.c_int64), ("n_nodes", C.c_int64), ("n_owned_nodes", C.c_int64),
                 ("cell_nodes", C.c_void_p), ("node_coords", C.c_void_p),
                 ("node_cmask", C.c_void_p), ("cell_measure", C.c_void_p),
-                ("cell_hmin", C.c_void_p)]
+                ("cell_hmin", C.c_void_p), ("brick", C.c_int * 3)]
 
 
 class OpParams(C.Structure):
@@ -119,7 +119,8 @@ class NavierStokesOperator:
     the HIP C-ABI.  precision: "f64" (fine level, Number=double) or "f32"
     (MG levels, MGNumber=float, config.h:6-7)."""
 
-    def __init__(self, mesh, cmask, precision="f64", cells=None, n_owned_nodes=None):
+    def __init__(self, mesh, cmask, precision="f64", cells=None, n_owned_nodes=None,
+                 brick=None):
         import torch
         if not torch.cuda.is_available():
             raise GlsError("NavierStokesOperator needs a GPU (no CPU fallback by design)")
@@ -138,10 +139,13 @@ class NavierStokesOperator:
                       np.ascontiguousarray(meas), np.ascontiguousarray(hmin)]
         k = self._keep
         self.n_cells = k[0].shape[0]
+        if brick is None:
+            brick = mesh.brick() if cells is None else (0, 0, 0)
+        self.brick = tuple(brick)
         d = OpDesc(self.dim, self.degree, self.prec, self.n_cells, mesh.n_nodes,
                    mesh.n_nodes if n_owned_nodes is None else n_owned_nodes,
                    k[0].ctypes.data, k[1].ctypes.data, k[2].ctypes.data, k[3].ctypes.data,
-                   k[4].ctypes.data)
+                   k[4].ctypes.data, (C.c_int * 3)(*self.brick))
         h = C.c_void_p()
         _check(lib().gls_op_create(C.byref(d), C.byref(h)))
         self.h = h

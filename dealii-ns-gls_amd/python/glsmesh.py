@@ -44,6 +44,7 @@ def lib():
         L.gls_mesh_constraint_mask.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, vp]
         L.gls_mesh_child_lattice.argtypes = [vp, vp, vp]
         L.gls_mesh_cell_measure.argtypes = [vp, vp, vp]
+        L.gls_mesh_brick.argtypes = [vp, vp]
         L.gls_mesh_last_error.restype = C.c_char_p
         _lib = L
     return _lib
@@ -105,6 +106,12 @@ class Mesh:
         _check(lib().gls_mesh_constraint_mask(self._h, bits(vel_ids), bits(p_ids),
                                               bits(slip_ids), out.ctypes.data))
         return out
+
+    def brick(self):
+        """(bx, by, bz): cells per brick (gls_mesh_brick)."""
+        dims = (C.c_int * 3)()
+        _check(lib().gls_mesh_brick(self._h, dims))
+        return tuple(dims)
 
     def cell_measure(self):
         meas = np.zeros(self.n_cells)

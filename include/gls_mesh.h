@@ -81,6 +81,13 @@ int gls_mesh_constraint_mask(const glsMesh *m, uint32_t vel_ids,
                              uint32_t p_ids, uint32_t slip_ids,
                              uint8_t *out);
 
+/* Cells are ordered brick-major inside every coarse cell: bricks of
+ * dims[0] x dims[1] x dims[2] cells (min(2^n_ref, 4) per direction in 3D,
+ * min(2^n_ref, 8) in 2D), lexicographic inside a brick, so the cell list is
+ * a sequence of equal-shape bricks — the structure hint glsOpDesc.brick
+ * takes.  Returns 0 on success. */
+int gls_mesh_brick(const glsMesh *m, int *dims);
+
 /* Child lattice for MG transfer: `coarse` and `fine` must come from the same
  * generator call parameters with fine.n_ref == coarse.n_ref + 1.  For every
  * coarse-level cell, writes the (2k+1)^dim fine-level node indices of the

@@ -90,6 +90,12 @@ typedef struct
   const uint8_t  *node_cmask; /* host [n_nodes] constrained component bits    */
   const double   *cell_measure;     /* host [n_cells] vertex measure |K|      */
   const double   *cell_hmin;        /* host [n_cells] min vertex distance     */
+  int             brick[3];   /* structure hint: the cell list is a sequence
+                                 of bricks of brick[0]*brick[1]*brick[2]
+                                 cells, lexicographic inside a brick, sharing
+                                 nodes like a structured block (as produced by
+                                 gls_mesh_brick).  {0,0,0}: no structure —
+                                 every cell is its own brick.               */
 } glsOpDesc;
 
 typedef struct
