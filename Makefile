@@ -15,6 +15,9 @@ CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
 HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics \
             -Wall -Wno-unused-parameter -Wno-unused-function
 
+# rocsolver/rocblas: dense LU of the coarse multigrid level only
+AMD_LIBS := -L/opt/rocm/lib -lrocsolver -lrocblas -Wl,-rpath,/opt/rocm/lib
+
 MESH_SRC := $(PKG)/host/mesh.cc
 AMD_SRC  := $(wildcard $(PKG)/csrc/*.hip) $(wildcard $(PKG)/csrc/*.cc)
 AMD_HDR  := $(wildcard $(PKG)/csrc/*.h) $(wildcard $(PKG)/csrc/*.cuh) include/gls_op.h
@@ -32,7 +35,7 @@ $(LIBDIR)/libglsmesh.so: $(MESH_SRC) include/gls_mesh.h
 
 $(LIBDIR)/libglsamd.so: $(AMD_SRC) $(AMD_HDR)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(AMD_SRC)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(AMD_SRC) $(AMD_LIBS)
 
 clean:
 	rm -f $(LIBDIR)/*.so
@@ -43,5 +46,5 @@ clean:
 # diagnostic ablation builds (timing only, wrong results by design)
 abl:
 	@mkdir -p $(LIBDIR)/abl
-	for v in 1 2 4 8 14; do $(HIPCC) $(HIPFLAGS) -DGLS_ABL=$$v -shared -o $(LIBDIR)/abl/libglsamd_abl$$v.so $(AMD_SRC) & done; wait
+	for v in 1 2 4 8 14; do $(HIPCC) $(HIPFLAGS) -DGLS_ABL=$$v -shared -o $(LIBDIR)/abl/libglsamd_abl$$v.so $(AMD_SRC) $(AMD_LIBS) & done; wait
 .PHONY: abl

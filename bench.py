@@ -55,7 +55,7 @@ def cpu_baseline(case_mesh, cmask, params, weights, u_star, hist, src, n_dofs, b
         o.vmult(src)
         reps += 1
         el = time.perf_counter() - t0
-        if el > budget_s or reps >= 50:
+        if el > budget_s:
             break
     return dict(value=n_dofs * reps / el, unit="DoF/s", cores=threads, kind="port",
                 sample=f"{reps} full FP64 Newton vmults of the same Re3900 mesh "
@@ -71,7 +71,7 @@ def main():
     ap.add_argument("--nref", type=int, default=None)
     ap.add_argument("--precision", default="f64")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
     args = ap.parse_args()
 
     import torch
@@ -105,9 +105,14 @@ def main():
         src = runner.scatter_global(src_h)
         dst = runner.new_vector()
         apply_fn = lambda: runner.vmult(dst, src)  # noqa: E731
-        kernel_fn = None
         local_cells = runner.n_local_cells
         op = runner.op
+
+        def kernel_fn(ev0, ev1):
+            # rank-local cell loop (k_brick + k_shared_reduce), no exchange
+            ev0.record()
+            op.vmult(dst, src)
+            ev1.record()
     else:
         op = glsamd.NavierStokesOperator(mesh, cmask, args.precision)
         op.set_parameters(**params)
@@ -198,7 +203,8 @@ def main():
                        "parallelism": f"cells x-slab partitioned over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
-                         "kernel": "gls::k_apply<3,2,double,MODE_NEWTON>",
+                         "kernel": "vmult = gls::k_brick<3,2,double,MODE_NEWTON> + "
+                                   "gls::k_shared_reduce (both inside the events)",
                          "kernel_ms": kernel_ms, "algorithmic_bytes": bytes_per_vmult},
             "cpu_baseline": cpu,
         }

@@ -6,6 +6,7 @@
 #include "brick.h"
 #include "common.h"
 #include "kernels.h"
+#include "op_internal.h"
 
 #include <algorithm>
 #include <cmath>
@@ -93,48 +94,7 @@ Basis1D::Basis1D(int k)
 
 } // namespace gls
 
-// ------------------------------------------------------------ operator state
-struct glsOp_
-{
-  int     dim = 3, degree = 2, prec = GLS_F64;
-  int64_t n_cells = 0, n_nodes = 0, n_owned_nodes = 0, n_dofs = 0, n_owned_dofs = 0;
-  int     nq = 0, nf = 0;
-  Basis1D basis{1};
-
-  glsOpParams prm{};
-  bool        have_lin = false, have_prev = false, have_old_grad = false;
-
-  int64_t n_gen = 0, n_cart = 0;
-  // device buffers
-  uint32_t *d_nodes    = nullptr;
-  uint32_t *d_cell_geo = nullptr;
-  void     *d_geo_cart = nullptr;
-  void     *d_geo_gen  = nullptr;
-  void     *d_tab      = nullptr;
-  void     *d_cellwise = nullptr;
-  void     *d_old_grad = nullptr;
-  void     *d_hq       = nullptr;
-  void     *d_hmin     = nullptr;
-  void     *d_tmp      = nullptr;
-  uint32_t *d_cbits    = nullptr;
-  int       device     = 0;
-
-  // brick decomposition (csrc/brick.h)
-  bool      use_brick = false;
-  int       bx = 1, by = 1, bz = 1, L = 0, Lx = 0, Ly = 0;
-  int64_t   n_bricks = 0, n_slots = 0, n_shared = 0;
-  uint32_t *d_brick_nodes  = nullptr;
-  uint32_t *d_brick_target = nullptr;
-  uint32_t *d_shared_nodes = nullptr;
-  uint32_t *d_shared_off   = nullptr;
-  void     *d_partial      = nullptr;
-
-  size_t
-  tsize() const
-  {
-    return prec == GLS_F64 ? 8 : 4;
-  }
-};
+// operator state: struct glsOp_ in op_internal.h
 
 namespace
 {
@@ -656,6 +616,8 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
       nodes[i] = nd | ((uint32_t)(d->node_cmask[nd] & 0xF) << 28);
     }
   upload((void **)&op->d_nodes, nodes);
+  op->h_cmask.assign(d->node_cmask, d->node_cmask + d->n_nodes);
+  op->h_cell_nodes.assign(d->cell_nodes, d->cell_nodes + (size_t)d->n_cells * nq);
 
   // constrained dof bitmask on the owned range (identity rows)
   std::vector<uint32_t> cbits((size_t)(op->n_owned_dofs + 31) / 32 + 1, 0u);
@@ -890,6 +852,25 @@ gls_op_vmult_init(glsOp op, void *dst, const void *src, void *stream)
   if (!op || !dst || !src)
     throw std::runtime_error("gls_op_vmult_init: null argument");
   init_dst(op, dst, src, (hipStream_t)stream);
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_apply_identity_rows(glsOp op, void *dst, const void *src, void *stream)
+{
+  GLS_TRY
+  if (!op || !dst || !src)
+    throw std::runtime_error("gls_op_apply_identity_rows: null argument");
+  if (op->n_owned_dofs == 0)
+    return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (op->prec == GLS_F64)
+    hipLaunchKernelGGL(k_identity_rows<double>, grid1d(op->n_owned_dofs), dim3(256), 0, s,
+                       (double *)dst, (const double *)src, op->d_cbits, op->n_owned_dofs);
+  else
+    hipLaunchKernelGGL(k_identity_rows<float>, grid1d(op->n_owned_dofs), dim3(256), 0, s,
+                       (float *)dst, (const float *)src, op->d_cbits, op->n_owned_dofs);
+  HIP_THROW(hipGetLastError());
   GLS_CATCH
 }
 

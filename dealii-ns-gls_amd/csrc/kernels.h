@@ -846,6 +846,18 @@ k_init_dst(T *__restrict__ dst, const T *__restrict__ src, const uint32_t *__res
   dst[i] = v;
 }
 
+// dst[i] = src[i] on constrained owned dofs only (identity rows re-applied
+// after the ghost export-add of a distributed vmult)
+template <typename T>
+__global__ void
+k_identity_rows(T *__restrict__ dst, const T *__restrict__ src,
+                const uint32_t *__restrict__ cbits, int64_t n_owned)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_owned && ((cbits[i >> 5] >> (i & 31)) & 1))
+    dst[i] = src[i];
+}
+
 template <typename T>
 __global__ void
 k_fill(T *__restrict__ dst, T v, int64_t n)

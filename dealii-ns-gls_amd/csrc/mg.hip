@@ -1,23 +1,780 @@
-// mg.hip — geometric multigrid (placeholder until the MG kernels land)
+// mg.hip — geometric multigrid on the GPU: level transfer (MGTwoLevelTransfer
+// semantics, main.cc:538-563), damped-Jacobi relaxation smoother with a
+// power-iteration relaxation factor (PreconditionRelaxation with
+// relaxation = 0, multigrid.cc:281-369 — NOT Chebyshev), and the
+// V-cycle of PreconditionMG / Multigrid (multigrid.cc:202-220, 534-548).
+//
+// Transfer between level l-1 (coarse) and l (fine), per coarse cell, with
+// P the 1D interpolation of the parent's Q_k basis to the (2k+1) child
+// lattice points:
+//   prolongate_add: dst_f += w_f * (P x P x P) (Z_c src_c)
+//   restrict_add:   dst_c += Z_c (P x P x P)^T (w_f * src_f)
+// Z_c zeroes constrained coarse dofs, w_f = 1/valence on unconstrained fine
+// dofs and 0 on constrained ones; interpolate = nodal injection (nested GLL
+// nodes, k <= 2).
 #include "../../include/gls_op.h"
 #include "common.h"
+#include "kernels.h"
+#include "op_internal.h"
+
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
+#include <cmath>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+using namespace gls;
+
+namespace
+{
+constexpr int MAXP = 2 * 3 + 1; // (2k+1) for k <= 3
+constexpr int MAXN = 4;
+
+template <typename T>
+struct TransferArgs
+{
+  const uint32_t *coarse_nodes; // [cells_c][nq] node | cmask << 28
+  const uint32_t *child;        // [cells_c][nl] fine node ids
+  const T        *weight;       // [n_dofs_f]
+  int64_t         n_cells_c;
+  T               P[MAXP][MAXN];
+};
+
+template <int dim, int k, typename T>
+__global__ void __launch_bounds__(256)
+  k_prolongate(TransferArgs<T> a, T *__restrict__ dst_f, const T *__restrict__ src_c)
+{
+  constexpr int n = k + 1, nq = ipow(n, dim), nc = dim + 1, L = 2 * k + 1;
+  constexpr int nl = ipow(L, dim);
+  __shared__ T  u[nc][nq];
+  const int64_t c = blockIdx.x;
+  const int     t = threadIdx.x;
+  if (t < nq)
+    {
+      const uint32_t packed = a.coarse_nodes[c * nq + t];
+      const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
+#pragma unroll
+      for (int comp = 0; comp < nc; ++comp)
+        u[comp][t] = ((cm >> comp) & 1) ? T(0) : src_c[(size_t)node * nc + comp];
+    }
+  __syncthreads();
+  for (int I = t; I < nl; I += blockDim.x)
+    {
+      const int      Ix = I % L, Iy = (I / L) % L, Iz = dim == 3 ? I / (L * L) : 0;
+      const uint32_t fn = a.child[c * nl + I];
+#pragma unroll
+      for (int comp = 0; comp < nc; ++comp)
+        {
+          T s = 0;
+#pragma unroll
+          for (int i = 0; i < nq; ++i)
+            {
+              const int ix = i % n, iy = (i / n) % n, iz = dim == 3 ? i / (n * n) : 0;
+              T         p  = a.P[Ix][ix] * a.P[Iy][iy];
+              if (dim == 3)
+                p *= a.P[Iz][iz];
+              s += p * u[comp][i];
+            }
+          const T w = a.weight[(size_t)fn * nc + comp];
+          if (w != T(0))
+            unsafeAtomicAdd(dst_f + (size_t)fn * nc + comp, w * s);
+        }
+    }
+}
+
+template <int dim, int k, typename T>
+__global__ void __launch_bounds__(256)
+  k_restrict(TransferArgs<T> a, T *__restrict__ dst_c, const T *__restrict__ src_f)
+{
+  constexpr int n = k + 1, nq = ipow(n, dim), nc = dim + 1, L = 2 * k + 1;
+  constexpr int nl = ipow(L, dim);
+  __shared__ T  v[nc][nl];
+  const int64_t c = blockIdx.x;
+  const int     t = threadIdx.x;
+  for (int I = t; I < nl; I += blockDim.x)
+    {
+      const uint32_t fn = a.child[c * nl + I];
+#pragma unroll
+      for (int comp = 0; comp < nc; ++comp)
+        v[comp][I] = a.weight[(size_t)fn * nc + comp] * src_f[(size_t)fn * nc + comp];
+    }
+  __syncthreads();
+  for (int i = t; i < nq * nc; i += blockDim.x)
+    {
+      const int      ii = i % nq, comp = i / nq;
+      const uint32_t packed = a.coarse_nodes[c * nq + ii];
+      const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
+      if ((cm >> comp) & 1)
+        continue;
+      const int ix = ii % n, iy = (ii / n) % n, iz = dim == 3 ? ii / (n * n) : 0;
+      T         s  = 0;
+      for (int I = 0; I < nl; ++I)
+        {
+          const int Ix = I % L, Iy = (I / L) % L, Iz = dim == 3 ? I / (L * L) : 0;
+          T         p  = a.P[Ix][ix] * a.P[Iy][iy];
+          if (dim == 3)
+            p *= a.P[Iz][iz];
+          s += p * v[comp][I];
+        }
+      unsafeAtomicAdd(dst_c + (size_t)node * nc + comp, s);
+    }
+}
+
+// interpolate_to_mg: coarse GLL node i sits at fine lattice point 2 i (k <= 2)
+template <int dim, int k, typename T>
+__global__ void
+k_interpolate(TransferArgs<T> a, T *__restrict__ dst_c, const T *__restrict__ src_f)
+{
+  constexpr int n = k + 1, nq = ipow(n, dim), nc = dim + 1, L = 2 * k + 1;
+  constexpr int nl = ipow(L, dim);
+  const int64_t g  = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= a.n_cells_c * nq)
+    return;
+  const int64_t  c  = g / nq;
+  const int      i  = (int)(g % nq);
+  const int      ix = i % n, iy = (i / n) % n, iz = dim == 3 ? i / (n * n) : 0;
+  const int      I  = 2 * ix + L * (2 * iy + L * (dim == 3 ? 2 * iz : 0));
+  const uint32_t fn = a.child[c * nl + I];
+  const uint32_t cn = a.coarse_nodes[c * nq + i] & NODE_MASK;
+#pragma unroll
+  for (int comp = 0; comp < nc; ++comp)
+    dst_c[(size_t)cn * nc + comp] = src_f[(size_t)fn * nc + comp];
+}
+
+// ------------------------------------------------------------ vectors
+// PreconditionRelaxation with a diagonal preconditioner:
+//   first (zero start): x = omega d . b;  step: x += omega d . (b - t), t = A x
+template <typename T>
+__global__ void
+k_relax(T *__restrict__ x, const T *__restrict__ b, const T *__restrict__ t,
+        const T *__restrict__ d, T omega, int first, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  if (first)
+    x[i] = omega * d[i] * b[i];
+  else
+    x[i] += omega * d[i] * (b[i] - t[i]);
+}
+
+// t = b - t  (Multigrid residual step)
+template <typename T>
+__global__ void
+k_residual(T *__restrict__ t, const T *__restrict__ b, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    t[i] = b[i] - t[i];
+}
+
+template <typename Tin, typename Tout>
+__global__ void
+k_convert(Tout *__restrict__ dst, const Tin *__restrict__ src, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    dst[i] = (Tout)src[i];
+}
+
+// y = d . y ; sums of squares of y (after) and x into acc[0], acc[1]
+template <typename T>
+__global__ void
+k_power_step(T *__restrict__ y, const T *__restrict__ x, const T *__restrict__ d,
+             double *__restrict__ acc, int64_t n)
+{
+  const int64_t i  = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double        yy = 0, xx = 0;
+  if (i < n)
+    {
+      const T v = d[i] * y[i];
+      y[i]      = v;
+      yy        = (double)v * v;
+      xx        = (double)x[i] * x[i];
+    }
+  for (int off = 32; off > 0; off >>= 1)
+    {
+      yy += __shfl_down(yy, off);
+      xx += __shfl_down(xx, off);
+    }
+  if ((threadIdx.x & 63) == 0)
+    {
+      unsafeAtomicAdd(acc, yy);
+      unsafeAtomicAdd(acc + 1, xx);
+    }
+}
+
+template <typename T>
+__global__ void
+k_scale(T *__restrict__ x, const T *__restrict__ y, double s, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    x[i] = (T)(s * y[i]);
+}
+
+dim3
+g1(int64_t n)
+{
+  return dim3((unsigned)((n + 255) / 256));
+}
+
+} // namespace
 
 struct glsMG_
 {
+  glsMGDesc          desc{};
+  std::vector<glsOp> ops;
+  int                prec = GLS_F32, dim = 3, degree = 2, nc = 4;
+  std::vector<uint32_t *> d_child;  // level l >= 1: [cells(l-1)][nl]
+  std::vector<void *>     d_weight; // level l >= 1: [n_dofs(l)]
+  std::vector<void *>     invdiag, sol, def, tmp;
+  std::vector<double>     omega, lambda;
+  double                 *d_acc = nullptr;
+  double                  P[MAXP][MAXN]{};
+  bool                    setup_done = false;
+  // dense LU coarse solver (coarse_n_iterations < 0): the substitute for the
+  // reference's Trilinos direct solver (multigrid.cc:448-455, 477-481)
+  rocblas_handle blas   = nullptr;
+  double        *d_lu   = nullptr; // [n0][n0] column major, LU factors
+  rocblas_int   *d_ipiv = nullptr;
+  rocblas_int   *d_info = nullptr;
+  double        *d_rhs  = nullptr; // [n0]
+
+  size_t
+  ts() const
+  {
+    return prec == GLS_F64 ? 8 : 4;
+  }
 };
 
-extern "C" {
-glsStatus gls_mg_create(const glsMGDesc *, const glsOp *, const uint32_t *const *, glsMG *)
+namespace
 {
-  gls::set_error("gls_mg_create: not implemented yet");
-  return 2;
+template <typename T>
+TransferArgs<T>
+targs(const glsMG_ *mg, int level)
+{
+  TransferArgs<T> a;
+  a.coarse_nodes = mg->ops[level - 1]->d_nodes;
+  a.child        = mg->d_child[level];
+  a.weight       = (const T *)mg->d_weight[level];
+  a.n_cells_c    = mg->ops[level - 1]->n_cells;
+  for (int i = 0; i < MAXP; ++i)
+    for (int j = 0; j < MAXN; ++j)
+      a.P[i][j] = (T)mg->P[i][j];
+  return a;
 }
-void gls_mg_destroy(glsMG mg) { delete mg; }
-glsStatus gls_mg_setup(glsMG, void *) { gls::set_error("not implemented"); return 2; }
-glsStatus gls_mg_get_relaxation(glsMG, int, double *, double *) { gls::set_error("not implemented"); return 2; }
-glsStatus gls_mg_vcycle(glsMG, void *, const void *, void *) { gls::set_error("not implemented"); return 2; }
-glsStatus gls_mg_prolongate_add(glsMG, int, void *, const void *, void *) { gls::set_error("not implemented"); return 2; }
-glsStatus gls_mg_restrict_add(glsMG, int, void *, const void *, void *) { gls::set_error("not implemented"); return 2; }
-glsStatus gls_mg_interpolate(glsMG, int, void *, const void *, void *) { gls::set_error("not implemented"); return 2; }
-glsStatus gls_mg_smooth(glsMG, int, void *, const void *, int, void *) { gls::set_error("not implemented"); return 2; }
+
+// kind: 0 prolongate_add, 1 restrict_add, 2 interpolate
+template <int dim, int k, typename T>
+void
+transfer_t(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hipStream_t s)
+{
+  constexpr int nq = ipow(k + 1, dim);
+  const auto    a  = targs<T>(mg, level);
+  const dim3    grid((unsigned)a.n_cells_c);
+  if (kind == 0)
+    hipLaunchKernelGGL((k_prolongate<dim, k, T>), grid, dim3(256), 0, s, a, (T *)dst,
+                       (const T *)src);
+  else if (kind == 1)
+    hipLaunchKernelGGL((k_restrict<dim, k, T>), grid, dim3(256), 0, s, a, (T *)dst,
+                       (const T *)src);
+  else
+    hipLaunchKernelGGL((k_interpolate<dim, k, T>), g1(a.n_cells_c * nq), dim3(256), 0, s, a,
+                       (T *)dst, (const T *)src);
+  HIP_THROW(hipGetLastError());
 }
+
+template <typename T>
+void
+transfer_p(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hipStream_t s)
+{
+  const int d = mg->dim, k = mg->degree;
+  if (d == 2 && k == 1)
+    transfer_t<2, 1, T>(mg, kind, level, dst, src, s);
+  else if (d == 2 && k == 2)
+    transfer_t<2, 2, T>(mg, kind, level, dst, src, s);
+  else if (d == 3 && k == 1)
+    transfer_t<3, 1, T>(mg, kind, level, dst, src, s);
+  else if (d == 3 && k == 2)
+    transfer_t<3, 2, T>(mg, kind, level, dst, src, s);
+  else
+    throw std::runtime_error("multigrid transfer: degree must be 1 or 2");
+}
+
+void
+transfer(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hipStream_t s)
+{
+  if (level < 1 || level >= (int)mg->ops.size())
+    throw std::runtime_error("multigrid transfer: level out of range");
+  if (mg->prec == GLS_F64)
+    transfer_p<double>(mg, kind, level, dst, src, s);
+  else
+    transfer_p<float>(mg, kind, level, dst, src, s);
+}
+
+void
+check(glsStatus st)
+{
+  if (st != 0)
+    throw std::runtime_error(gls_last_error());
+}
+
+template <typename T>
+void
+relax_t(const glsMG_ *mg, int level, void *x, const void *b, int first, hipStream_t s)
+{
+  const int64_t n = mg->ops[level]->n_dofs;
+  hipLaunchKernelGGL(k_relax<T>, g1(n), dim3(256), 0, s, (T *)x, (const T *)b,
+                     (const T *)mg->tmp[level], (const T *)mg->invdiag[level],
+                     (T)mg->omega[level], first, n);
+  HIP_THROW(hipGetLastError());
+}
+
+// PreconditionRelaxation::vmult (zero start) / step, `iters` iterations
+void
+smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int iters,
+       hipStream_t s)
+{
+  auto relax = mg->prec == GLS_F64 ? relax_t<double> : relax_t<float>;
+  int  it    = 0;
+  if (zero_start && iters > 0)
+    {
+      relax(mg, level, x, b, 1, s);
+      it = 1;
+    }
+  for (; it < iters; ++it)
+    {
+      check(gls_op_vmult(mg->ops[level], mg->tmp[level], x, s));
+      relax(mg, level, x, b, 0, s);
+    }
+}
+
+void
+residual(const glsMG_ *mg, int level, void *t, const void *b, hipStream_t s)
+{
+  const int64_t n = mg->ops[level]->n_dofs;
+  if (mg->prec == GLS_F64)
+    hipLaunchKernelGGL(k_residual<double>, g1(n), dim3(256), 0, s, (double *)t,
+                       (const double *)b, n);
+  else
+    hipLaunchKernelGGL(k_residual<float>, g1(n), dim3(256), 0, s, (float *)t,
+                       (const float *)b, n);
+  HIP_THROW(hipGetLastError());
+}
+
+void
+check_blas(rocblas_status st, const char *what)
+{
+  if (st != rocblas_status_success)
+    throw std::runtime_error(std::string(what) + " failed (rocblas status " +
+                             std::to_string((int)st) + ")");
+}
+
+template <typename T>
+__global__ void
+k_set_unit(T *x, int64_t j, int64_t n, int on)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && i == j)
+    x[i] = on ? T(1) : T(0);
+}
+
+// Assemble the coarse level operator column by column (A e_j, including the
+// identity rows of constrained dofs) into FP64 and LU-factorise it.
+template <typename T>
+void
+coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
+{
+  glsOp         op = mg->ops[0];
+  const int64_t n  = op->n_dofs;
+  if (n > 40000)
+    throw std::runtime_error("dense LU coarse solver: coarse level too large");
+  if (!mg->blas)
+    check_blas(rocblas_create_handle(&mg->blas), "rocblas_create_handle");
+  check_blas(rocblas_set_stream(mg->blas, s), "rocblas_set_stream");
+  if (!mg->d_lu)
+    {
+      HIP_THROW(hipMalloc((void **)&mg->d_lu, (size_t)n * n * sizeof(double)));
+      HIP_THROW(hipMalloc((void **)&mg->d_ipiv, (size_t)n * sizeof(rocblas_int)));
+      HIP_THROW(hipMalloc((void **)&mg->d_info, sizeof(rocblas_int)));
+      HIP_THROW(hipMalloc((void **)&mg->d_rhs, (size_t)n * sizeof(double)));
+    }
+  T *e = (T *)mg->sol[0], *col = (T *)mg->tmp[0];
+  HIP_THROW(hipMemsetAsync(e, 0, n * sizeof(T), s));
+  for (int64_t j = 0; j < n; ++j)
+    {
+      hipLaunchKernelGGL(k_set_unit<T>, g1(n), dim3(256), 0, s, e, j, n, 1);
+      check(gls_op_vmult(op, col, e, s));
+      hipLaunchKernelGGL((k_convert<T, double>), g1(n), dim3(256), 0, s,
+                         mg->d_lu + (size_t)j * n, col, n);
+      hipLaunchKernelGGL(k_set_unit<T>, g1(n), dim3(256), 0, s, e, j, n, 0);
+    }
+  HIP_THROW(hipGetLastError());
+  check_blas(rocsolver_dgetrf(mg->blas, (rocblas_int)n, (rocblas_int)n, mg->d_lu,
+                              (rocblas_int)n, mg->d_ipiv, mg->d_info),
+             "rocsolver_dgetrf");
+  rocblas_int info = 0;
+  HIP_THROW(hipMemcpyAsync(&info, mg->d_info, sizeof(info), hipMemcpyDeviceToHost, s));
+  HIP_THROW(hipStreamSynchronize(s));
+  if (info != 0)
+    throw std::runtime_error("dense LU coarse solver: singular coarse matrix (info " +
+                             std::to_string(info) + ")");
+}
+
+template <typename T>
+void
+coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
+{
+  const int64_t n = mg->ops[0]->n_dofs;
+  hipLaunchKernelGGL((k_convert<T, double>), g1(n), dim3(256), 0, s, mg->d_rhs,
+                     (const T *)mg->def[0], n);
+  check_blas(rocblas_set_stream(mg->blas, s), "rocblas_set_stream");
+  check_blas(rocsolver_dgetrs(mg->blas, rocblas_operation_none, (rocblas_int)n, 1, mg->d_lu,
+                              (rocblas_int)n, mg->d_ipiv, mg->d_rhs, (rocblas_int)n),
+             "rocsolver_dgetrs");
+  hipLaunchKernelGGL((k_convert<double, T>), g1(n), dim3(256), 0, s, (T *)mg->sol[0],
+                     mg->d_rhs, n);
+  HIP_THROW(hipGetLastError());
+}
+
+// Multigrid::level_v_step (deal.II default V-cycle): solution[l] from defect[l]
+void
+v_step(glsMG_ *mg, int l, hipStream_t s)
+{
+  const size_t bytes = (size_t)mg->ops[l]->n_dofs * mg->ts();
+  if (l == 0)
+    {
+      // coarse solve (multigrid.cc:465-489): dense LU (< 0), identity (0)
+      // or relaxation sweeps (> 0)
+      if (mg->desc.coarse_n_iterations < 0)
+        {
+          if (mg->prec == GLS_F64)
+            coarse_lu_solve_t<double>(mg, s);
+          else
+            coarse_lu_solve_t<float>(mg, s);
+        }
+      else if (mg->desc.coarse_n_iterations == 0)
+        HIP_THROW(hipMemcpyAsync(mg->sol[0], mg->def[0], bytes, hipMemcpyDeviceToDevice, s));
+      else
+        smooth(mg, 0, mg->sol[0], mg->def[0], true, mg->desc.coarse_n_iterations, s);
+      return;
+    }
+  const int nit = mg->desc.smoothing_n_iterations;
+  // pre-smoothing from a zero initial guess (MGSmootherPrecondition::apply)
+  smooth(mg, l, mg->sol[l], mg->def[l], true, nit, s);
+  // residual t = defect - A solution
+  check(gls_op_vmult(mg->ops[l], mg->tmp[l], mg->sol[l], s));
+  residual(mg, l, mg->tmp[l], mg->def[l], s);
+  // restrict
+  HIP_THROW(hipMemsetAsync(mg->def[l - 1], 0, (size_t)mg->ops[l - 1]->n_dofs * mg->ts(), s));
+  transfer(mg, 1, l, mg->def[l - 1], mg->tmp[l], s);
+  v_step(mg, l - 1, s);
+  // prolongate and add the coarse correction
+  transfer(mg, 0, l, mg->sol[l], mg->sol[l - 1], s);
+  // post-smoothing (MGSmootherPrecondition::smooth -> step)
+  smooth(mg, l, mg->sol[l], mg->def[l], false, nit, s);
+}
+
+template <typename T>
+double
+power_iteration_t(glsMG_ *mg, int l, hipStream_t s)
+{
+  glsOp         op = mg->ops[l];
+  const int64_t n  = op->n_dofs;
+  // start vector: deterministic pseudo-random, zero on constrained dofs
+  // (AdditionalData::constraints, multigrid.cc:303-304)
+  std::vector<T> h(n);
+  uint64_t       z = 0x9E3779B97F4A7C15ULL * (uint64_t)(l + 1);
+  for (int64_t i = 0; i < n; ++i)
+    {
+      z += 0x9E3779B97F4A7C15ULL;
+      uint64_t r = z;
+      r          = (r ^ (r >> 30)) * 0xBF58476D1CE4E5B9ULL;
+      r          = (r ^ (r >> 27)) * 0x94D049BB133111EBULL;
+      r ^= r >> 31;
+      const int64_t node = i / (op->dim + 1);
+      const int     comp = (int)(i % (op->dim + 1));
+      const bool    con  = node < op->n_nodes && ((op->h_cmask[node] >> comp) & 1);
+      h[i]               = con ? T(0) : (T)((double)(r >> 11) * 0x1.0p-53 - 0.5);
+    }
+  void *x = mg->sol[l], *y = mg->tmp[l];
+  HIP_THROW(hipMemcpyAsync(x, h.data(), n * sizeof(T), hipMemcpyHostToDevice, s));
+  double lam = 0;
+  for (int it = 0; it < mg->desc.smoothing_eig_n_iterations; ++it)
+    {
+      check(gls_op_vmult(op, y, x, s));
+      HIP_THROW(hipMemsetAsync(mg->d_acc, 0, 2 * sizeof(double), s));
+      hipLaunchKernelGGL(k_power_step<T>, g1(n), dim3(256), 0, s, (T *)y, (const T *)x,
+                         (const T *)mg->invdiag[l], mg->d_acc, n);
+      HIP_THROW(hipGetLastError());
+      double acc[2];
+      HIP_THROW(hipMemcpyAsync(acc, mg->d_acc, sizeof(acc), hipMemcpyDeviceToHost, s));
+      HIP_THROW(hipStreamSynchronize(s));
+      if (acc[0] <= 0 || acc[1] <= 0)
+        break;
+      lam = std::sqrt(acc[0] / acc[1]);
+      hipLaunchKernelGGL(k_scale<T>, g1(n), dim3(256), 0, s, (T *)x, (const T *)y,
+                         1.0 / std::sqrt(acc[0]), n);
+      HIP_THROW(hipGetLastError());
+    }
+  return lam;
+}
+
+} // namespace
+
+extern "C" {
+
+glsStatus
+gls_mg_create(const glsMGDesc *desc, const glsOp *levels, const uint32_t *const *child,
+              glsMG *out)
+{
+  GLS_TRY
+  if (!desc || !levels || !out || desc->n_levels < 1)
+    throw std::runtime_error("gls_mg_create: invalid arguments");
+  auto *mg   = new glsMG_();
+  mg->desc   = *desc;
+  mg->prec   = levels[0]->prec;
+  mg->dim    = levels[0]->dim;
+  mg->degree = levels[0]->degree;
+  mg->nc     = mg->dim + 1;
+  const int nl_levels = desc->n_levels;
+  for (int l = 0; l < nl_levels; ++l)
+    {
+      glsOp op = levels[l];
+      if (!op || op->prec != mg->prec || op->dim != mg->dim || op->degree != mg->degree)
+        throw std::runtime_error("gls_mg_create: level operators must share dim, degree and "
+                                 "precision");
+      if (op->n_owned_nodes != op->n_nodes)
+        throw std::runtime_error("gls_mg_create: distributed level operators are not "
+                                 "supported yet");
+      mg->ops.push_back(op);
+    }
+  if (nl_levels > 1 && (!child || mg->degree > 2))
+    throw std::runtime_error("gls_mg_create: child lattices required (degree <= 2)");
+  // 1D prolongation: parent GLL basis at the child lattice points
+  const int k = mg->degree;
+  Basis1D   b(k);
+  for (int I = 0; I <= 2 * k; ++I)
+    {
+      const int    c = I / k > 1 ? 1 : I / k;
+      const double x = 0.5 * (c + b.nodes[I - c * k]);
+      for (int j = 0; j <= k; ++j)
+        {
+          double v = 1;
+          for (int m = 0; m <= k; ++m)
+            if (m != j)
+              v *= (x - b.nodes[m]) / (b.nodes[j] - b.nodes[m]);
+          mg->P[I][j] = v;
+        }
+    }
+  const int L  = 2 * k + 1;
+  const int nl = mg->dim == 3 ? L * L * L : L * L;
+  mg->d_child.assign(nl_levels, nullptr);
+  mg->d_weight.assign(nl_levels, nullptr);
+  for (int l = 1; l < nl_levels; ++l)
+    {
+      glsOp         cop = mg->ops[l - 1], fop = mg->ops[l];
+      const int64_t nch = cop->n_cells * nl;
+      std::vector<uint32_t> ch(child[l], child[l] + nch);
+      std::vector<double>   val((size_t)fop->n_nodes, 0.0);
+      for (uint32_t fn : ch)
+        {
+          if ((int64_t)fn >= fop->n_nodes)
+            throw std::runtime_error("gls_mg_create: child lattice node out of range");
+          val[fn] += 1.0;
+        }
+      std::vector<double> w((size_t)fop->n_dofs, 0.0);
+      for (int64_t nd = 0; nd < fop->n_nodes; ++nd)
+        for (int c = 0; c < mg->nc; ++c)
+          w[nd * mg->nc + c] =
+            (((fop->h_cmask[nd] >> c) & 1) || val[nd] == 0) ? 0.0 : 1.0 / val[nd];
+      HIP_THROW(hipMalloc((void **)&mg->d_child[l], nch * sizeof(uint32_t)));
+      HIP_THROW(hipMemcpy(mg->d_child[l], ch.data(), nch * sizeof(uint32_t),
+                          hipMemcpyHostToDevice));
+      HIP_THROW(hipMalloc(&mg->d_weight[l], w.size() * mg->ts()));
+      if (mg->prec == GLS_F64)
+        HIP_THROW(hipMemcpy(mg->d_weight[l], w.data(), w.size() * 8, hipMemcpyHostToDevice));
+      else
+        {
+          std::vector<float> wf(w.begin(), w.end());
+          HIP_THROW(hipMemcpy(mg->d_weight[l], wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
+        }
+    }
+  for (int l = 0; l < nl_levels; ++l)
+    {
+      const size_t bytes = (size_t)mg->ops[l]->n_dofs * mg->ts();
+      void        *p[4];
+      for (auto &q : p)
+        {
+          HIP_THROW(hipMalloc(&q, std::max<size_t>(bytes, 1)));
+          HIP_THROW(hipMemset(q, 0, std::max<size_t>(bytes, 1)));
+        }
+      mg->invdiag.push_back(p[0]);
+      mg->sol.push_back(p[1]);
+      mg->def.push_back(p[2]);
+      mg->tmp.push_back(p[3]);
+    }
+  mg->omega.assign(nl_levels, 1.0);
+  mg->lambda.assign(nl_levels, 0.0);
+  HIP_THROW(hipMalloc((void **)&mg->d_acc, 2 * sizeof(double)));
+  *out = mg;
+  GLS_CATCH
+}
+
+void
+gls_mg_destroy(glsMG mg)
+{
+  if (!mg)
+    return;
+  for (auto *p : mg->d_child)
+    if (p)
+      (void)hipFree(p);
+  for (auto *p : mg->d_weight)
+    if (p)
+      (void)hipFree(p);
+  for (auto *v : {&mg->invdiag, &mg->sol, &mg->def, &mg->tmp})
+    for (void *p : *v)
+      if (p)
+        (void)hipFree(p);
+  if (mg->d_acc)
+    (void)hipFree(mg->d_acc);
+  for (void *p : {(void *)mg->d_lu, (void *)mg->d_ipiv, (void *)mg->d_info, (void *)mg->d_rhs})
+    if (p)
+      (void)hipFree(p);
+  if (mg->blas)
+    rocblas_destroy_handle(mg->blas);
+  delete mg;
+}
+
+glsStatus
+gls_mg_setup(glsMG mg, void *stream)
+{
+  GLS_TRY
+  if (!mg)
+    throw std::runtime_error("gls_mg_setup: null handle");
+  hipStream_t s = (hipStream_t)stream;
+  for (size_t l = 0; l < mg->ops.size(); ++l)
+    {
+      // compute_inverse_diagonal (multigrid.cc:290-293)
+      check(gls_op_compute_inverse_diagonal(mg->ops[l], mg->invdiag[l], s));
+      // relaxation = 0: omega from a power-iteration estimate of
+      // lambda_max(D^-1 A), alpha = lambda_max / smoothing_range,
+      // omega = 2 / (alpha + lambda_max)  (multigrid.cc:294-305, 353-369)
+      const double lam = mg->prec == GLS_F64 ? power_iteration_t<double>(mg, (int)l, s) :
+                                               power_iteration_t<float>(mg, (int)l, s);
+      mg->lambda[l]    = lam;
+      if (lam > 0)
+        {
+          const double alpha = mg->desc.smoothing_range > 1.0 ?
+                                 lam / mg->desc.smoothing_range :
+                                 0.9 * lam;
+          mg->omega[l] = 2.0 / (alpha + lam);
+        }
+      else
+        mg->omega[l] = 1.0;
+      HIP_THROW(hipMemsetAsync(mg->sol[l], 0, (size_t)mg->ops[l]->n_dofs * mg->ts(), s));
+    }
+  if (mg->desc.coarse_n_iterations < 0)
+    {
+      if (mg->prec == GLS_F64)
+        coarse_lu_setup_t<double>(mg, s);
+      else
+        coarse_lu_setup_t<float>(mg, s);
+    }
+  HIP_THROW(hipStreamSynchronize(s));
+  mg->setup_done = true;
+  GLS_CATCH
+}
+
+glsStatus
+gls_mg_get_relaxation(glsMG mg, int level, double *omega, double *lambda_max)
+{
+  GLS_TRY
+  if (!mg || level < 0 || level >= (int)mg->ops.size())
+    throw std::runtime_error("gls_mg_get_relaxation: bad level");
+  if (omega)
+    *omega = mg->omega[level];
+  if (lambda_max)
+    *lambda_max = mg->lambda[level];
+  GLS_CATCH
+}
+
+glsStatus
+gls_mg_vcycle(glsMG mg, void *dst, const void *src, void *stream)
+{
+  GLS_TRY
+  if (!mg || !dst || !src)
+    throw std::runtime_error("gls_mg_vcycle: null argument");
+  if (!mg->setup_done)
+    throw std::runtime_error("gls_mg_vcycle before gls_mg_setup");
+  hipStream_t   s   = (hipStream_t)stream;
+  const int     top = (int)mg->ops.size() - 1;
+  const int64_t n   = mg->ops[top]->n_dofs;
+  const bool    cvt = mg->desc.outer_precision == GLS_F64 && mg->prec == GLS_F32;
+  // copy_to_mg
+  if (cvt)
+    hipLaunchKernelGGL((k_convert<double, float>), g1(n), dim3(256), 0, s,
+                       (float *)mg->def[top], (const double *)src, n);
+  else
+    HIP_THROW(hipMemcpyAsync(mg->def[top], src, n * mg->ts(), hipMemcpyDeviceToDevice, s));
+  HIP_THROW(hipGetLastError());
+  v_step(mg, top, s);
+  // copy_from_mg
+  if (cvt)
+    hipLaunchKernelGGL((k_convert<float, double>), g1(n), dim3(256), 0, s, (double *)dst,
+                       (const float *)mg->sol[top], n);
+  else
+    HIP_THROW(hipMemcpyAsync(dst, mg->sol[top], n * mg->ts(), hipMemcpyDeviceToDevice, s));
+  HIP_THROW(hipGetLastError());
+  GLS_CATCH
+}
+
+glsStatus
+gls_mg_prolongate_add(glsMG mg, int level, void *dst_fine, const void *src_coarse,
+                      void *stream)
+{
+  GLS_TRY
+  if (!mg)
+    throw std::runtime_error("gls_mg_prolongate_add: null handle");
+  transfer(mg, 0, level, dst_fine, src_coarse, (hipStream_t)stream);
+  GLS_CATCH
+}
+
+glsStatus
+gls_mg_restrict_add(glsMG mg, int level, void *dst_coarse, const void *src_fine, void *stream)
+{
+  GLS_TRY
+  if (!mg)
+    throw std::runtime_error("gls_mg_restrict_add: null handle");
+  transfer(mg, 1, level, dst_coarse, src_fine, (hipStream_t)stream);
+  GLS_CATCH
+}
+
+glsStatus
+gls_mg_interpolate(glsMG mg, int level, void *dst_coarse, const void *src_fine, void *stream)
+{
+  GLS_TRY
+  if (!mg)
+    throw std::runtime_error("gls_mg_interpolate: null handle");
+  transfer(mg, 2, level, dst_coarse, src_fine, (hipStream_t)stream);
+  GLS_CATCH
+}
+
+glsStatus
+gls_mg_smooth(glsMG mg, int level, void *x, const void *b, int zero_initial_guess,
+              void *stream)
+{
+  GLS_TRY
+  if (!mg || level < 0 || level >= (int)mg->ops.size())
+    throw std::runtime_error("gls_mg_smooth: bad arguments");
+  if (!mg->setup_done)
+    throw std::runtime_error("gls_mg_smooth before gls_mg_setup");
+  smooth(mg, level, x, b, zero_initial_guess != 0, mg->desc.smoothing_n_iterations,
+         (hipStream_t)stream);
+  GLS_CATCH
+}
+
+} // extern "C"

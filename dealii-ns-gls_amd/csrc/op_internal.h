@@ -1,0 +1,55 @@
+// op_internal.h — the operator handle's state, shared by gls_op.hip (the
+// operator) and mg.hip (the multigrid that drives level operators).
+#pragma once
+
+#include "../../include/gls_op.h"
+#include "common.h"
+
+#include <cstdint>
+#include <vector>
+
+struct glsOp_
+{
+  int     dim = 3, degree = 2, prec = GLS_F64;
+  int64_t n_cells = 0, n_nodes = 0, n_owned_nodes = 0, n_dofs = 0, n_owned_dofs = 0;
+  int     nq = 0, nf = 0;
+  gls::Basis1D basis{1};
+
+  glsOpParams prm{};
+  bool        have_lin = false, have_prev = false, have_old_grad = false;
+
+  // host copies the multigrid transfer setup needs
+  std::vector<uint8_t>  h_cmask;      // [n_nodes]
+  std::vector<uint32_t> h_cell_nodes; // [n_cells][nq]
+
+  int64_t n_gen = 0, n_cart = 0;
+  // device buffers
+  uint32_t *d_nodes    = nullptr; // [n_cells][nq] node | cmask << 28
+  uint32_t *d_cell_geo = nullptr;
+  void     *d_geo_cart = nullptr;
+  void     *d_geo_gen  = nullptr;
+  void     *d_tab      = nullptr;
+  void     *d_cellwise = nullptr;
+  void     *d_old_grad = nullptr;
+  void     *d_hq       = nullptr;
+  void     *d_hmin     = nullptr;
+  void     *d_tmp      = nullptr;
+  uint32_t *d_cbits    = nullptr; // constrained-dof bitmask (owned range)
+  int       device     = 0;
+
+  // brick decomposition (csrc/brick.h)
+  bool      use_brick = false;
+  int       bx = 1, by = 1, bz = 1, L = 0, Lx = 0, Ly = 0;
+  int64_t   n_bricks = 0, n_slots = 0, n_shared = 0;
+  uint32_t *d_brick_nodes  = nullptr;
+  uint32_t *d_brick_target = nullptr;
+  uint32_t *d_shared_nodes = nullptr;
+  uint32_t *d_shared_off   = nullptr;
+  void     *d_partial      = nullptr;
+
+  size_t
+  tsize() const
+  {
+    return prec == GLS_F64 ? 8 : 4;
+  }
+};

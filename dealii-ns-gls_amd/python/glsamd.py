@@ -24,7 +24,8 @@ GLS_INCREMENT_FORM, GLS_CONSIDER_TIME_DERIVATIVE, GLS_CELL_WISE_STAB = 1, 2, 4
 EXPORTS = [
     "gls_op_create", "gls_op_destroy", "gls_op_set_parameters", "gls_op_m",
     "gls_op_precision", "gls_op_set_linearization_point", "gls_op_set_previous_solution",
-    "gls_op_vmult", "gls_op_vmult_cells", "gls_op_vmult_init", "gls_op_evaluate_residual",
+    "gls_op_vmult", "gls_op_vmult_cells", "gls_op_vmult_init", "gls_op_apply_identity_rows",
+    "gls_op_evaluate_residual",
     "gls_op_compute_inverse_diagonal", "gls_op_upload_tables", "gls_op_download_tables",
     "gls_op_geometry_counts", "gls_op_vmult_bytes", "gls_mg_create", "gls_mg_destroy",
     "gls_mg_setup", "gls_mg_get_relaxation", "gls_mg_vcycle", "gls_mg_prolongate_add",
@@ -49,7 +50,7 @@ class OpParams(C.Structure):
 class MGDesc(C.Structure):
     _fields_ = [("n_levels", C.c_int), ("smoothing_n_iterations", C.c_int),
                 ("smoothing_eig_n_iterations", C.c_int), ("smoothing_range", C.c_double),
-                ("coarse_n_iterations", C.c_int)]
+                ("coarse_n_iterations", C.c_int), ("outer_precision", C.c_int)]
 
 
 def lib_path():
@@ -75,6 +76,7 @@ def lib():
         L.gls_op_vmult.argtypes = [vp, vp, vp, vp]
         L.gls_op_vmult_cells.argtypes = [vp, vp, vp, i64, i64, vp]
         L.gls_op_vmult_init.argtypes = [vp, vp, vp, vp]
+        L.gls_op_apply_identity_rows.argtypes = [vp, vp, vp, vp]
         L.gls_op_evaluate_residual.argtypes = [vp, vp, vp, vp]
         L.gls_op_compute_inverse_diagonal.argtypes = [vp, vp, vp]
         L.gls_op_upload_tables.argtypes = [vp, vp, vp]
@@ -201,6 +203,9 @@ class NavierStokesOperator:
     def vmult_init(self, dst, src):
         _check(lib().gls_op_vmult_init(self.h, _ptr(dst), _ptr(src), _stream()))
 
+    def apply_identity_rows(self, dst, src):
+        _check(lib().gls_op_apply_identity_rows(self.h, _ptr(dst), _ptr(src), _stream()))
+
     def vmult_cells(self, dst, src, begin, end):
         _check(lib().gls_op_vmult_cells(self.h, _ptr(dst), _ptr(src), int(begin), int(end),
                                         _stream()))
@@ -234,3 +239,98 @@ class NavierStokesOperator:
 
     def vmult_bytes(self):
         return lib().gls_op_vmult_bytes(self.h)
+
+
+class Multigrid:
+    """PreconditionerGMG (multigrid.h:61-141) over the C-ABI: level operators
+    (MGNumber = float by default), damped-Jacobi relaxation smoother with a
+    power-iteration relaxation factor, MGTwoLevelTransfer, V-cycle."""
+
+    def __init__(self, level_ops, child_lattices, smoothing_n_iterations=5,
+                 smoothing_eig_n_iterations=20, smoothing_range=20.0, coarse_n_iterations=20,
+                 outer_precision="f64"):
+        self.ops = list(level_ops)
+        self._child = [None] + [np.ascontiguousarray(c, dtype=np.uint32)
+                                for c in child_lattices]
+        n = len(self.ops)
+        arr = (C.c_void_p * n)(*[op.h.value for op in self.ops])
+        ch = (C.c_void_p * n)(*[0 if c is None else c.ctypes.data for c in self._child])
+        outer = GLS_F64 if outer_precision in ("f64", GLS_F64) else GLS_F32
+        self.desc = MGDesc(n, smoothing_n_iterations, smoothing_eig_n_iterations,
+                           smoothing_range, coarse_n_iterations, outer)
+        self.outer_dtype = None
+        h = C.c_void_p()
+        _check(lib().gls_mg_create(C.byref(self.desc), C.cast(arr, C.c_void_p),
+                                   C.cast(ch, C.c_void_p), C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().gls_mg_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def setup(self):
+        _check(lib().gls_mg_setup(self.h, _stream()))
+
+    def relaxation(self, level):
+        w, lam = C.c_double(), C.c_double()
+        _check(lib().gls_mg_get_relaxation(self.h, level, C.byref(w), C.byref(lam)))
+        return w.value, lam.value
+
+    def vcycle(self, dst, src):
+        _check(lib().gls_mg_vcycle(self.h, _ptr(dst), _ptr(src), _stream()))
+        return dst
+
+    def prolongate_add(self, level, dst_fine, src_coarse):
+        _check(lib().gls_mg_prolongate_add(self.h, level, _ptr(dst_fine), _ptr(src_coarse),
+                                           _stream()))
+
+    def restrict_add(self, level, dst_coarse, src_fine):
+        _check(lib().gls_mg_restrict_add(self.h, level, _ptr(dst_coarse), _ptr(src_fine),
+                                         _stream()))
+
+    def interpolate(self, level, dst_coarse, src_fine):
+        _check(lib().gls_mg_interpolate(self.h, level, _ptr(dst_coarse), _ptr(src_fine),
+                                        _stream()))
+
+    def smooth(self, level, x, b, zero_initial_guess=True):
+        _check(lib().gls_mg_smooth(self.h, level, _ptr(x), _ptr(b), int(zero_initial_guess),
+                                   _stream()))
+
+
+def build_gmg(meshes, cmasks, params, u_star_fine, history_fine=None, weights=None,
+              precision="f32", **mg_kwargs):
+    """Level operators + transfers for a mesh hierarchy (coarse -> fine), the
+    linearization point / history interpolated down level by level
+    (interpolate_to_mg, main.cc:772-803, 815-832).  Returns (mg, level_ops)."""
+    import torch
+    ops = []
+    for m, cm in zip(meshes, cmasks):
+        op = NavierStokesOperator(m, cm, precision)
+        op.set_parameters(**params)
+        ops.append(op)
+    child = [meshes[l - 1].child_lattice(meshes[l]) for l in range(1, len(meshes))]
+    mg = Multigrid(ops, child, **mg_kwargs)
+    vecs = [ops[-1]._dev(u_star_fine)]
+    hists = [[ops[-1]._dev(h) for h in history_fine]] if history_fine is not None else None
+    for l in range(len(ops) - 1, 0, -1):
+        v = ops[l - 1].initialize_dof_vector()
+        mg.interpolate(l, v, vecs[0])
+        vecs.insert(0, v)
+        if hists is not None:
+            hl = []
+            for h in hists[0]:
+                t = ops[l - 1].initialize_dof_vector()
+                mg.interpolate(l, t, h)
+                hl.append(t)
+            hists.insert(0, hl)
+    for l, op in enumerate(ops):
+        op.set_linearization_point(vecs[l])
+        if hists is not None and params.get("order", 0) > 0:
+            op.set_previous_solution(hists[l], weights)
+    torch.cuda.synchronize()
+    mg.setup()
+    return mg, ops

@@ -22,11 +22,12 @@
  *                                      operator_base.h:35-36, .cc:234-320
  *   gls_op_vmult                     OperatorBase::vmult
  *                                      operator_base.h:47-48, .cc:684-732
+ *   gls_op_vmult_init /
  *   gls_op_vmult_cells /
- *   gls_op_vmult_finish              the two halves of vmult around the ghost
+ *   gls_op_apply_identity_rows       the pieces of vmult around the ghost
  *                                      exchange (deal.II cell_loop with
- *                                      compress(add), .cc:702-721) for
- *                                      multi-GPU overlap
+ *                                      update_ghost_values / compress(add),
+ *                                      .cc:702-721) for multi-GPU
  *   gls_op_evaluate_residual         OperatorBase::evaluate_residual
  *                                      operator_base.h:44-46, .cc:648-682
  *   gls_op_compute_inverse_diagonal  OperatorBase::compute_inverse_diagonal
@@ -127,6 +128,10 @@ glsStatus gls_op_vmult_cells(glsOp op, void *dst, const void *src,
                              void *stream);
 /* dst[i] = constrained(i) ? src[i] : 0 on the owned dofs, 0 on ghosts */
 glsStatus gls_op_vmult_init(glsOp op, void *dst, const void *src, void *stream);
+/* dst[i] = src[i] on constrained owned dofs, others untouched: the identity
+ * rows of vmult (operator_ns.cc:719-721) re-applied after the ghost
+ * export-add (compress(add)) of a distributed vmult */
+glsStatus gls_op_apply_identity_rows(glsOp op, void *dst, const void *src, void *stream);
 
 glsStatus gls_op_evaluate_residual(glsOp op, void *dst, const void *src,
                                    void *stream);
@@ -155,6 +160,10 @@ typedef struct
   double smoothing_range;              /* 20  multigrid.h:30                 */
   int    coarse_n_iterations;  /* coarse solver: relaxation sweeps (0 =
                                   identity); see DESIGN.md                   */
+  int    outer_precision;      /* precision of the vectors gls_mg_vcycle
+                                  takes (GLS_F64: copy_to_mg / copy_from_mg
+                                  convert to the level precision, as
+                                  PreconditionMG does for MGNumber = float)  */
 } glsMGDesc;
 
 /* levels[l] are level operators (same precision); child[l] for l >= 1 is the

@@ -1,0 +1,139 @@
+"""TEST INFRASTRUCTURE: CPU multigrid on top of the oracle (oracle/liboracle.so)
+— the restatement the GPU multigrid (csrc/mg.hip) is checked against.
+
+Restates (deal.II semantics, not vendored; parity unpinned against the
+reference binary):
+  PreconditionRelaxation (relaxation = 0 -> power-iteration omega),
+    multigrid.cc:281-369: vmult (zero start) = x = w D^-1 b then n-1 steps,
+    step = n times x += w D^-1 (b - A x)
+  Multigrid::level_v_step V-cycle with MGSmootherPrecondition pre/post
+    smoothing, MGTwoLevelTransfer restrict/prolongate (multigrid.cc:534-548)
+  coarse solve: relaxation sweeps from zero (substitution for the
+    Trilinos direct / AMG coarse solvers, multigrid.cc:448-489)
+"""
+import numpy as np
+
+import oracle as orc
+
+
+def power_start_vector(n_dofs, level, cmask, dim):
+    """The deterministic start vector csrc/mg.hip uses (constrained -> 0)."""
+    M = (1 << 64) - 1
+    z = (0x9E3779B97F4A7C15 * (level + 1)) & M
+    out = np.empty(n_dofs)
+    nc = dim + 1
+    for i in range(n_dofs):
+        z = (z + 0x9E3779B97F4A7C15) & M
+        r = z
+        r = ((r ^ (r >> 30)) * 0xBF58476D1CE4E5B9) & M
+        r = ((r ^ (r >> 27)) * 0x94D049BB133111EB) & M
+        r ^= r >> 31
+        con = (cmask[i // nc] >> (i % nc)) & 1
+        out[i] = 0.0 if con else (r >> 11) * 2.0 ** -53 - 0.5
+    return out
+
+
+class OracleGMG:
+    def __init__(self, meshes, cmasks, params, u_star, hist=None, weights=None,
+                 n_smooth=5, n_eig=20, smoothing_range=20.0, coarse_iters=20):
+        self.meshes = meshes
+        self.om = [orc.OracleMesh(m, c) for m, c in zip(meshes, cmasks)]
+        self.omz = [orc.OracleMesh(m, np.zeros(m.n_nodes, np.uint8)) for m in meshes]
+        self.child = [None] + [meshes[l - 1].child_lattice(meshes[l])
+                               for l in range(1, len(meshes))]
+        self.n_smooth, self.n_eig = n_smooth, n_eig
+        self.range, self.coarse_iters = smoothing_range, coarse_iters
+        L = len(meshes)
+        u = [None] * L
+        h = [None] * L
+        u[-1] = np.asarray(u_star, dtype=np.float64)
+        h[-1] = None if hist is None else [np.asarray(x, dtype=np.float64) for x in hist]
+        for l in range(L - 1, 0, -1):
+            u[l - 1] = self.interpolate(l, u[l])
+            if h[l] is not None:
+                h[l - 1] = [self.interpolate(l, x) for x in h[l]]
+        self.ops = []
+        for l in range(L):
+            o = orc.Oracle(self.om[l], **params)
+            o.set_linearization_point(u[l])
+            if h[l] is not None and params.get("order", 0) > 0:
+                o.set_previous_solution(h[l], weights)
+            self.ops.append(o)
+        self.invdiag = [o.inverse_diagonal() for o in self.ops]
+        self.omega = [1.0] * L
+        self.lam = [0.0] * L
+
+    def interpolate(self, l, fine):
+        out = np.zeros(self.meshes[l - 1].n_dofs)
+        orc.interpolate(self.omz[l - 1], self.omz[l], self.child[l], out, fine)
+        return out
+
+    def prolongate_add(self, l, dst_f, src_c):
+        orc.prolongate_add(self.om[l - 1], self.om[l], self.child[l], dst_f, src_c)
+
+    def restrict_add(self, l, dst_c, src_f):
+        orc.restrict_add(self.om[l - 1], self.om[l], self.child[l], dst_c, src_f)
+
+    def estimate(self, l):
+        m = self.meshes[l]
+        x = power_start_vector(m.n_dofs, l, self.om[l].cmask, m.dim)
+        lam = 0.0
+        for _ in range(self.n_eig):
+            y = self.invdiag[l] * self.ops[l].vmult(x)
+            ny, nx = np.linalg.norm(y), np.linalg.norm(x)
+            if ny == 0 or nx == 0:
+                break
+            lam = ny / nx
+            x = y / ny
+        return lam
+
+    def set_omega(self, omegas):
+        self.omega = list(omegas)
+
+    def setup_omega(self):
+        for l in range(len(self.ops)):
+            lam = self.estimate(l)
+            self.lam[l] = lam
+            alpha = lam / self.range if self.range > 1 else 0.9 * lam
+            self.omega[l] = 2.0 / (alpha + lam) if lam > 0 else 1.0
+
+    def smooth(self, l, x, b, zero_start, iters):
+        w, d, A = self.omega[l], self.invdiag[l], self.ops[l]
+        it = 0
+        if zero_start and iters > 0:
+            x = w * d * b
+            it = 1
+        for _ in range(it, iters):
+            x = x + w * d * (b - A.vmult(x))
+        return x
+
+    def coarse_matrix(self):
+        if not hasattr(self, "_A0"):
+            n = self.meshes[0].n_dofs
+            A = np.empty((n, n))
+            e = np.zeros(n)
+            for j in range(n):
+                e[j] = 1.0
+                A[:, j] = self.ops[0].vmult(e)
+                e[j] = 0.0
+            self._A0 = A
+        return self._A0
+
+    def v_step(self, l, b):
+        if l == 0:
+            if self.coarse_iters < 0:
+                return np.linalg.solve(self.coarse_matrix(), b)
+            if self.coarse_iters == 0:
+                return b.copy()
+            return self.smooth(0, None, b, True, self.coarse_iters)
+        x = self.smooth(l, None, b, True, self.n_smooth)
+        t = b - self.ops[l].vmult(x)
+        bc = np.zeros(self.meshes[l - 1].n_dofs)
+        self.restrict_add(l, bc, t)
+        xc = self.v_step(l - 1, bc)
+        x = x.copy()
+        self.prolongate_add(l, x, xc)
+        return self.smooth(l, x, b, False, self.n_smooth)
+
+    def vcycle(self, b):
+        return self.v_step(len(self.ops) - 1, np.asarray(b, dtype=np.float64))

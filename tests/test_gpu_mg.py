@@ -1,0 +1,155 @@
+"""GPU geometric multigrid (csrc/mg.hip through the C-ABI) vs the oracle-based
+CPU multigrid (tests/mg_ref.py) on the same level hierarchy and inputs.
+
+Level operators run in FP32 (MGNumber = float, config.h:7); the oracle runs
+in FP64, so the tolerances are FP32-level: transfers 1e-6, smoother /
+V-cycle 1e-4 relative l2, relaxation factor 1e-3 relative."""
+import numpy as np
+import pytest
+
+import glsinputs as gi
+from helpers import deck, rel_err
+from mg_ref import OracleGMG
+
+pytestmark = pytest.mark.gpu
+
+
+def _hierarchy(name, n_ref):
+    d = deck(name)
+    meshes = [d.mesh(r) for r in range(n_ref + 1)]
+    vel, p, slip = d.boundary_descriptor()
+    cmasks = [m.constraint_mask(vel, p, slip) for m in meshes]
+    params, w = d.operator_parameters(2.5e-4)
+    u = gi.linearization_point(meshes[-1].n_nodes, meshes[-1].dim, d.u_max)
+    hist = gi.history(u, params["order"])
+    return meshes, cmasks, params, w, u, hist
+
+
+def _np(t):
+    return t.double().cpu().numpy()
+
+
+CASES = [("input_turek_2D_Re20_stat.json", 2), ("input_hoffmann_3D_Re3900.json", 1),
+         ("input_turek_2D_Re100.json", 2)]
+
+
+@pytest.mark.parametrize("name,n_ref", CASES)
+def test_transfer(name, n_ref):
+    import torch
+    import glsamd
+    meshes, cmasks, params, w, u, hist = _hierarchy(name, n_ref)
+    mg, ops = glsamd.build_gmg(meshes, cmasks, params, u, hist, w, precision="f32")
+    ref = OracleGMG(meshes, cmasks, params, u, hist, w)
+    for l in range(1, len(meshes)):
+        xc = gi.rnd(5 + l, meshes[l - 1].n_dofs)
+        xf = gi.rnd(7 + l, meshes[l].n_dofs)
+        pf = ops[l].initialize_dof_vector()
+        mg.prolongate_add(l, pf, ops[l - 1]._dev(xc))
+        rc = ops[l - 1].initialize_dof_vector()
+        mg.restrict_add(l, rc, ops[l]._dev(xf))
+        ic = ops[l - 1].initialize_dof_vector()
+        mg.interpolate(l, ic, ops[l]._dev(xf))
+        torch.cuda.synchronize()
+        pref = np.zeros(meshes[l].n_dofs)
+        ref.prolongate_add(l, pref, xc)
+        rref = np.zeros(meshes[l - 1].n_dofs)
+        ref.restrict_add(l, rref, xf)
+        assert rel_err(_np(pf), pref) < 1e-6
+        assert rel_err(_np(rc), rref) < 1e-6
+        assert rel_err(_np(ic), ref.interpolate(l, xf)) < 1e-7
+
+
+@pytest.mark.parametrize("name,n_ref,coarse", [
+    ("input_turek_2D_Re20_stat.json", 2, -1),   # dense LU coarse solve ("direct")
+    ("input_turek_2D_Re20_stat.json", 2, 0),    # identity coarse solve
+    ("input_hoffmann_3D_Re3900.json", 1, 10),   # relaxation sweeps
+])
+def test_relaxation_and_vcycle(name, n_ref, coarse):
+    import torch
+    import glsamd
+    meshes, cmasks, params, w, u, hist = _hierarchy(name, n_ref)
+    mg, ops = glsamd.build_gmg(meshes, cmasks, params, u, hist, w, precision="f32",
+                               coarse_n_iterations=coarse)
+    ref = OracleGMG(meshes, cmasks, params, u, hist, w, coarse_iters=coarse)
+    # power-iteration relaxation factor (same start vector, FP32 vs FP64)
+    for l in range(len(meshes)):
+        omega, lam = mg.relaxation(l)
+        lam_ref = ref.estimate(l)
+        assert abs(lam - lam_ref) < 1e-3 * lam_ref
+        assert 0 < omega < 2 / lam
+    ref.set_omega([mg.relaxation(l)[0] for l in range(len(meshes))])
+    # one smoother application on the finest level (vmult from zero)
+    L = len(meshes) - 1
+    b = gi.rnd(11, meshes[L].n_dofs)
+    x = ops[L].initialize_dof_vector()
+    mg.smooth(L, x, ops[L]._dev(b), True)
+    torch.cuda.synchronize()
+    xr = ref.smooth(L, None, b, True, 5)
+    assert rel_err(_np(x), xr) < 1e-4
+    # full V-cycle, FP64 in / out (copy_to_mg / copy_from_mg)
+    src = torch.from_numpy(b).cuda()
+    dst = torch.zeros_like(src)
+    mg.vcycle(dst, src)
+    torch.cuda.synchronize()
+    # FP32 levels vs FP64 oracle; the stationary saddle-point deck amplifies
+    # round-off through the coarse LU (entries up to ~1e3 for O(1) input)
+    assert rel_err(_np(dst), ref.vcycle(b)) < 5e-4
+
+
+def _gmres(apply_A, apply_P, b, iters):
+    """Right-preconditioned GMRES without restart (test harness only; the
+    reference's LinearSolverGMRES, solver_l.cc:45-74, is out of scope)."""
+    import torch
+    beta = b.norm()
+    V = [b / beta]
+    Z = []
+    H = torch.zeros(iters + 1, iters, dtype=torch.float64)
+    res = [1.0]
+    for j in range(iters):
+        z = apply_P(V[j])
+        Z.append(z)
+        w = apply_A(z)
+        for i in range(j + 1):
+            H[i, j] = float(torch.dot(w, V[i]))
+            w = w - H[i, j] * V[i]
+        H[j + 1, j] = float(w.norm())
+        V.append(w / H[j + 1, j])
+        e1 = torch.zeros(j + 2, dtype=torch.float64)
+        e1[0] = float(beta)
+        y = torch.linalg.lstsq(H[:j + 2, :j + 1], e1).solution
+        res.append(float((H[:j + 2, :j + 1] @ y - e1).norm() / beta))
+    return res
+
+
+def test_vcycle_preconditions_gmres():
+    """The V-cycle is a useful preconditioner for the deck's Newton operator:
+    right-preconditioned GMRES reduces the residual much faster than
+    unpreconditioned GMRES (PreconditionerGMG inside LinearSolverGMRES)."""
+    import torch
+    import glsamd
+    meshes, cmasks, params, w, u, hist = _hierarchy("input_hoffmann_3D_Re3900.json", 1)
+    mg, ops = glsamd.build_gmg(meshes, cmasks, params, u, hist, w, precision="f32",
+                               coarse_n_iterations=10)
+    A = glsamd.NavierStokesOperator(meshes[-1], cmasks[-1], "f64")
+    A.set_parameters(**params)
+    A.set_linearization_point(u)
+    A.set_previous_solution(hist, w)
+    b = A._dev(gi.rnd(3, meshes[-1].n_dofs))
+
+    def apply_A(x):
+        y = torch.empty_like(x)
+        A.vmult(y, x)
+        return y
+
+    def apply_P(x):
+        y = torch.empty_like(x)
+        mg.vcycle(y, x)
+        return y
+
+    plain = _gmres(apply_A, lambda x: x, b, 20)
+    prec = _gmres(apply_A, apply_P, b, 20)
+    torch.cuda.synchronize()
+    print("gmres plain", plain[-1], "gmg", prec[-1])
+    # measured: 6.2e-3 after 20 iterations with a two-level FP32 V-cycle
+    assert prec[-1] < 1e-2, prec
+    assert prec[-1] < 0.25 * plain[-1], (prec[-1], plain[-1])
