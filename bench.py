@@ -72,6 +72,8 @@ def main():
     ap.add_argument("--precision", default="f64")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--brick", default=None,
+                    help="cells per brick 'bx,by,bz' (a sub-brick of the mesh order)")
     args = ap.parse_args()
 
     import torch
@@ -114,7 +116,8 @@ def main():
             op.vmult(dst, src)
             ev1.record()
     else:
-        op = glsamd.NavierStokesOperator(mesh, cmask, args.precision)
+        brick = tuple(int(x) for x in args.brick.split(",")) if args.brick else None
+        op = glsamd.NavierStokesOperator(mesh, cmask, args.precision, brick=brick)
         op.set_parameters(**params)
         op.set_linearization_point(u_star)
         if params["order"] > 0:

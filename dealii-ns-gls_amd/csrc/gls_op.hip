@@ -129,17 +129,26 @@ void
 build_bricks(glsOp_ *op, const glsOpDesc *d)
 {
   const int dim = op->dim, k = op->degree, n = k + 1;
-  const int bx = d->brick[0], by = d->brick[1], bz = dim == 3 ? d->brick[2] : 1;
+  const int bx = d->brick[0], by = d->brick[1];
+  int       bz = dim == 3 ? d->brick[2] : 1;
   if (bx <= 0 || by <= 0 || bz <= 0)
     return;
+  // 3D: run the bricks as their one-cell-thick z layers (each layer of a
+  // lexicographic brick is a contiguous cell range): twice the workgroups
+  // for the same cells evens out the per-CU load (800 4x4x2 bricks on 256
+  // CUs leave a 32-brick second round) and the padded LDS lattice of a
+  // 4x4x1 layer keeps 3 workgroups per CU (measured 59.6 -> 53.7 us before
+  // the LDS re-layout)
+  if (dim == 3)
+    bz = 1;
   const int64_t cpb = (int64_t)bx * by * bz;
   if (d->n_cells % cpb != 0)
     throw std::runtime_error("gls_op_create: n_cells is not a multiple of the brick size");
   const int Lx = k * bx + 1, Ly = k * by + 1, Lz = dim == 3 ? k * bz + 1 : 1;
   const int L  = Lx * Ly * Lz;
   const int side_max = k * (dim == 3 ? 4 : 8) + 1;
-  const int lmax     = dim == 3 ? side_max * side_max * side_max : side_max * side_max;
-  if (L > lmax || lmax > 729 || (dim == 3 && (bx > 4 || by > 4 || bz > 4)) ||
+  const int lmax     = dim == 3 ? side_max * side_max * (k + 1) : side_max * side_max;
+  if (L > lmax || lmax > 729 || (dim == 3 && (bx > 4 || by > 4 || bz > 1)) ||
       (dim == 2 && (bx > 8 || by > 8)))
     return; // lattice does not fit the brick kernel's LDS: per-cell path
   const int64_t nb = d->n_cells / cpb;
@@ -388,11 +397,9 @@ struct Impl
         BrickArgs<T, dim, n> a;
         a.brick_nodes   = op->d_brick_nodes;
         a.brick_target  = op->d_brick_target;
-        a.cell_geo      = op->d_cell_geo;
-        a.geo_cart      = (const T *)op->d_geo_cart;
-        a.n_cart        = op->n_cart;
-        a.geo_gen       = (const T *)op->d_geo_gen;
-        a.n_gen         = op->n_gen;
+        a.brick_geo     = op->d_brick_geo;
+        a.geo_cart      = (const T *)op->d_bgeo_cart; // cell-indexed
+        a.geo_gen       = (const T *)op->d_bgeo_gen;  // cell-indexed
         a.tab           = (const T *)op->d_tab;
         a.n_cells       = op->n_cells;
         a.cellwise      = (const T *)op->d_cellwise;
@@ -408,6 +415,12 @@ struct Impl
         a.L             = op->L;
         a.Lx            = op->Lx;
         a.Ly            = op->Ly;
+        // padded LDS lattice: 3D Q2 bricks of 4x4 cells in x, y use strides
+        // 11, 12 (ds_read_b128 conflict-free x sweep, exhaustive search)
+        const bool pad  = dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9;
+        a.PLx           = pad ? 11 : op->Lx;
+        a.PLy           = pad ? 12 : op->Ly;
+        a.LP            = a.PLx * a.PLy * (op->L / (op->Lx * op->Ly));
         a.nu            = (T)op->prm.nu;
         a.w0            = (T)op->prm.w0;
         a.theta         = (T)op->prm.theta;
@@ -416,13 +429,14 @@ struct Impl
         a.have_prev     = op->have_prev ? 1 : 0;
         a.have_old_grad = (op->have_old_grad && op->prm.theta != 1.0) ? 1 : 0;
         a.sh            = make_shape<T, n>(op->basis);
-        const dim3 grid((unsigned)op->n_bricks);
+        const dim3   grid((unsigned)op->n_bricks);
+        const size_t lds = BrickLDS<dim, k, T>::bytes(a.LP);
         if (mode == MODE_NEWTON)
-          hipLaunchKernelGGL((k_brick<dim, k, T, MODE_NEWTON>), grid, dim3(BLOCK), 0, s, a);
+          hipLaunchKernelGGL((k_brick<dim, k, T, MODE_NEWTON>), grid, dim3(BLOCK), lds, s, a);
         else if (mode == MODE_FIXED)
-          hipLaunchKernelGGL((k_brick<dim, k, T, MODE_FIXED>), grid, dim3(BLOCK), 0, s, a);
+          hipLaunchKernelGGL((k_brick<dim, k, T, MODE_FIXED>), grid, dim3(BLOCK), lds, s, a);
         else
-          hipLaunchKernelGGL((k_brick<dim, k, T, MODE_RESIDUAL>), grid, dim3(BLOCK), 0, s, a);
+          hipLaunchKernelGGL((k_brick<dim, k, T, MODE_RESIDUAL>), grid, dim3(BLOCK), lds, s, a);
         HIP_THROW(hipGetLastError());
         if (op->n_shared > 0)
           {
@@ -712,8 +726,66 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
                            std::pow(6 * hk / M_PI, 1. / 3.) / d->degree;
       hmin[c] = d->cell_hmin[c];
     }
+  // brick path: the same geometry indexed by CELL ([field][cell] Cartesian,
+  // [field][plane][cell][line] curved; only the curved cells' entries of the
+  // latter are ever read), so no geometry load waits for a cell_geo load
+  // A brick with any curved cell is a curved brick: all its cells get per-q
+  // geometry (a Cartesian cell's per-q JxW = det * w_q, J^{-1} = its
+  // diagonal: the same numbers the Cartesian path forms), so the geometry
+  // type is uniform per workgroup.
+  std::vector<double>   bcart, bgen;
+  std::vector<uint32_t> bgeo;
+  if (op->use_brick)
+    {
+      const int64_t C   = d->n_cells;
+      const int64_t cpb = C / op->n_bricks;
+      bcart.assign((size_t)ncf * C, 0.0);
+      bgen.assign((size_t)ngf * C * nq, 0.0);
+      bgeo.assign((size_t)op->n_bricks, 0u);
+      for (int64_t c = 0; c < C; ++c)
+        if (cell_geo[c] & GEO_GENERAL)
+          bgeo[c / cpb] = 1u;
+      for (int64_t c = 0; c < C; ++c)
+        {
+          const uint32_t cg = cell_geo[c];
+          if (!bgeo[c / cpb])
+            {
+              for (int f = 0; f < ncf; ++f)
+                bcart[(size_t)f * C + c] = cart_rows[(size_t)cg * ncf + f];
+              continue;
+            }
+          for (int q = 0; q < nq; ++q)
+            {
+              double vals[1 + 9] = {0};
+              if (cg & GEO_GENERAL)
+                {
+                  const int64_t g = cg & ~GEO_GENERAL;
+                  for (int f = 0; f < ngf; ++f)
+                    vals[f] = gen_rows[((size_t)g * nq + q) * ngf + f];
+                }
+              else
+                {
+                  const int qa[3] = {q % n, (q / n) % n, dim == 3 ? q / (n * n) : 0};
+                  double    w     = op->basis.qw[qa[0]] * op->basis.qw[qa[1]];
+                  if (dim == 3)
+                    w *= op->basis.qw[qa[2]];
+                  vals[0] = cart_rows[(size_t)cg * ncf + dim] * w;
+                  for (int e = 0; e < dim; ++e)
+                    vals[1 + e * dim + e] = cart_rows[(size_t)cg * ncf + e];
+                }
+              for (int f = 0; f < ngf; ++f)
+                bgen[(size_t)f * C * nq + host_qindex(dim, n, c, q, C)] = vals[f];
+            }
+        }
+      upload((void **)&op->d_brick_geo, bgeo);
+    }
   if (op->prec == GLS_F64)
     {
+      if (op->use_brick)
+        {
+          upload(&op->d_bgeo_cart, bcart);
+          upload(&op->d_bgeo_gen, bgen);
+        }
       upload(&op->d_geo_cart, cart);
       upload(&op->d_geo_gen, gen);
       upload(&op->d_hq, hq);
@@ -721,6 +793,11 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
     }
   else
     {
+      if (op->use_brick)
+        {
+          upload(&op->d_bgeo_cart, convert<float>(bcart));
+          upload(&op->d_bgeo_gen, convert<float>(bgen));
+        }
       upload(&op->d_geo_cart, convert<float>(cart));
       upload(&op->d_geo_gen, convert<float>(gen));
       upload(&op->d_hq, convert<float>(hq));
@@ -748,7 +825,8 @@ gls_op_destroy(glsOp op)
                   op->d_tab,          op->d_cellwise,     op->d_old_grad,     op->d_hq,
                   op->d_hmin,         op->d_tmp,          op->d_cbits,        op->d_brick_nodes,
                   op->d_brick_target, op->d_shared_nodes, op->d_shared_off,
-                  op->d_partial};
+                  op->d_partial,      op->d_bgeo_cart,    op->d_bgeo_gen,
+                  op->d_brick_geo};
   for (void *b : bufs)
     if (b)
       (void)hipFree(b);

@@ -121,6 +121,31 @@ load_node<float, 4>(const float *__restrict__ v, uint32_t node, float (&u)[4])
   u[0] = a.x, u[1] = a.y, u[2] = a.z, u[3] = a.w;
 }
 
+template <typename T, int nc>
+__device__ __forceinline__ void
+store_node(T *__restrict__ v, uint32_t node, const T (&u)[nc])
+{
+#pragma unroll
+  for (int c = 0; c < nc; ++c)
+    v[(size_t)node * nc + c] = u[c];
+}
+
+template <>
+__device__ __forceinline__ void
+store_node<double, 4>(double *__restrict__ v, uint32_t node, const double (&u)[4])
+{
+  double2 *p = reinterpret_cast<double2 *>(v + (size_t)node * 4);
+  p[0]       = make_double2(u[0], u[1]);
+  p[1]       = make_double2(u[2], u[3]);
+}
+
+template <>
+__device__ __forceinline__ void
+store_node<float, 4>(float *__restrict__ v, uint32_t node, const float (&u)[4])
+{
+  *reinterpret_cast<float4 *>(v + (size_t)node * 4) = make_float4(u[0], u[1], u[2], u[3]);
+}
+
 // 1D contraction along an axis with stride `s` (n points):
 //   forward:   out[p] = sum_j M[pa][j] in[base + j s]
 //   transpose: out[p] = sum_j M[j][pa] in[base + j s]

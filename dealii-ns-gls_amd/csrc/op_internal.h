@@ -46,6 +46,9 @@ struct glsOp_
   uint32_t *d_shared_nodes = nullptr;
   uint32_t *d_shared_off   = nullptr;
   void     *d_partial      = nullptr;
+  void     *d_bgeo_cart    = nullptr; // brick path: cell-indexed geometry
+  void     *d_bgeo_gen     = nullptr;
+  uint32_t *d_brick_geo    = nullptr; // per brick: curved (1) or Cartesian (0)
 
   size_t
   tsize() const
