@@ -22,7 +22,7 @@ MESH_SRC := $(PKG)/host/mesh.cc
 AMD_SRC  := $(wildcard $(PKG)/csrc/*.hip) $(wildcard $(PKG)/csrc/*.cc)
 AMD_HDR  := $(wildcard $(PKG)/csrc/*.h) $(wildcard $(PKG)/csrc/*.cuh) include/gls_op.h
 
-all: mesh amd oracle
+all: mesh amd oracle cpptest
 
 mesh: $(LIBDIR)/libglsmesh.so
 amd: $(LIBDIR)/libglsamd.so
@@ -37,11 +37,22 @@ $(LIBDIR)/libglsamd.so: $(AMD_SRC) $(AMD_HDR)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(AMD_SRC) $(AMD_LIBS)
 
+# C++ facade parity program (test infrastructure: links the oracle)
+CPPTEST := tests/cpp/build/test_operator
+cpptest: $(CPPTEST)
+$(CPPTEST): tests/cpp/test_operator.cc include/gls_operator.hpp include/gls_op.h include/gls_mesh.h \
+            $(LIBDIR)/libglsamd.so $(LIBDIR)/libglsmesh.so oracle
+	@mkdir -p tests/cpp/build
+	$(CXX) -O2 -std=c++17 -Wall -D__HIP_PLATFORM_AMD__ -Iinclude -I/opt/rocm/include -o $@ $< \
+	  -L$(LIBDIR) -lglsamd -lglsmesh -Loracle -loracle -L/opt/rocm/lib -lamdhip64 \
+	  -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../../oracle' \
+	  -Wl,-rpath,/opt/rocm/lib
+
 clean:
-	rm -f $(LIBDIR)/*.so
+	rm -f $(LIBDIR)/*.so $(CPPTEST)
 	$(MAKE) -C oracle clean
 
-.PHONY: all mesh amd oracle clean
+.PHONY: all mesh amd oracle cpptest clean
 
 # diagnostic ablation builds (timing only, wrong results by design)
 abl:

@@ -308,6 +308,10 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
   const int64_t brick = a.brick_begin + blockIdx.x;
   if (brick >= a.brick_end)
     return;
+#ifdef GLS_BLIMIT
+  if (blockIdx.x >= GLS_BLIMIT) // diagnostic: time a partial grid
+    return;
+#endif
   const int t   = threadIdx.x;
   const int cpb = a.bx * a.by * a.bz;
   if (t < n * n)

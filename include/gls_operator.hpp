@@ -1,0 +1,192 @@
+// gls_operator.hpp — header-only C++17 facade over the C ABI of
+// libglsamd.so (include/gls_op.h): the host-side mirror of the reference's
+// OperatorBase<Number> (include/operator_base.h:13-73) and
+// PreconditionerGMG (include/multigrid.h:61-141) for the matrix-free GLS
+// Navier–Stokes operator on MI355X.
+//
+// RAII handles; a nonzero status becomes gls::Error (std::runtime_error)
+// carrying gls_last_error() — the reference's AssertThrow convention.
+// Vectors are device pointers in the operator's precision, local layout
+// [owned | ghost], dof = node * (dim+1) + component.  Calls are
+// stream-ordered (hipStream_t passed as void*, nullptr = default stream)
+// and, like the reference's const-but-mutable operator, not reentrant per
+// handle.
+#pragma once
+
+#include "gls_op.h"
+
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace gls
+{
+class Error : public std::runtime_error
+{
+public:
+  using std::runtime_error::runtime_error;
+};
+
+inline void
+check(glsStatus s, const char *what)
+{
+  if (s != 0)
+    throw Error(std::string(what) + ": " + gls_last_error());
+}
+
+// the scalars NavierStokesOperator / TimeIntegratorData feed the cell kernel
+// (operator_ns.h:102-114, time_integration.h:10-36)
+struct Parameters
+{
+  double nu = 1, c1 = 1, c2 = 1;
+  double theta = 1;  // get_theta()
+  double w0    = 0;  // get_primary_weight()
+  double dt    = 1;  // get_current_dt()
+  int    order = 0;  // get_order()
+  int    flags = 0;  // GLS_INCREMENT_FORM | GLS_CONSIDER_TIME_DERIVATIVE | GLS_CELL_WISE_STAB
+};
+
+class Operator
+{
+public:
+  Operator() = default;
+  explicit Operator(const glsOpDesc &desc) { check(gls_op_create(&desc, &h), "gls_op_create"); }
+  ~Operator()
+  {
+    if (h)
+      gls_op_destroy(h);
+  }
+  Operator(const Operator &)            = delete;
+  Operator &operator=(const Operator &) = delete;
+  Operator(Operator &&o) noexcept : h(std::exchange(o.h, nullptr)) {}
+  Operator &
+  operator=(Operator &&o) noexcept
+  {
+    if (this != &o)
+      {
+        if (h)
+          gls_op_destroy(h);
+        h = std::exchange(o.h, nullptr);
+      }
+    return *this;
+  }
+
+  glsOp handle() const { return h; }
+
+  // OperatorBase::m()  operator_base.h:23-24
+  int64_t m() const { return gls_op_m(h); }
+
+  void
+  set_parameters(const Parameters &p)
+  {
+    const glsOpParams q{p.nu, p.c1, p.c2, p.theta, p.w0, p.dt, p.order, p.flags};
+    check(gls_op_set_parameters(h, &q), "gls_op_set_parameters");
+  }
+
+  // operator_base.h:38-39 (operator_ns.cc:570-620)
+  void
+  set_linearization_point(const void *src, void *stream = nullptr)
+  {
+    check(gls_op_set_linearization_point(h, src, stream), "set_linearization_point");
+  }
+
+  // operator_base.h:35-36 (operator_ns.cc:234-320): history[0] unused,
+  // weights[i] the BDF weights of TimeIntegratorData::get_weights()
+  void
+  set_previous_solution(const std::vector<const void *> &history,
+                        const std::vector<double> &weights, void *stream = nullptr)
+  {
+    check(gls_op_set_previous_solution(h, history.data(), (int)history.size(), weights.data(),
+                                       stream),
+          "set_previous_solution");
+  }
+
+  // operator_base.h:47-48 (operator_ns.cc:684-732)
+  void
+  vmult(void *dst, const void *src, void *stream = nullptr) const
+  {
+    check(gls_op_vmult(h, dst, src, stream), "vmult");
+  }
+
+  // operator_base.h:44-46 (operator_ns.cc:648-682)
+  void
+  evaluate_residual(void *dst, const void *src, void *stream = nullptr) const
+  {
+    check(gls_op_evaluate_residual(h, dst, src, stream), "evaluate_residual");
+  }
+
+  // operator_base.h:29-30 (operator_ns.cc:195-225)
+  void
+  compute_inverse_diagonal(void *diag, void *stream = nullptr) const
+  {
+    check(gls_op_compute_inverse_diagonal(h, diag, stream), "compute_inverse_diagonal");
+  }
+
+  // identity rows after a ghost export-add (distributed vmult)
+  void
+  apply_identity_rows(void *dst, const void *src, void *stream = nullptr) const
+  {
+    check(gls_op_apply_identity_rows(h, dst, src, stream), "apply_identity_rows");
+  }
+
+  double vmult_bytes() const { return gls_op_vmult_bytes(h); }
+
+private:
+  glsOp h = nullptr;
+};
+
+// PreconditionerGMG: level operators (MGNumber precision), transfers,
+// relaxation smoother, V-cycle
+class Multigrid
+{
+public:
+  Multigrid() = default;
+  Multigrid(const glsMGDesc &desc, const std::vector<const Operator *> &levels,
+            const std::vector<const uint32_t *> &child_lattices)
+  {
+    std::vector<glsOp> ops;
+    for (const Operator *o : levels)
+      ops.push_back(o->handle());
+    std::vector<const uint32_t *> ch(levels.size(), nullptr);
+    for (size_t l = 1; l < levels.size() && l - 1 < child_lattices.size(); ++l)
+      ch[l] = child_lattices[l - 1];
+    check(gls_mg_create(&desc, ops.data(), ch.data(), &h), "gls_mg_create");
+  }
+  ~Multigrid()
+  {
+    if (h)
+      gls_mg_destroy(h);
+  }
+  Multigrid(const Multigrid &)            = delete;
+  Multigrid &operator=(const Multigrid &) = delete;
+  Multigrid(Multigrid &&o) noexcept : h(std::exchange(o.h, nullptr)) {}
+
+  // PreconditionerGMG::initialize (multigrid.cc:247-370)
+  void initialize(void *stream = nullptr) { check(gls_mg_setup(h, stream), "gls_mg_setup"); }
+
+  // PreconditionerGMG::vmult (multigrid.cc:202-220): one V-cycle
+  void
+  vmult(void *dst, const void *src, void *stream = nullptr) const
+  {
+    check(gls_mg_vcycle(h, dst, src, stream), "gls_mg_vcycle");
+  }
+
+  std::pair<double, double>
+  relaxation(int level) const
+  {
+    double w = 0, lam = 0;
+    check(gls_mg_get_relaxation(h, level, &w, &lam), "gls_mg_get_relaxation");
+    return {w, lam};
+  }
+
+  void
+  interpolate(int level, void *dst_coarse, const void *src_fine, void *stream = nullptr) const
+  {
+    check(gls_mg_interpolate(h, level, dst_coarse, src_fine, stream), "gls_mg_interpolate");
+  }
+
+private:
+  glsMG h = nullptr;
+};
+} // namespace gls

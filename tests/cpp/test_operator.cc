@@ -1,0 +1,250 @@
+// TEST INFRASTRUCTURE: C++ parity check of the HIP operator through the
+// header-only facade include/gls_operator.hpp (the host-side mirror of the
+// reference's OperatorBase), against the CPU oracle (oracle/gls_oracle.h)
+// on the same mesh and §8d synthetic inputs.  Driven by tests/test_cpp.py.
+//
+//   test_operator dim degree n_ref length height position diameter shift
+//                 vel_bits p_bits slip_bits u_inf nu c1 c2 theta dt order
+//                 flags w0 [w1 w2 w3]
+// exit 0: all relative l2 errors < 1e-12 and the error path throws.
+#include "gls_mesh.h"
+#include "gls_operator.hpp"
+#include "../../oracle/gls_oracle.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+static uint64_t
+splitmix64(uint64_t x)
+{
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z          = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z          = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// glsinputs.rnd: ((splitmix64(seed * 2^32 + i) >> 11) * 2^-53) * 2 - 1
+static std::vector<double>
+rnd(uint64_t seed, size_t n)
+{
+  std::vector<double> r(n);
+  for (size_t i = 0; i < n; ++i)
+    r[i] = (double)(splitmix64(seed * (1ull << 32) + i) >> 11) * 0x1.0p-53 * 2.0 - 1.0;
+  return r;
+}
+
+static double
+rel_err(const std::vector<double> &a, const std::vector<double> &b)
+{
+  double num = 0, den = 0;
+  for (size_t i = 0; i < a.size(); ++i)
+    {
+      num += (a[i] - b[i]) * (a[i] - b[i]);
+      den += b[i] * b[i];
+    }
+  return std::sqrt(num) / std::max(std::sqrt(den), 1e-300);
+}
+
+#define HIPCHK(x)                                                              \
+  do                                                                           \
+    {                                                                          \
+      if ((x) != hipSuccess)                                                   \
+        {                                                                      \
+          std::fprintf(stderr, "HIP error %s line %d\n", #x, __LINE__);        \
+          return 2;                                                            \
+        }                                                                      \
+    }                                                                          \
+  while (0)
+
+struct DevVec
+{
+  double *p = nullptr;
+  size_t  n = 0;
+  explicit DevVec(size_t n_) : n(n_) { (void)hipMalloc(&p, n * sizeof(double)); }
+  ~DevVec() { (void)hipFree(p); }
+  void up(const std::vector<double> &h) { (void)hipMemcpy(p, h.data(), n * 8, hipMemcpyHostToDevice); }
+  std::vector<double>
+  down() const
+  {
+    std::vector<double> h(n);
+    (void)hipMemcpy(h.data(), p, n * 8, hipMemcpyDeviceToHost);
+    return h;
+  }
+};
+
+static int run(int argc, char **argv);
+
+int
+main(int argc, char **argv)
+{
+  try
+    {
+      return run(argc, argv);
+    }
+  catch (const std::exception &e)
+    {
+      std::printf("uncaught: %s\n", e.what());
+      return 2;
+    }
+}
+
+static int
+run(int argc, char **argv)
+{
+  if (argc < 21)
+    {
+      std::fprintf(stderr, "usage: see header\n");
+      return 2;
+    }
+  int         a = 1;
+  const int   dim = std::atoi(argv[a++]), degree = std::atoi(argv[a++]), n_ref = std::atoi(argv[a++]);
+  const double length = std::atof(argv[a++]), height = std::atof(argv[a++]),
+               position = std::atof(argv[a++]), diameter = std::atof(argv[a++]),
+               shift = std::atof(argv[a++]);
+  const uint32_t vel = (uint32_t)std::atol(argv[a++]), pb = (uint32_t)std::atol(argv[a++]),
+                 slip = (uint32_t)std::atol(argv[a++]);
+  const double u_inf = std::atof(argv[a++]);
+  gls::Parameters prm;
+  prm.nu    = std::atof(argv[a++]);
+  prm.c1    = std::atof(argv[a++]);
+  prm.c2    = std::atof(argv[a++]);
+  prm.theta = std::atof(argv[a++]);
+  prm.dt    = std::atof(argv[a++]);
+  prm.order = std::atoi(argv[a++]);
+  prm.flags = std::atoi(argv[a++]);
+  std::vector<double> w;
+  for (; a < argc; ++a)
+    w.push_back(std::atof(argv[a]));
+  prm.w0 = w.empty() ? 0.0 : w[0];
+
+  glsMesh *mesh = nullptr;
+  if (gls_mesh_cylinder(dim, degree, n_ref, length, height, position, diameter, shift, &mesh))
+    {
+      std::fprintf(stderr, "mesh: %s\n", gls_mesh_last_error());
+      return 2;
+    }
+  const int64_t        nc = gls_mesh_n_cells(mesh), nn = gls_mesh_n_nodes(mesh);
+  const int            ncomp = dim + 1;
+  const size_t         ndof  = (size_t)nn * ncomp;
+  std::vector<uint8_t> cmask((size_t)nn);
+  std::vector<double>  meas((size_t)nc), hmin((size_t)nc);
+  int                  brick[3] = {0, 0, 0};
+  if (gls_mesh_constraint_mask(mesh, vel, pb, slip, cmask.data()) ||
+      gls_mesh_cell_measure(mesh, meas.data(), hmin.data()) || gls_mesh_brick(mesh, brick))
+    {
+      std::fprintf(stderr, "mesh: %s\n", gls_mesh_last_error());
+      return 2;
+    }
+
+  glsOpDesc d{};
+  d.dim           = dim;
+  d.degree        = degree;
+  d.precision     = GLS_F64;
+  d.n_cells       = nc;
+  d.n_nodes       = nn;
+  d.n_owned_nodes = nn;
+  d.cell_nodes    = gls_mesh_cell_nodes(mesh);
+  d.node_coords   = gls_mesh_node_coords(mesh);
+  d.node_cmask    = cmask.data();
+  d.cell_measure  = meas.data();
+  d.cell_hmin     = hmin.data();
+  for (int i = 0; i < 3; ++i)
+    d.brick[i] = brick[i];
+
+  // error convention: an invalid descriptor throws gls::Error
+  {
+    glsOpDesc bad     = d;
+    bad.n_owned_nodes = nn + 1;
+    bool thrown       = false;
+    try
+      {
+        gls::Operator op(bad);
+      }
+    catch (const gls::Error &e)
+      {
+        thrown = true;
+        std::printf("error path ok: %s\n", e.what());
+        std::fflush(stdout);
+      }
+    if (!thrown)
+      {
+        std::fprintf(stderr, "invalid descriptor did not throw\n");
+        return 1;
+      }
+  }
+
+  // §8d inputs (glsinputs.py)
+  std::vector<double> src = rnd(1, ndof), r2 = rnd(2, ndof), u(ndof);
+  for (int64_t i = 0; i < nn; ++i)
+    {
+      u[i * ncomp] = u_inf * (1.0 + 0.1 * r2[i * ncomp]);
+      for (int c = 1; c < dim; ++c)
+        u[i * ncomp + c] = 0.1 * u_inf * r2[i * ncomp + c];
+      u[i * ncomp + dim] = r2[i * ncomp + dim];
+    }
+  std::vector<std::vector<double>> hist(1, u);
+  for (int i = 1; i <= prm.order; ++i)
+    {
+      std::vector<double> h(u);
+      for (double &x : h)
+        x *= 1.0 - 0.01 * i;
+      hist.push_back(h);
+    }
+
+  // HIP operator through the facade
+  gls::Operator op(d);
+  op.set_parameters(prm);
+  DevVec dsrc(ndof), du(ndof), ddst(ndof), dres(ndof), ddiag(ndof);
+  dsrc.up(src);
+  du.up(u);
+  op.set_linearization_point(du.p);
+  std::vector<DevVec *> dh;
+  std::vector<const void *> hp;
+  for (auto &h : hist)
+    {
+      dh.push_back(new DevVec(ndof));
+      dh.back()->up(h);
+      hp.push_back(dh.back()->p);
+    }
+  if (prm.order > 0)
+    op.set_previous_solution(hp, w);
+  op.vmult(ddst.p, dsrc.p);
+  op.evaluate_residual(dres.p, dsrc.p);
+  op.compute_inverse_diagonal(ddiag.p);
+  HIPCHK(hipDeviceSynchronize());
+  const std::vector<double> g_dst = ddst.down(), g_res = dres.down(), g_diag = ddiag.down();
+  for (DevVec *p : dh)
+    delete p;
+
+  // oracle
+  orc_mesh   om{dim, degree, nc, nn, d.cell_nodes, d.node_coords, cmask.data(), meas.data(),
+              hmin.data()};
+  orc_params oprm{prm.nu, prm.c1, prm.c2, prm.theta, prm.w0, prm.dt, prm.order,
+                  (prm.flags & GLS_CONSIDER_TIME_DERIVATIVE) ? 1 : 0,
+                  (prm.flags & GLS_INCREMENT_FORM) ? 1 : 0,
+                  (prm.flags & GLS_CELL_WISE_STAB) ? 1 : 0};
+  orc_op    *o = orc_create(&om, &oprm);
+  orc_set_linearization_point(o, u.data());
+  if (prm.order > 0)
+    {
+      std::vector<const double *> hh;
+      for (auto &h : hist)
+        hh.push_back(h.data());
+      orc_set_previous_solution(o, hh.data(), (int)hh.size(), w.data());
+    }
+  std::vector<double> c_dst(ndof), c_res(ndof), c_diag(ndof);
+  orc_vmult(o, c_dst.data(), src.data());
+  orc_evaluate_residual(o, c_res.data(), src.data());
+  orc_compute_inverse_diagonal(o, c_diag.data());
+  orc_destroy(o);
+  gls_mesh_destroy(mesh);
+
+  const double e0 = rel_err(g_dst, c_dst), e1 = rel_err(g_res, c_res), e2 = rel_err(g_diag, c_diag);
+  std::printf("cells %lld dofs %zu  vmult %.3e  residual %.3e  inverse_diagonal %.3e\n",
+              (long long)nc, ndof, e0, e1, e2);
+  return (e0 < 1e-12 && e1 < 1e-12 && e2 < 1e-12) ? 0 : 1;
+}
