@@ -26,16 +26,33 @@
 
 #include "kernels.h"
 
-// GLS_BABL: diagnostic ablations of k_brick (timing only, wrong results):
-// 1 trivial q-point physics, 2 no evaluate sweeps, 4 no per-q table loads,
-// 8 no integrate sweeps, 16 no src gather, 32 no write-out, 64 no cell rounds
-#ifndef GLS_BABL
-#define GLS_BABL 0
-#endif
 
 namespace gls
 {
-constexpr uint32_t SHARED_BIT = 0x80000000u;
+constexpr uint32_t SHARED_BIT  = 0x80000000u;
+constexpr uint32_t UNUSED_NODE = 0x0FFFFFFFu; // lattice node outside a split brick
+
+// GLS_STAMPS: diagnostic timeline build (never the product library): lane 0
+// of every wave records s_memrealtime (100 MHz) at phase boundaries of each
+// brick into g_stamps[brick][wave][8].
+#ifdef GLS_STAMPS
+constexpr size_t GLS_STAMP_MAX = 16384 * 4 * 8;
+__device__ unsigned long long g_stamps[GLS_STAMP_MAX];
+#define GLS_STAMP(brick, i)                                                                   \
+  do                                                                                         \
+    {                                                                                        \
+      const size_t si_ = ((size_t)(brick) * (BLOCK / 64) + (threadIdx.x >> 6)) * 8 + (i);    \
+      if ((threadIdx.x & 63) == 0 && si_ < GLS_STAMP_MAX)                                    \
+        g_stamps[si_] = __builtin_amdgcn_s_memrealtime();                                    \
+    }                                                                                        \
+  while (0)
+#else
+#define GLS_STAMP(brick, i)                                                                   \
+  do                                                                                         \
+    {                                                                                        \
+    }                                                                                        \
+  while (0)
+#endif
 
 template <int dim>
 struct BrickMax
@@ -66,7 +83,9 @@ struct BrickArgs
 {
   const uint32_t *brick_nodes;  // [n_bricks][L] node | cmask << 28
   const uint32_t *brick_target; // [n_bricks][L] node, or SHARED_BIT | slot
-  const uint32_t *brick_geo; // per brick: 1 = curved (per-q geometry for all its cells)
+  const uint32_t *brick_geo; // per brick: bit 0 curved (per-q geometry for all its
+                             // cells) | number of cells << 8
+  const uint32_t *brick_cell0; // per brick: first cell
   const T        *geo_cart;  // [dim+1][cell]               (cells of Cartesian bricks)
   const T        *geo_gen;   // [1+dim^2][plane][cell][line] (cells of curved bricks)
   const T        *tab;      // [field][plane][cell][line]
@@ -104,15 +123,37 @@ struct Pack<float>
   static constexpr int W = 4;
 };
 
+// 1D coefficient row of a lane: M[pa][j] (TR false) or M[j][pa] (TR true),
+// read once into registers and applied to every component pack (the LDS
+// stores of a sweep may alias the tables, so reading M inside the pack loop
+// would re-read it after every store)
+template <int n, bool TR, typename T>
+__device__ __forceinline__ void
+coefs(const T (*M)[n], int pa, T (&c)[n])
+{
+#pragma unroll
+  for (int j = 0; j < n; ++j)
+    c[j] = TR ? M[j][pa] : M[pa][j];
+}
+
+template <int n, typename T, typename V>
+__device__ __forceinline__ V
+contract_c(const V *in, const T (&c)[n], int base, int s)
+{
+  V acc = c[0] * in[base];
+#pragma unroll
+  for (int j = 1; j < n; ++j)
+    acc += c[j] * in[base + j * s];
+  return acc;
+}
+
 template <int n, bool TR, typename T, typename V>
 __device__ __forceinline__ V
 contract_v(const V *in, const T (*M)[n], int pa, int base, int s)
 {
-  V acc = (TR ? M[0][pa] : M[pa][0]) * in[base];
-#pragma unroll
-  for (int j = 1; j < n; ++j)
-    acc += (TR ? M[j][pa] : M[pa][j]) * in[base + j * s];
-  return acc;
+  T c[n];
+  coefs<n, TR>(M, pa, c);
+  return contract_c<n>(in, c, base, s);
 }
 
 // Sweep-buffer layout of one cell (in packs): point (x, y, z) at
@@ -171,20 +212,19 @@ struct LaneData
 // for once, at the q-point physics.
 template <int dim, int k, typename T, int MODE>
 __device__ __forceinline__ void
-load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t brick, bool general, int lcell,
+load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int ncell, bool general, int lcell,
           bool in_wave, int p, const int (&pa)[3], LaneData<dim, T, MODE> &r)
 {
   constexpr int n   = k + 1;
   constexpr int nq  = ipow(n, dim);
   constexpr bool R  = MODE == MODE_RESIDUAL;
   using F           = Fields<dim>;
-  const int     cpb = a.bx * a.by * a.bz;
-  r.active          = in_wave && lcell < cpb;
+  r.active          = in_wave && lcell < ncell;
   const int cx      = r.active ? lcell % a.bx : 0;
   const int cy      = r.active ? (lcell / a.bx) % a.by : 0;
   const int cz      = r.active ? lcell / (a.bx * a.by) : 0;
   r.li = (cx * k + pa[0]) + a.PLx * ((cy * k + pa[1]) + a.PLy * (cz * k + pa[2]));
-  const int64_t cell = brick * cpb + lcell;
+  const int64_t cell = cell0 + lcell;
   const int64_t nqc  = a.n_cells * nq;
   r.JxW = r.d1 = r.d2 = 0;
 #pragma unroll
@@ -224,15 +264,28 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t brick, bool general, int lc
         r.inv[i][i] = a.geo_cart[i * a.n_cells + cell];
       r.JxW = a.geo_cart[dim * a.n_cells + cell] * w;
     }
-  if (GLS_BABL & 4)
+#ifdef GLS_TABX
+  // timing-only ablation: per-wave-round contiguous 16-byte table loads
+  if constexpr (sizeof(T) == 8 && dim == 3)
     {
+      typedef double D2 __attribute__((ext_vector_type(2)));
+      const D2 *tb = reinterpret_cast<const D2 *>(a.tab) + (cell / 2) * (10 * 54) +
+                     (lcell % 2) * 27 + p;
+      D2 g[10];
 #pragma unroll
-      for (int d = 0; d < dim; ++d)
-        r.U[d] = T(1) + d;
-      r.d1 = T(1e-4) * p;
-      r.d2 = T(1e-3);
+      for (int i = 0; i < 10; ++i)
+        g[i] = tb[i * 54];
+      r.d1 = g[0][0];
+      r.d2 = g[0][1];
+      r.U[0] = g[1][0], r.U[1] = g[1][1], r.U[2] = g[2][0];
+      r.GU[0][0] = g[2][1], r.GU[0][1] = g[3][0], r.GU[0][2] = g[3][1];
+      r.GU[1][0] = g[4][0], r.GU[1][1] = g[4][1], r.GU[1][2] = g[5][0];
+      r.GU[2][0] = g[5][1], r.GU[2][1] = g[6][0], r.GU[2][2] = g[6][1];
+      r.GP[0] = g[7][0], r.GP[1] = g[7][1], r.GP[2] = g[8][0];
+      r.UT[0] = g[8][1], r.UT[1] = g[9][0], r.UT[2] = g[9][1];
       return;
     }
+#endif
   // per-q tables (operator_ns.h:120-132)
   const int64_t tq = qindex<dim, n>(cell, p, a.n_cells);
 #pragma unroll
@@ -308,12 +361,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
   const int64_t brick = a.brick_begin + blockIdx.x;
   if (brick >= a.brick_end)
     return;
-#ifdef GLS_BLIMIT
-  if (blockIdx.x >= GLS_BLIMIT) // diagnostic: time a partial grid
-    return;
-#endif
   const int t   = threadIdx.x;
-  const int cpb = a.bx * a.by * a.bz;
   if (t < n * n)
     {
       sS[t / n][t % n] = a.sh.S[t / n][t % n];
@@ -347,7 +395,10 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
       pk[it]      = i < L ? bn[i] : 0u;
       tg[it]      = i < L ? bt[i] : 0u;
     }
-  const bool general = a.brick_geo[brick] != 0;
+  const uint32_t binfo   = a.brick_geo[brick];
+  const bool     general = (binfo & 1u) != 0;
+  const int      ncell   = (int)(binfo >> 8);
+  const int64_t  cell0   = a.brick_cell0[brick];
 
   // ---- stage the brick's src values once per node (read_dof_values:
   // homogeneous constraints read as 0; the residual reads plain values).
@@ -359,15 +410,15 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
   for (int it = 0; it < NI; ++it)
     {
       const int i = t + it * BLOCK;
-      if (GLS_BABL & 16)
+      if (i < L && (pk[it] & NODE_MASK) != UNUSED_NODE)
+        load_node<T, nc>(a.src, pk[it] & NODE_MASK, u[it]);
+      else
 #pragma unroll
         for (int c = 0; c < nc; ++c)
-          u[it][c] = T(1e-3) * (i + c);
-      else if (i < L)
-        load_node<T, nc>(a.src, pk[it] & NODE_MASK, u[it]);
+          u[it][c] = T(0);
     }
   LaneData<dim, T, MODE> cur;
-  load_lane<dim, k, T, MODE>(a, brick, general, wave * CPW + slot, in_wave, p, pa, cur);
+  load_lane<dim, k, T, MODE>(a, cell0, ncell, general, wave * CPW + slot, in_wave, p, pa, cur);
 #pragma unroll
   for (int it = 0; it < NI; ++it)
     {
@@ -392,11 +443,10 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
     }
   __syncthreads();
 
-  for (int base = 0; base < ((GLS_BABL & 64) ? 0 : cpb); base += step)
+  for (int base = 0; base < ncell; base += step)
     {
 
       // ---- evaluate: x sweep straight from the src lattice, then y (, z)
-      if (!(GLS_BABL & 2))
       {
         const int lb = cur.li - pa[0];
         if (in_wave)
@@ -407,7 +457,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
       wave_sync();
       V *in = A, *out = B;
 #pragma unroll
-      for (int ax = 1; ax < dim && !(GLS_BABL & 2); ++ax)
+      for (int ax = 1; ax < dim; ++ax)
         {
           if (in_wave)
 #pragma unroll
@@ -431,16 +481,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
         }
       // left-over lanes stay out of the reads (they would only add bank
       // conflicts in their ds_read_b128 lane groups)
-      if (GLS_BABL & 2)
-#pragma unroll
-        for (int c = 0; c < nc; ++c)
-          {
-            val[c] = cur.U[0] * (c + 1);
-#pragma unroll
-            for (int ax = 0; ax < dim; ++ax)
-              gref[c][ax] = cur.inv[ax][ax] * c;
-          }
-      else if (in_wave)
+      if (in_wave)
 #pragma unroll
       for (int kp = 0; kp < NP; ++kp)
         {
@@ -478,27 +519,6 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
               gp[e] = s;
           }
       T vr[nc], gr[nc][dim];
-      if (GLS_BABL & 1)
-        {
-          T keep = cur.d1 + cur.d2;
-#pragma unroll
-          for (int d = 0; d < dim; ++d)
-            {
-              keep += cur.U[d] + cur.GP[d] + cur.UT[d];
-#pragma unroll
-              for (int e = 0; e < dim; ++e)
-                keep += cur.GU[d][e];
-            }
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-            {
-              vr[c] = val[c] * keep;
-#pragma unroll
-              for (int e = 0; e < dim; ++e)
-                gr[c][e] = c < dim ? gu[c][e] : gp[e];
-            }
-        }
-      else
         qpoint_physics<dim, T, MODE>(val, val[dim], gu, gp, cur.U, cur.GU, cur.GP, cur.UT,
                                      cur.oldg, cur.d1, cur.d2, a.nu, a.w0, a.theta, a.td,
                                      a.have_prev, a.have_old_grad, vr, gr);
@@ -524,20 +544,6 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
       // fused with the accumulation into the brick lattice
       V wv[NP];
       to_packs<V, T, nc, NP, W>(wq, wv);
-      if (GLS_BABL & 8)
-        {
-          if (cur.active)
-#pragma unroll
-            for (int c = 0; c < nc; ++c)
-              {
-                T v = wq[c];
-#pragma unroll
-                for (int i = 0; i < dim; ++i)
-                  v += ghat[i][c];
-                lds_add(s_acc + c * LP + cur.li, v);
-              }
-          continue;
-        }
 #pragma unroll
       for (int ax0 = 0; ax0 < dim; ax0 += 2)
         {
@@ -578,10 +584,13 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
         for (int kp = 0; kp < NP; ++kp)
           A[kp * BL::KS + q] = wv[kp];
       // the next round's geometry and tables: issued here (few registers
-      // live), in flight during the S^T sweeps and the next evaluate
-      if (base + step < cpb)
-        load_lane<dim, k, T, MODE>(a, brick, general, base + step + wave * CPW + slot, in_wave,
-                                   p, pa, cur);
+      // live), in flight during the S^T sweeps and the next evaluate (this
+      // round's lattice position is kept: the prefetch overwrites cur)
+      const int  li_now     = cur.li;
+      const bool active_now = cur.active;
+      if (base + step < ncell)
+        load_lane<dim, k, T, MODE>(a, cell0, ncell, general, base + step + wave * CPW + slot,
+                                   in_wave, p, pa, cur);
       wave_sync();
       in  = A;
       out = B;
@@ -598,15 +607,17 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
           in     = out;
           out    = tmp;
         }
-      if (cur.active)
+      T cx[n];
+      coefs<n, true>(sS, pa[0], cx);
+      if (active_now)
 #pragma unroll
         for (int kp = 0; kp < NP; ++kp)
           {
-            const V r = contract_v<n, true>(in + kp * BL::KS, sS, pa[0], q - pa[0], 1);
+            const V r = contract_c<n>(in + kp * BL::KS, cx, q - pa[0], 1);
 #pragma unroll
             for (int w = 0; w < W; ++w)
               if (kp * W + w < nc)
-                lds_add(s_acc + (kp * W + w) * LP + cur.li, r[w]);
+                lds_add(s_acc + (kp * W + w) * LP + li_now, r[w]);
           }
       wave_sync();
     }
@@ -614,7 +625,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
 
   // ---- write out: exclusive nodes -> dst, boundary nodes -> partials
 #pragma unroll
-  for (int it = 0; it < ((GLS_BABL & 32) ? 0 : NI); ++it)
+  for (int it = 0; it < NI; ++it)
     {
       const int i = t + it * BLOCK;
       if (i >= L)
@@ -622,6 +633,8 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
       const int      iz = i / Lxy, iy = (i - iz * Lxy) / a.Lx;
       const int      ip = (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
       const uint32_t tgt = tg[it];
+      if (tgt == UNUSED_NODE)
+        continue;
       if (tgt & SHARED_BIT)
         {
           T r[nc];

@@ -151,14 +151,34 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
   if (L > lmax || lmax > 729 || (dim == 3 && (bx > 4 || by > 4 || bz > 1)) ||
       (dim == 2 && (bx > 8 || by > 8)))
     return; // lattice does not fit the brick kernel's LDS: per-cell path
-  const int64_t nb = d->n_cells / cpb;
-  const int     nq = op->nq;
+  const int64_t nb_full = d->n_cells / cpb;
+  const int     nq      = op->nq;
+  // Work units: full bricks in mesh order, then the last n_split bricks
+  // split into halves along y (bx x by/2 cells, the lattice's upper rows
+  // unused).  Workgroups are dispatched in unit order, so the smaller units
+  // fill the last dispatch wave and shorten the tail (LPT order).
+  int64_t n_split = 0;
+  if (const char *e = getenv("GLS_BRICK_SPLIT"))
+    n_split = std::atoll(e);
+  if (by % 2 != 0)
+    n_split = 0;
+  n_split = std::max<int64_t>(0, std::min(n_split, nb_full));
+  const int64_t nb = nb_full + n_split;
+  std::vector<uint32_t> bcell0((size_t)nb), bncell((size_t)nb);
+  for (int64_t b = 0; b < nb_full - n_split; ++b)
+    bcell0[b] = (uint32_t)(b * cpb), bncell[b] = (uint32_t)cpb;
+  for (int64_t h = 0; h < 2 * n_split; ++h)
+    {
+      const int64_t b = nb_full - n_split + h;
+      bcell0[b] = (uint32_t)((nb_full - n_split + h / 2) * cpb + (h % 2) * (cpb / 2));
+      bncell[b] = (uint32_t)(cpb / 2);
+    }
   std::vector<uint32_t> bnodes((size_t)nb * L, UINT32_MAX);
   for (int64_t b = 0; b < nb; ++b)
-    for (int64_t lc = 0; lc < cpb; ++lc)
+    for (int64_t lc = 0; lc < (int64_t)bncell[b]; ++lc)
       {
         const int     cx = (int)(lc % bx), cy = (int)((lc / bx) % by), cz = (int)(lc / (bx * by));
-        const int64_t cell = b * cpb + lc;
+        const int64_t cell = bcell0[b] + lc;
         for (int p = 0; p < nq; ++p)
           {
             const int i = p % n, j = (p / n) % n, l = dim == 3 ? p / (n * n) : 0;
@@ -178,6 +198,8 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
     for (int i = 0; i < L; ++i)
       {
         const uint32_t node = bnodes[(size_t)b * L + i];
+        if (node == UINT32_MAX)
+          continue;
         if (last[node] != (uint32_t)b)
           {
             last[node] = (uint32_t)b;
@@ -196,7 +218,8 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
       const bool owned  = node < d->n_owned_nodes;
       const bool shared = mult[node] > 1                 // brick boundary
                           || (!owned && mult[node] > 0)  // ghost partial sums
-                          || (owned && mult[node] == 0); // untouched owned row
+                          || (owned && mult[node] == 0)  // untouched owned row
+                          || (d->node_cmask[node] & 0xF); // identity / zero rows
       if (shared)
         {
           shared_index[node] = (int64_t)shared_nodes.size();
@@ -216,7 +239,12 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
       for (int i = 0; i < L; ++i)
         {
           const uint32_t node = bnodes[(size_t)b * L + i];
-          const int64_t  s    = shared_index[node];
+          if (node == UINT32_MAX) // unused lattice node of a split brick
+            {
+              target[(size_t)b * L + i] = UNUSED_NODE;
+              continue;
+            }
+          const int64_t s = shared_index[node];
           if (s < 0)
             target[(size_t)b * L + i] = node;
           else
@@ -226,7 +254,7 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
   const uint32_t slot = (uint32_t)n_slot_total;
   // packed node | cmask for the gather and the reduction
   for (auto &v : bnodes)
-    v |= (uint32_t)(d->node_cmask[v] & 0xF) << 28;
+    v = v == UINT32_MAX ? UNUSED_NODE : v | (uint32_t)(d->node_cmask[v] & 0xF) << 28;
   for (auto &v : shared_nodes)
     v |= (uint32_t)(d->node_cmask[v] & 0xF) << 28;
 
@@ -236,6 +264,9 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
   op->n_bricks = nb;
   op->n_slots  = slot;
   op->n_shared = (int64_t)shared_nodes.size();
+  op->brick_cell0 = bcell0;
+  op->brick_ncell  = bncell;
+  upload((void **)&op->d_brick_cell0, bcell0);
   upload((void **)&op->d_brick_nodes, bnodes);
   upload((void **)&op->d_brick_target, target);
   upload((void **)&op->d_shared_nodes, shared_nodes);
@@ -388,6 +419,24 @@ struct Impl
     HIP_THROW(hipGetLastError());
   }
 
+#ifndef GLS_PERSISTENT
+#define GLS_PERSISTENT 0
+#endif
+  // persistent brick kernel: one workgroup per resident slot (occupancy x
+  // CUs of the current device), each walking bricks g, g + grid, ...
+  template <typename K, typename Args>
+  static void
+  launch_persistent(K kernel, int64_t n_bricks, size_t lds, hipStream_t s, const Args &a)
+  {
+    int dev = 0, n_cu = 0, per_cu = 0;
+    HIP_THROW(hipGetDevice(&dev));
+    HIP_THROW(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_THROW(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, BLOCK, lds));
+    const int64_t slots = (int64_t)std::max(1, per_cu) * std::max(1, n_cu);
+    const int64_t g     = GLS_PERSISTENT ? std::max<int64_t>(1, std::min(n_bricks, slots)) : n_bricks;
+    hipLaunchKernelGGL(kernel, dim3((unsigned)g), dim3(BLOCK), lds, s, a);
+  }
+
   // brick kernel + shared-node reduction: dst fully (over)written
   static void
   brick(const glsOp_ *op, int mode, void *dst, const void *src, hipStream_t s)
@@ -398,6 +447,7 @@ struct Impl
         a.brick_nodes   = op->d_brick_nodes;
         a.brick_target  = op->d_brick_target;
         a.brick_geo     = op->d_brick_geo;
+        a.brick_cell0   = op->d_brick_cell0;
         a.geo_cart      = (const T *)op->d_bgeo_cart; // cell-indexed
         a.geo_gen       = (const T *)op->d_bgeo_gen;  // cell-indexed
         a.tab           = (const T *)op->d_tab;
@@ -429,14 +479,13 @@ struct Impl
         a.have_prev     = op->have_prev ? 1 : 0;
         a.have_old_grad = (op->have_old_grad && op->prm.theta != 1.0) ? 1 : 0;
         a.sh            = make_shape<T, n>(op->basis);
-        const dim3   grid((unsigned)op->n_bricks);
         const size_t lds = BrickLDS<dim, k, T>::bytes(a.LP);
         if (mode == MODE_NEWTON)
-          hipLaunchKernelGGL((k_brick<dim, k, T, MODE_NEWTON>), grid, dim3(BLOCK), lds, s, a);
+          launch_persistent(k_brick<dim, k, T, MODE_NEWTON>, op->n_bricks, lds, s, a);
         else if (mode == MODE_FIXED)
-          hipLaunchKernelGGL((k_brick<dim, k, T, MODE_FIXED>), grid, dim3(BLOCK), lds, s, a);
+          launch_persistent(k_brick<dim, k, T, MODE_FIXED>, op->n_bricks, lds, s, a);
         else
-          hipLaunchKernelGGL((k_brick<dim, k, T, MODE_RESIDUAL>), grid, dim3(BLOCK), lds, s, a);
+          launch_persistent(k_brick<dim, k, T, MODE_RESIDUAL>, op->n_bricks, lds, s, a);
         HIP_THROW(hipGetLastError());
         if (op->n_shared > 0)
           {
@@ -737,18 +786,23 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
   std::vector<uint32_t> bgeo;
   if (op->use_brick)
     {
-      const int64_t C   = d->n_cells;
-      const int64_t cpb = C / op->n_bricks;
+      const int64_t C = d->n_cells;
       bcart.assign((size_t)ncf * C, 0.0);
       bgen.assign((size_t)ngf * C * nq, 0.0);
       bgeo.assign((size_t)op->n_bricks, 0u);
+      std::vector<int64_t> brick_of((size_t)C, -1);
+      for (int64_t b = 0; b < op->n_bricks; ++b)
+        for (uint32_t lc = 0; lc < op->brick_ncell[b]; ++lc)
+          brick_of[op->brick_cell0[b] + lc] = b;
       for (int64_t c = 0; c < C; ++c)
         if (cell_geo[c] & GEO_GENERAL)
-          bgeo[c / cpb] = 1u;
+          bgeo[brick_of[c]] |= 1u;
+      for (int64_t b = 0; b < op->n_bricks; ++b)
+        bgeo[b] |= op->brick_ncell[b] << 8;
       for (int64_t c = 0; c < C; ++c)
         {
           const uint32_t cg = cell_geo[c];
-          if (!bgeo[c / cpb])
+          if (!(bgeo[brick_of[c]] & 1u))
             {
               for (int f = 0; f < ncf; ++f)
                 bcart[(size_t)f * C + c] = cart_rows[(size_t)cg * ncf + f];
@@ -826,7 +880,7 @@ gls_op_destroy(glsOp op)
                   op->d_hmin,         op->d_tmp,          op->d_cbits,        op->d_brick_nodes,
                   op->d_brick_target, op->d_shared_nodes, op->d_shared_off,
                   op->d_partial,      op->d_bgeo_cart,    op->d_bgeo_gen,
-                  op->d_brick_geo};
+                  op->d_brick_geo,    op->d_brick_cell0};
   for (void *b : bufs)
     if (b)
       (void)hipFree(b);
@@ -1150,6 +1204,23 @@ gls_op_vmult_bytes(glsOp op)
   if (op->prm.flags & GLS_CELL_WISE_STAB)
     b += s * 2.0 * C;
   return b;
+}
+
+// diagnostic timeline builds only (GLS_STAMPS): copy g_stamps to the host
+int
+gls_debug_stamps(void *host, size_t bytes)
+{
+  GLS_TRY
+#ifdef GLS_STAMPS
+  const size_t nb = bytes < sizeof(g_stamps) ? bytes : sizeof(g_stamps);
+  HIP_THROW(hipDeviceSynchronize());
+  HIP_THROW(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), nb, 0, hipMemcpyDeviceToHost));
+#else
+  (void)host;
+  (void)bytes;
+  throw std::runtime_error("gls_debug_stamps: not a GLS_STAMPS build");
+#endif
+  GLS_CATCH
 }
 
 } // extern "C"

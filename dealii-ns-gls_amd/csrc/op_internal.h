@@ -48,7 +48,9 @@ struct glsOp_
   void     *d_partial      = nullptr;
   void     *d_bgeo_cart    = nullptr; // brick path: cell-indexed geometry
   void     *d_bgeo_gen     = nullptr;
-  uint32_t *d_brick_geo    = nullptr; // per brick: curved (1) or Cartesian (0)
+  uint32_t *d_brick_geo    = nullptr; // per brick: curved (bit 0) | cells << 8
+  uint32_t *d_brick_cell0  = nullptr; // per brick: first cell
+  std::vector<uint32_t> brick_cell0, brick_ncell;
 
   size_t
   tsize() const

@@ -33,9 +33,9 @@ class Case:
         self._om = om
         return o
 
-    def gpu(self, precision="f64"):
+    def gpu(self, precision="f64", brick=None):
         import glsamd
-        op = glsamd.NavierStokesOperator(self.mesh, self.cmask, precision)
+        op = glsamd.NavierStokesOperator(self.mesh, self.cmask, precision, brick=brick)
         op.set_parameters(**self.params)
         op.set_linearization_point(self.u_star)
         if self.params["order"] > 0:

@@ -95,3 +95,39 @@ def test_residual_3d(prec):
     op.evaluate_residual(res, op._dev(case.u_star))
     torch.cuda.synchronize()
     assert rel_err(_to_np(res), ref) < TOL[prec]
+
+
+# The headline workload (Re3900 r2, BASELINE.json configs[3]): 4x4x1 bricks run
+# in two rounds of 8 cells per workgroup and the persistent grid walks several
+# bricks per workgroup, which the r0/r1 decks above (one round, one brick per
+# workgroup) do not reach.  Smaller bricks change the round count and the
+# shared-node structure; all must give the same operator.
+@pytest.fixture(scope="module")
+def re3900_r2():
+    case = deck_case("input_hoffmann_3D_Re3900.json", 2)
+    o = case.oracle()
+    return case, o.vmult(case.src), o.evaluate_residual(case.u_star)
+
+
+@pytest.mark.parametrize("brick", [None, (4, 2, 1), (4, 1, 1)])
+def test_vmult_headline_r2(re3900_r2, brick):
+    import torch
+    case, ref, _ = re3900_r2
+    op = case.gpu("f64", brick=brick)
+    dst = op.initialize_dof_vector()
+    src = op._dev(case.src)
+    for _ in range(2):  # repeated applies overwrite dst completely
+        op.vmult(dst, src)
+    torch.cuda.synchronize()
+    assert rel_err(_to_np(dst), ref) < TOL["f64"]
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_residual_headline_r2(re3900_r2, prec):
+    import torch
+    case, _, ref = re3900_r2
+    op = case.gpu(prec)
+    res = op.initialize_dof_vector()
+    op.evaluate_residual(res, op._dev(case.u_star))
+    torch.cuda.synchronize()
+    assert rel_err(_to_np(res), ref) < TOL[prec]
