@@ -78,32 +78,6 @@ lds_add(T *p, T v)
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <typename T, int dim, int n>
-struct BrickArgs
-{
-  const uint32_t *brick_nodes;  // [n_bricks][L] node | cmask << 28
-  const uint32_t *brick_target; // [n_bricks][L] node, or SHARED_BIT | slot
-  const uint32_t *brick_geo; // per brick: bit 0 curved (per-q geometry for all its
-                             // cells) | number of cells << 8
-  const uint32_t *brick_cell0; // per brick: first cell
-  const T        *geo_cart;  // [dim+1][cell]               (cells of Cartesian bricks)
-  const T        *geo_gen;   // [1+dim^2][plane][cell][line] (cells of curved bricks)
-  const T        *tab;      // [field][plane][cell][line]
-  int64_t         n_cells;
-  const T        *cellwise;
-  const T        *old_grad;
-  T              *dst;
-  const T        *src;
-  T              *partial; // [slot][dim+1], slots of a node contiguous
-  int64_t         brick_begin, brick_end;
-  int             bx, by, bz;
-  int             L, Lx, Ly;
-  int             PLx, PLy, LP; // padded LDS lattice strides / size (>= L)
-  T               nu, w0, theta;
-  int             td, cw, have_prev, have_old_grad;
-  Shape<T, n>     sh;
-};
-
 // 16-byte LDS packs of solution components: the sum-factorisation sweeps
 // move (dim+1) components as ceil((dim+1)/W) ds_read_b128 / ds_write_b128
 // instead of one 8-byte access per component (and no ds_read2_b64, which
@@ -121,6 +95,34 @@ struct Pack<float>
 {
   typedef float V __attribute__((ext_vector_type(4)));
   static constexpr int W = 4;
+};
+
+template <typename T, int dim, int n>
+struct BrickArgs
+{
+  const uint32_t *brick_nodes;  // [n_bricks][L] node | cmask << 28
+  const uint32_t *brick_target; // [n_bricks][L] node, or SHARED_BIT | slot
+  const uint32_t *brick_geo; // per brick: bit 0 curved (per-q geometry for all its
+                             // cells) | number of cells << 8
+  const uint32_t *brick_cell0;  // per brick: first cell
+  const uint32_t *brick_chunk0; // per brick: first table chunk
+  const T        *geo_cart;  // [dim+1][cell]               (cells of Cartesian bricks)
+  const T        *geo_gen;   // [1+dim^2][plane][cell][line] (cells of curved bricks)
+  const typename Pack<T>::V *tab_v; // tables: 16-byte field groups, a chunk per
+                                    // wavefront round (group stride CPW * nq)
+  int64_t         n_cells;
+  const T        *cellwise;
+  const T        *old_grad;
+  T              *dst;
+  const T        *src;
+  T              *partial; // [slot][dim+1], slots of a node contiguous
+  int64_t         brick_begin, brick_end;
+  int             bx, by, bz;
+  int             L, Lx, Ly;
+  int             PLx, PLy, LP; // padded LDS lattice strides / size (>= L)
+  T               nu, w0, theta;
+  int             td, cw, have_prev, have_old_grad;
+  Shape<T, n>     sh;
 };
 
 // 1D coefficient row of a lane: M[pa][j] (TR false) or M[j][pa] (TR true),
@@ -212,17 +214,22 @@ struct LaneData
 // for once, at the q-point physics.
 template <int dim, int k, typename T, int MODE>
 __device__ __forceinline__ void
-load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int ncell, bool general, int lcell,
-          bool in_wave, int p, const int (&pa)[3], LaneData<dim, T, MODE> &r)
+load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int ncell,
+          bool general, int lcell, bool in_wave, int p, const int (&pa)[3],
+          LaneData<dim, T, MODE> &r)
 {
-  constexpr int n   = k + 1;
-  constexpr int nq  = ipow(n, dim);
-  constexpr bool R  = MODE == MODE_RESIDUAL;
-  using F           = Fields<dim>;
-  r.active          = in_wave && lcell < ncell;
-  const int cx      = r.active ? lcell % a.bx : 0;
-  const int cy      = r.active ? (lcell / a.bx) % a.by : 0;
-  const int cz      = r.active ? lcell / (a.bx * a.by) : 0;
+  constexpr int  n   = k + 1;
+  constexpr int  nq  = ipow(n, dim);
+  constexpr int  CPW = 64 / nq > 0 ? 64 / nq : 1;
+  constexpr bool R   = MODE == MODE_RESIDUAL;
+  constexpr int  W   = Pack<T>::W;
+  using V            = typename Pack<T>::V;
+  using F            = Fields<dim>;
+  constexpr int NG   = (F::N + W - 1) / W;
+  r.active           = in_wave && lcell < ncell;
+  const int cx       = r.active ? lcell % a.bx : 0;
+  const int cy       = r.active ? (lcell / a.bx) % a.by : 0;
+  const int cz       = r.active ? lcell / (a.bx * a.by) : 0;
   r.li = (cx * k + pa[0]) + a.PLx * ((cy * k + pa[1]) + a.PLy * (cz * k + pa[2]));
   const int64_t cell = cell0 + lcell;
   const int64_t nqc  = a.n_cells * nq;
@@ -264,48 +271,50 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int ncell, bool gene
         r.inv[i][i] = a.geo_cart[i * a.n_cells + cell];
       r.JxW = a.geo_cart[dim * a.n_cells + cell] * w;
     }
-#ifdef GLS_TABX
-  // timing-only ablation: per-wave-round contiguous 16-byte table loads
-  if constexpr (sizeof(T) == 8 && dim == 3)
-    {
-      typedef double D2 __attribute__((ext_vector_type(2)));
-      const D2 *tb = reinterpret_cast<const D2 *>(a.tab) + (cell / 2) * (10 * 54) +
-                     (lcell % 2) * 27 + p;
-      D2 g[10];
+  // per-q tables (operator_ns.h:120-132): the round's CPW cells form one
+  // chunk, each 16-byte field group of it one contiguous wave load; the
+  // groups a mode reads are fixed at compile time (fields a runtime flag
+  // switches off are loaded and ignored)
+  constexpr int GS = CPW * nq; // group stride in packs
+  const V *tv = a.tab_v + (chunk0 + lcell / CPW) * (NG * GS) + (lcell % CPW) * nq + p;
+  T        tf[NG * W];
 #pragma unroll
-      for (int i = 0; i < 10; ++i)
-        g[i] = tb[i * 54];
-      r.d1 = g[0][0];
-      r.d2 = g[0][1];
-      r.U[0] = g[1][0], r.U[1] = g[1][1], r.U[2] = g[2][0];
-      r.GU[0][0] = g[2][1], r.GU[0][1] = g[3][0], r.GU[0][2] = g[3][1];
-      r.GU[1][0] = g[4][0], r.GU[1][1] = g[4][1], r.GU[1][2] = g[5][0];
-      r.GU[2][0] = g[5][1], r.GU[2][1] = g[6][0], r.GU[2][2] = g[6][1];
-      r.GP[0] = g[7][0], r.GP[1] = g[7][1], r.GP[2] = g[8][0];
-      r.UT[0] = g[8][1], r.UT[1] = g[9][0], r.UT[2] = g[9][1];
-      return;
+  for (int g = 0; g < NG; ++g)
+    {
+      bool any = false;
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        {
+          const int  f   = g * W + w;
+          const bool d12 = f == F::D1 || f == F::D2;
+          const bool u   = f >= F::U && f < F::U + dim;
+          const bool ut  = f >= F::UT && f < F::N;
+          any = any || d12 || u || (MODE == MODE_NEWTON && f < F::N) || (R && ut);
+        }
+      V v = {};
+      if (any)
+        v = tv[g * GS];
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        tf[g * W + w] = v[w];
     }
-#endif
-  // per-q tables (operator_ns.h:120-132)
-  const int64_t tq = qindex<dim, n>(cell, p, a.n_cells);
 #pragma unroll
   for (int d = 0; d < dim; ++d)
     {
-      r.U[d] = a.tab[(F::U + d) * nqc + tq];
-      if (MODE == MODE_NEWTON)
-        {
+      r.U[d]  = tf[F::U + d];
+      r.GP[d] = tf[F::GP + d];
+      r.UT[d] = tf[F::UT + d];
 #pragma unroll
-          for (int e = 0; e < dim; ++e)
-            r.GU[d][e] = a.tab[(F::GU + d * dim + e) * nqc + tq];
-          r.GP[d] = a.tab[(F::GP + d) * nqc + tq];
-        }
-      if ((MODE == MODE_NEWTON && a.td) || (R && a.have_prev))
-        r.UT[d] = a.tab[(F::UT + d) * nqc + tq];
+      for (int e = 0; e < dim; ++e)
+        r.GU[d][e] = tf[F::GU + d * dim + e];
     }
   if (R && a.have_old_grad)
+    {
+      const int64_t tq = qindex<dim, n>(cell, p, a.n_cells);
 #pragma unroll
-    for (int i = 0; i < LaneData<dim, T, MODE>::NOLD; ++i)
-      r.oldg[i] = a.old_grad[i * nqc + tq];
+      for (int i = 0; i < LaneData<dim, T, MODE>::NOLD; ++i)
+        r.oldg[i] = a.old_grad[i * nqc + tq];
+    }
   if (a.cw)
     {
       r.d1 = a.cellwise[cell];
@@ -313,8 +322,8 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int ncell, bool gene
     }
   else
     {
-      r.d1 = a.tab[F::D1 * nqc + tq];
-      r.d2 = a.tab[F::D2 * nqc + tq];
+      r.d1 = tf[F::D1];
+      r.d2 = tf[F::D2];
     }
 }
 
@@ -399,6 +408,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
   const bool     general = (binfo & 1u) != 0;
   const int      ncell   = (int)(binfo >> 8);
   const int64_t  cell0   = a.brick_cell0[brick];
+  const int64_t  chunk0  = a.brick_chunk0[brick];
 
   // ---- stage the brick's src values once per node (read_dof_values:
   // homogeneous constraints read as 0; the residual reads plain values).
@@ -418,7 +428,8 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
           u[it][c] = T(0);
     }
   LaneData<dim, T, MODE> cur;
-  load_lane<dim, k, T, MODE>(a, cell0, ncell, general, wave * CPW + slot, in_wave, p, pa, cur);
+  load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, wave * CPW + slot, in_wave, p, pa,
+                             cur);
 #pragma unroll
   for (int it = 0; it < NI; ++it)
     {
@@ -589,7 +600,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
       const int  li_now     = cur.li;
       const bool active_now = cur.active;
       if (base + step < ncell)
-        load_lane<dim, k, T, MODE>(a, cell0, ncell, general, base + step + wave * CPW + slot,
+        load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, base + step + wave * CPW + slot,
                                    in_wave, p, pa, cur);
       wave_sync();
       in  = A;

@@ -275,6 +275,52 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
                       std::max<size_t>(1, (size_t)slot * (dim + 1) * op->tsize())));
 }
 
+// host twin of gls::tab_index (kernels.h)
+size_t
+host_tab_index(const glsOp_ *op, int64_t c, int q, int f)
+{
+  const int W = (int)(16 / op->tsize());
+  return (size_t)(op->h_tab_cbase[c] + (int64_t)(f / W) * op->tab_gs + (int64_t)q * W + f % W);
+}
+
+// Per-q table layout (kernels.h tab_index): cells are grouped into chunks of
+// CPW = 64 / nq cells — with bricks, the cells one wavefront of k_brick runs
+// in one round — and a chunk stores its fields in 16-byte groups, lanes
+// (cell slot, q) contiguous inside a group.
+void
+build_table_layout(glsOp_ *op)
+{
+  const int     W   = (int)(16 / op->tsize());
+  const int     NG  = (op->nf + W - 1) / W;
+  const int     nq  = op->nq;
+  const int     CPW = std::max(1, 64 / nq);
+  const int64_t gs  = (int64_t)CPW * nq * W;
+  op->h_tab_cbase.assign((size_t)op->n_cells, 0);
+  int64_t n_chunks = 0;
+  if (op->use_brick)
+    {
+      std::vector<uint32_t> chunk0((size_t)op->n_bricks);
+      for (int64_t b = 0; b < op->n_bricks; ++b)
+        {
+          chunk0[b] = (uint32_t)n_chunks;
+          for (uint32_t lc = 0; lc < op->brick_ncell[b]; ++lc)
+            op->h_tab_cbase[op->brick_cell0[b] + lc] =
+              (n_chunks + lc / CPW) * NG * gs + (int64_t)(lc % CPW) * nq * W;
+          n_chunks += (op->brick_ncell[b] + CPW - 1) / CPW;
+        }
+      upload((void **)&op->d_brick_chunk0, chunk0);
+    }
+  else
+    {
+      for (int64_t c = 0; c < op->n_cells; ++c)
+        op->h_tab_cbase[c] = (c / CPW) * NG * gs + (c % CPW) * nq * W;
+      n_chunks = (op->n_cells + CPW - 1) / CPW;
+    }
+  op->tab_gs    = gs;
+  op->tab_elems = n_chunks * NG * gs;
+  upload((void **)&op->d_tab_cbase, op->h_tab_cbase);
+}
+
 // geometry of one cell at all q: J[d][a] = dx_d / dxi_a by sum factorisation
 void
 cell_jacobians(int dim, const Basis1D &b, const double *X /* [nloc][dim] */,
@@ -367,7 +413,9 @@ struct Impl
     a.geo_gen       = (const T *)op->d_geo_gen;
     a.gen_stride    = op->n_gen * nq;
     a.tab           = (const T *)op->d_tab;
-    a.tab_stride    = op->n_cells * nq;
+    a.tab_cbase     = op->d_tab_cbase;
+    a.tab_gs        = op->tab_gs;
+    a.old_stride    = op->n_cells * nq;
     a.cellwise      = (const T *)op->d_cellwise;
     a.n_cells       = op->n_cells;
     a.old_grad      = (const T *)op->d_old_grad;
@@ -448,9 +496,10 @@ struct Impl
         a.brick_target  = op->d_brick_target;
         a.brick_geo     = op->d_brick_geo;
         a.brick_cell0   = op->d_brick_cell0;
+        a.brick_chunk0  = op->d_brick_chunk0;
+        a.tab_v         = (const typename Pack<T>::V *)op->d_tab;
         a.geo_cart      = (const T *)op->d_bgeo_cart; // cell-indexed
         a.geo_gen       = (const T *)op->d_bgeo_gen;  // cell-indexed
-        a.tab           = (const T *)op->d_tab;
         a.n_cells       = op->n_cells;
         a.cellwise      = (const T *)op->d_cellwise;
         a.old_grad      = (const T *)op->d_old_grad;
@@ -516,7 +565,9 @@ struct Impl
     a.geo_gen    = (const T *)op->d_geo_gen;
     a.gen_stride = op->n_gen * nq;
     a.tab        = (T *)op->d_tab;
-    a.tab_stride = op->n_cells * nq;
+    a.tab_cbase  = op->d_tab_cbase;
+    a.tab_gs     = op->tab_gs;
+    a.old_stride = op->n_cells * nq;
     a.cellwise   = (T *)op->d_cellwise;
     a.n_cells    = op->n_cells;
     a.old_grad   = (T *)op->d_old_grad;
@@ -858,8 +909,9 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
       upload(&op->d_hmin, convert<float>(hmin));
     }
   const size_t ts = op->tsize();
-  HIP_THROW(hipMalloc(&op->d_tab, std::max<size_t>(1, (size_t)op->nf * d->n_cells * nq * ts)));
-  HIP_THROW(hipMemset(op->d_tab, 0, std::max<size_t>(1, (size_t)op->nf * d->n_cells * nq * ts)));
+  build_table_layout(op);
+  HIP_THROW(hipMalloc(&op->d_tab, std::max<size_t>(1, (size_t)op->tab_elems * ts)));
+  HIP_THROW(hipMemset(op->d_tab, 0, std::max<size_t>(1, (size_t)op->tab_elems * ts)));
   HIP_THROW(hipMalloc(&op->d_cellwise, std::max<size_t>(1, 2 * (size_t)d->n_cells * ts)));
   HIP_THROW(hipMemset(op->d_cellwise, 0, std::max<size_t>(1, 2 * (size_t)d->n_cells * ts)));
   HIP_THROW(hipMalloc(&op->d_tmp, std::max<size_t>(1, (size_t)op->n_dofs * ts)));
@@ -880,7 +932,7 @@ gls_op_destroy(glsOp op)
                   op->d_hmin,         op->d_tmp,          op->d_cbits,        op->d_brick_nodes,
                   op->d_brick_target, op->d_shared_nodes, op->d_shared_off,
                   op->d_partial,      op->d_bgeo_cart,    op->d_bgeo_gen,
-                  op->d_brick_geo,    op->d_brick_cell0};
+                  op->d_brick_geo,    op->d_brick_cell0,  op->d_brick_chunk0, op->d_tab_cbase};
   for (void *b : bufs)
     if (b)
       (void)hipFree(b);
@@ -1099,13 +1151,11 @@ gls_op_upload_tables(glsOp op, const double *tables, const double *cellwise)
   GLS_TRY
   if (!op || !tables)
     throw std::runtime_error("gls_op_upload_tables: null argument");
-  const int64_t       m = op->n_cells * op->nq;
-  std::vector<double> soa((size_t)op->nf * m);
+  std::vector<double> soa((size_t)op->tab_elems, 0.0);
   for (int64_t c = 0; c < op->n_cells; ++c)
     for (int q = 0; q < op->nq; ++q)
       for (int f = 0; f < op->nf; ++f)
-        soa[(size_t)f * m + host_qindex(op->dim, op->degree + 1, c, q, op->n_cells)] =
-          tables[((size_t)c * op->nq + q) * op->nf + f];
+        soa[host_tab_index(op, c, q, f)] = tables[((size_t)c * op->nq + q) * op->nf + f];
   std::vector<double> cw((size_t)2 * op->n_cells, 0.0);
   if (cellwise)
     for (int64_t c = 0; c < op->n_cells; ++c)
@@ -1137,8 +1187,7 @@ gls_op_download_tables(glsOp op, double *tables, double *cellwise)
   if (!op)
     throw std::runtime_error("gls_op_download_tables: null argument");
   HIP_THROW(hipDeviceSynchronize());
-  const int64_t       m = op->n_cells * op->nq;
-  std::vector<double> soa((size_t)op->nf * m), cw((size_t)2 * op->n_cells);
+  std::vector<double> soa((size_t)op->tab_elems), cw((size_t)2 * op->n_cells);
   if (op->prec == GLS_F64)
     {
       HIP_THROW(hipMemcpy(soa.data(), op->d_tab, soa.size() * 8, hipMemcpyDeviceToHost));
@@ -1156,8 +1205,7 @@ gls_op_download_tables(glsOp op, double *tables, double *cellwise)
     for (int64_t c = 0; c < op->n_cells; ++c)
       for (int q = 0; q < op->nq; ++q)
         for (int f = 0; f < op->nf; ++f)
-          tables[((size_t)c * op->nq + q) * op->nf + f] =
-            soa[(size_t)f * m + host_qindex(op->dim, op->degree + 1, c, q, op->n_cells)];
+          tables[((size_t)c * op->nq + q) * op->nf + f] = soa[host_tab_index(op, c, q, f)];
   if (cellwise)
     for (int64_t c = 0; c < op->n_cells; ++c)
       {

@@ -63,6 +63,21 @@ struct Fields
                        UT = 2 + 2 * dim + dim * dim, N = 2 + 3 * dim + dim * dim;
 };
 
+// Per-q tables (set_linearization_point / set_previous_solution outputs,
+// operator_ns.h:120-132) are stored in 16-byte field groups of W = 16 /
+// sizeof(T) fields: element (cell, q, field f) at
+//   cbase[cell] + (f / W) * gs + q * W + f % W.
+// With the brick kernel, a cell's cbase places the cells of one wavefront
+// round (csrc/brick.h: CPW cells) in one chunk, so every table load of the
+// round is one contiguous 16-byte-per-lane wave load.
+template <typename T>
+__device__ __forceinline__ int64_t
+tab_index(const int64_t *cbase, int64_t gs, int64_t cell, int p, int f)
+{
+  constexpr int W = 16 / sizeof(T);
+  return cbase[cell] + (int64_t)(f / W) * gs + (int64_t)p * W + (f % W);
+}
+
 template <typename T, int n>
 struct Shape
 {
@@ -80,8 +95,10 @@ struct ApplyArgs
   int64_t         n_cart;
   const T        *geo_gen;  // [1 + dim*dim][n_gen * nq]: JxW, invJ[a][e]
   int64_t         gen_stride;
-  const T        *tab;      // [Fields::N][n_cells * nq]
-  int64_t         tab_stride;
+  const T        *tab;      // 16-byte field groups (tab_index)
+  const int64_t  *tab_cbase;
+  int64_t         tab_gs;
+  int64_t         old_stride; // old_grad: [dim*dim + dim][plane][cell][line]
   const T        *cellwise; // [2][n_cells]
   int64_t         n_cells;
   const T        *old_grad; // [dim*dim + dim][n_cells * nq]
@@ -430,7 +447,10 @@ __global__ void __launch_bounds__(BLOCK)
 
   // ---- prefetch geometry and per-q tables (consumed after evaluate)
   const int64_t   q  = qindex<dim, n>(cell, p, a.n_cells);
-  const int64_t   ts = a.tab_stride;
+  const int64_t   ts = a.old_stride;
+  const int64_t   tb = active ? a.tab_cbase[cell] + (int64_t)p * (16 / sizeof(T)) : 0;
+  constexpr int   TW = 16 / sizeof(T);
+  auto            TI = [&](int f) { return tb + (int64_t)(f / TW) * a.tab_gs + f % TW; };
   QGeo<dim, n, T> g;
   T               U[dim], GU[dim][dim], GP[dim], UT[dim], oldg[dim * dim + dim], d1 = 0, d2 = 0;
   g.JxW = 0;
@@ -483,16 +503,16 @@ __global__ void __launch_bounds__(BLOCK)
 #pragma unroll
       for (int d = 0; d < dim; ++d)
         {
-          U[d] = a.tab[(F::U + d) * ts + q];
+          U[d] = a.tab[TI(F::U + d)];
           if (MODE == MODE_NEWTON)
             {
 #pragma unroll
               for (int e = 0; e < dim; ++e)
-                GU[d][e] = a.tab[(F::GU + d * dim + e) * ts + q];
-              GP[d] = a.tab[(F::GP + d) * ts + q];
+                GU[d][e] = a.tab[TI(F::GU + d * dim + e)];
+              GP[d] = a.tab[TI(F::GP + d)];
             }
           if ((MODE == MODE_NEWTON && a.td) || (MODE == MODE_RESIDUAL && a.have_prev))
-            UT[d] = a.tab[(F::UT + d) * ts + q];
+            UT[d] = a.tab[TI(F::UT + d)];
         }
       if (MODE == MODE_RESIDUAL && a.have_old_grad)
 #pragma unroll
@@ -505,8 +525,8 @@ __global__ void __launch_bounds__(BLOCK)
         }
       else
         {
-          d1 = a.tab[F::D1 * ts + q];
-          d2 = a.tab[F::D2 * ts + q];
+          d1 = a.tab[TI(F::D1)];
+          d2 = a.tab[TI(F::D2)];
         }
       if (!(cg & GEO_GENERAL))
         {
@@ -673,7 +693,9 @@ struct ProducerArgs
   const T        *geo_gen;
   int64_t         gen_stride;
   T              *tab;
-  int64_t         tab_stride;
+  const int64_t  *tab_cbase;
+  int64_t         tab_gs;
+  int64_t         old_stride;
   T              *cellwise;
   int64_t         n_cells;
   T              *old_grad;
@@ -755,7 +777,10 @@ __global__ void __launch_bounds__(BLOCK)
           gref[c][ax] = contract<n, false>(in + c * nq, sD, pa[ax], p - pa[ax] * st[ax], st[ax]);
       }
   const int64_t q  = qindex<dim, n>(cell, p, a.n_cells);
-  const int64_t ts = a.tab_stride;
+  const int64_t ts = a.old_stride;
+  constexpr int TW = 16 / sizeof(T);
+  const int64_t tb = active ? a.tab_cbase[cell] + (int64_t)p * TW : 0;
+  auto          TI = [&](int f) { return tb + (int64_t)(f / TW) * a.tab_gs + f % TW; };
   T             unorm = 0;
   if (active)
     {
@@ -764,7 +789,7 @@ __global__ void __launch_bounds__(BLOCK)
           // set_previous_solution: u_time_derivative_old (:262-271)
 #pragma unroll
           for (int d = 0; d < dim; ++d)
-            a.tab[(F::UT + d) * ts + q] = val[d];
+            a.tab[TI(F::UT + d)] = val[d];
         }
       else
         {
@@ -806,11 +831,11 @@ __global__ void __launch_bounds__(BLOCK)
 #pragma unroll
               for (int d = 0; d < dim; ++d)
                 {
-                  a.tab[(F::U + d) * ts + q] = val[d];
+                  a.tab[TI(F::U + d)] = val[d];
 #pragma unroll
                   for (int e = 0; e < dim; ++e)
-                    a.tab[(F::GU + d * dim + e) * ts + q] = gr[d][e];
-                  a.tab[(F::GP + d) * ts + q] = gr[dim][d];
+                    a.tab[TI(F::GU + d * dim + e)] = gr[d][e];
+                  a.tab[TI(F::GP + d)] = gr[dim][d];
                   u2 += val[d] * val[d];
                 }
               unorm = sqrt(u2);
@@ -818,9 +843,9 @@ __global__ void __launch_bounds__(BLOCK)
               const T h      = a.h_q[cell];
               const T umag2  = T(1e-12) + u2;
               const T fac    = T(4) * a.nu / (h * h);
-              a.tab[F::D1 * ts + q] =
+              a.tab[TI(F::D1)] =
                 T(1) / sqrt(a.stau * a.stau + T(4) * umag2 / h / h + T(9) * fac * fac);
-              a.tab[F::D2 * ts + q] = sqrt(umag2) * h * T(0.5);
+              a.tab[TI(F::D2)] = sqrt(umag2) * h * T(0.5);
             }
         }
     }

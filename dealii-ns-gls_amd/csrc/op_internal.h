@@ -50,6 +50,13 @@ struct glsOp_
   void     *d_bgeo_gen     = nullptr;
   uint32_t *d_brick_geo    = nullptr; // per brick: curved (bit 0) | cells << 8
   uint32_t *d_brick_cell0  = nullptr; // per brick: first cell
+  uint32_t *d_brick_chunk0 = nullptr; // per brick: first table chunk
+
+  // per-q table layout (kernels.h tab_index): 16-byte field groups, one
+  // chunk per wavefront round of the brick kernel
+  std::vector<int64_t> h_tab_cbase; // [n_cells]
+  int64_t  *d_tab_cbase = nullptr;
+  int64_t   tab_gs = 0, tab_elems = 0;
   std::vector<uint32_t> brick_cell0, brick_ncell;
 
   size_t
