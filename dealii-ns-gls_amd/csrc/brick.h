@@ -125,17 +125,43 @@ struct BrickArgs
   Shape<T, n>     sh;
 };
 
-// 1D coefficient row of a lane: M[pa][j] (TR false) or M[j][pa] (TR true),
-// read once into registers and applied to every component pack (the LDS
-// stores of a sweep may alias the tables, so reading M inside the pack loop
-// would re-read it after every store)
-template <int n, bool TR, typename T>
-__device__ __forceinline__ void
-coefs(const T (*M)[n], int pa, T (&c)[n])
+// 1D coefficient tables in LDS: S, S^T, Dq, Dq^T, each row padded to whole
+// 16-byte packs (RP values) so that a lane's row M[pa][*] (or M[*][pa]) is
+// one ds_read_b128 (+ one ds_read_b64 for Q2 FP64) instead of
+// ds_read2_b64 + ds_read_b64 on 24-byte rows
+template <typename T, int n>
+struct CoefRow
 {
+  static constexpr int W  = 16 / (int)sizeof(T);
+  static constexpr int RP = (n + W - 1) / W * W; // padded row length
+};
+enum
+{
+  TAB_S = 0,
+  TAB_ST,
+  TAB_D,
+  TAB_DT
+};
+
+// coefficient row of a lane, read once into registers and applied to every
+// component pack (the LDS stores of a sweep may alias the tables, so
+// reading M inside the pack loop would re-read it after every store)
+template <int n, typename T>
+__device__ __forceinline__ void
+coefs(const T *tab, int pa, T (&c)[n])
+{
+  using CR         = CoefRow<T, n>;
+  using V          = typename Pack<T>::V;
+  const V *row     = reinterpret_cast<const V *>(tab + pa * CR::RP);
 #pragma unroll
-  for (int j = 0; j < n; ++j)
-    c[j] = TR ? M[j][pa] : M[pa][j];
+  for (int g = 0; g < CR::RP / CR::W; ++g)
+    {
+      const V v = row[g];
+#pragma unroll
+      for (int w = 0; w < CR::W; ++w)
+        if (g * CR::W + w < n)
+          c[g * CR::W + w] = v[w];
+    }
 }
 
 template <int n, typename T, typename V>
@@ -149,12 +175,12 @@ contract_c(const V *in, const T (&c)[n], int base, int s)
   return acc;
 }
 
-template <int n, bool TR, typename T, typename V>
+template <int n, typename T, typename V>
 __device__ __forceinline__ V
-contract_v(const V *in, const T (*M)[n], int pa, int base, int s)
+contract_v(const V *in, const T *tab, int pa, int base, int s)
 {
   T c[n];
-  coefs<n, TR>(M, pa, c);
+  coefs<n>(tab, pa, c);
   return contract_c<n>(in, c, base, s);
 }
 
@@ -175,7 +201,7 @@ struct BufLayout
 };
 
 // dynamic LDS of one workgroup: src lattice packs | sweep buffers |
-// accumulator lattice | S, Dq
+// accumulator lattice | coefficient tables (S, S^T, Dq, Dq^T; padded rows)
 template <int dim, int k, typename T>
 struct BrickLDS
 {
@@ -190,8 +216,13 @@ struct BrickLDS
   static size_t
   bytes(int L) // L: padded LDS lattice size
   {
-    return 16 * ((size_t)NP * L + (size_t)WPB * CPW * WB) +
-           sizeof(T) * ((size_t)nc * L + 2 * n * n);
+    return 16 * ((size_t)NP * L + (size_t)WPB * CPW * WB) + tab_offset(L) +
+           sizeof(T) * 4 * n * CoefRow<T, n>::RP;
+  }
+  __host__ __device__ static size_t
+  tab_offset(int L) // accumulator bytes rounded up to 16
+  {
+    return (sizeof(T) * (size_t)nc * L + 15) / 16 * 16;
   }
 };
 
@@ -364,17 +395,26 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
   V        *s_src  = reinterpret_cast<V *>(smem);   // [NP][LP] brick src values
   V        *s_work = s_src + NP * LP;                // [WPB*CPW][WB]
   T        *s_acc  = reinterpret_cast<T *>(s_work + WPB * CPW * WB); // [nc][LP]
-  T(*sS)[n]        = reinterpret_cast<T(*)[n]>(s_acc + nc * LP);
-  T(*sD)[n]        = sS + n;
+  constexpr int RP = CoefRow<T, n>::RP;
+  T        *s_tab  = reinterpret_cast<T *>(reinterpret_cast<unsigned char *>(s_acc) +
+                                     LDS::tab_offset(LP)); // [4][n][RP]
+  const T  *sS     = s_tab + TAB_S * n * RP;
+  const T  *sST    = s_tab + TAB_ST * n * RP;
+  const T  *sD     = s_tab + TAB_D * n * RP;
+  const T  *sDT    = s_tab + TAB_DT * n * RP;
 
   const int64_t brick = a.brick_begin + blockIdx.x;
   if (brick >= a.brick_end)
     return;
   const int t   = threadIdx.x;
-  if (t < n * n)
+  if (t < n * RP)
     {
-      sS[t / n][t % n] = a.sh.S[t / n][t % n];
-      sD[t / n][t % n] = a.sh.Dq[t / n][t % n];
+      const int  r = t / RP, j = t % RP;
+      const bool v = j < n;
+      s_tab[TAB_S * n * RP + t]  = v ? a.sh.S[r][j] : T(0);
+      s_tab[TAB_ST * n * RP + t] = v ? a.sh.S[j][r] : T(0);
+      s_tab[TAB_D * n * RP + t]  = v ? a.sh.Dq[r][j] : T(0);
+      s_tab[TAB_DT * n * RP + t] = v ? a.sh.Dq[j][r] : T(0);
     }
   const int  wave    = t >> 6, lane = t & 63;
   const int  slot    = lane / nq;
@@ -463,7 +503,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
         if (in_wave)
 #pragma unroll
           for (int kp = 0; kp < NP; ++kp)
-            A[kp * BL::KS + q] = contract_v<n, false>(s_src + kp * LP, sS, pa[0], lb, 1);
+            A[kp * BL::KS + q] = contract_v<n>(s_src + kp * LP, sS, pa[0], lb, 1);
       }
       wave_sync();
       V *in = A, *out = B;
@@ -474,7 +514,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
 #pragma unroll
             for (int kp = 0; kp < NP; ++kp)
               out[kp * BL::KS + q] =
-                contract_v<n, false>(in + kp * BL::KS, sS, pa[ax], q - pa[ax] * st[ax], st[ax]);
+                contract_v<n>(in + kp * BL::KS, sS, pa[ax], q - pa[ax] * st[ax], st[ax]);
           wave_sync();
           V *tmp = in;
           in     = out;
@@ -500,7 +540,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
           V       g[dim];
 #pragma unroll
           for (int ax = 0; ax < dim; ++ax)
-            g[ax] = contract_v<n, false>(in + kp * BL::KS, sD, pa[ax], q - pa[ax] * st[ax], st[ax]);
+            g[ax] = contract_v<n>(in + kp * BL::KS, sD, pa[ax], q - pa[ax] * st[ax], st[ax]);
 #pragma unroll
           for (int w = 0; w < W; ++w)
             if (kp * W + w < nc)
@@ -514,39 +554,76 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
       wave_sync();
 
       // ---- q-point physics (do_vmult_cell)
+      // real-space gradients J^{-T} grad_ref: Cartesian bricks (wave-uniform
+      // branch) have a diagonal J^{-1}
       T gu[dim][dim], gp[dim];
+      if (general)
+        {
 #pragma unroll
-      for (int c = 0; c < nc; ++c)
+          for (int c = 0; c < nc; ++c)
 #pragma unroll
-        for (int e = 0; e < dim; ++e)
-          {
-            T s = 0;
+            for (int e = 0; e < dim; ++e)
+              {
+                T s = 0;
 #pragma unroll
-            for (int i = 0; i < dim; ++i)
-              s += cur.inv[i][e] * gref[c][i];
-            if (c < dim)
-              gu[c][e] = s;
-            else
-              gp[e] = s;
-          }
+                for (int i = 0; i < dim; ++i)
+                  s += cur.inv[i][e] * gref[c][i];
+                if (c < dim)
+                  gu[c][e] = s;
+                else
+                  gp[e] = s;
+              }
+        }
+      else
+        {
+#pragma unroll
+          for (int c = 0; c < nc; ++c)
+#pragma unroll
+            for (int e = 0; e < dim; ++e)
+              {
+                const T s = cur.inv[e][e] * gref[c][e];
+                if (c < dim)
+                  gu[c][e] = s;
+                else
+                  gp[e] = s;
+              }
+        }
       T vr[nc], gr[nc][dim];
         qpoint_physics<dim, T, MODE>(val, val[dim], gu, gp, cur.U, cur.GU, cur.GP, cur.UT,
                                      cur.oldg, cur.d1, cur.d2, a.nu, a.w0, a.theta, a.td,
                                      a.have_prev, a.have_old_grad, vr, gr);
       // submit_value / submit_gradient (JxW, J^{-T}); inactive lanes: JxW 0
       T wq[nc], ghat[dim][nc];
-#pragma unroll
-      for (int c = 0; c < nc; ++c)
+      if (general)
         {
-          wq[c] = vr[c] * cur.JxW;
+#pragma unroll
+          for (int c = 0; c < nc; ++c)
+            {
+              wq[c] = vr[c] * cur.JxW;
+#pragma unroll
+              for (int i = 0; i < dim; ++i)
+                {
+                  T s = 0;
+#pragma unroll
+                  for (int e = 0; e < dim; ++e)
+                    s += cur.inv[i][e] * gr[c][e];
+                  ghat[i][c] = s * cur.JxW;
+                }
+            }
+        }
+      else
+        {
+          T sc[dim];
 #pragma unroll
           for (int i = 0; i < dim; ++i)
-            {
-              T s = 0;
+            sc[i] = cur.inv[i][i] * cur.JxW;
 #pragma unroll
-              for (int e = 0; e < dim; ++e)
-                s += cur.inv[i][e] * gr[c][e];
-              ghat[i][c] = s * cur.JxW;
+          for (int c = 0; c < nc; ++c)
+            {
+              wq[c] = vr[c] * cur.JxW;
+#pragma unroll
+              for (int i = 0; i < dim; ++i)
+                ghat[i][c] = gr[c][i] * sc[i];
             }
         }
 
@@ -579,12 +656,12 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
 #pragma unroll
           for (int kp = 0; kp < NP; ++kp)
             {
-              wv[kp] += contract_v<n, true>(A + kp * BL::KS, sD, pa[ax0], q - pa[ax0] * st[ax0],
+              wv[kp] += contract_v<n>(A + kp * BL::KS, sDT, pa[ax0], q - pa[ax0] * st[ax0],
                                             st[ax0]);
               if (ax0 + 1 < dim)
                 {
                   const int ax1 = (ax0 + 1) % dim;
-                  wv[kp] += contract_v<n, true>(B + kp * BL::KS, sD, pa[ax1],
+                  wv[kp] += contract_v<n>(B + kp * BL::KS, sDT, pa[ax1],
                                                 q - pa[ax1] * st[ax1], st[ax1]);
                 }
             }
@@ -612,14 +689,14 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
 #pragma unroll
             for (int kp = 0; kp < NP; ++kp)
               out[kp * BL::KS + q] =
-                contract_v<n, true>(in + kp * BL::KS, sS, pa[ax], q - pa[ax] * st[ax], st[ax]);
+                contract_v<n>(in + kp * BL::KS, sST, pa[ax], q - pa[ax] * st[ax], st[ax]);
           wave_sync();
           V *tmp = in;
           in     = out;
           out    = tmp;
         }
       T cx[n];
-      coefs<n, true>(sS, pa[0], cx);
+      coefs<n>(sST, pa[0], cx);
       if (active_now)
 #pragma unroll
         for (int kp = 0; kp < NP; ++kp)
