@@ -407,6 +407,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
   if (brick >= a.brick_end)
     return;
   const int t   = threadIdx.x;
+  GLS_STAMP(brick, 0);
   if (t < n * RP)
     {
       const int  r = t / RP, j = t % RP;
@@ -493,6 +494,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
         s_src[kp * LP + ip] = v[kp];
     }
   __syncthreads();
+  GLS_STAMP(brick, 1);
 
   for (int base = 0; base < ncell; base += step)
     {
@@ -553,6 +555,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
         }
       wave_sync();
 
+      GLS_STAMP(brick, base == 0 ? 2 : 4);
       // ---- q-point physics (do_vmult_cell)
       // real-space gradients J^{-T} grad_ref: Cartesian bricks (wave-uniform
       // branch) have a diagonal J^{-1}
@@ -674,6 +677,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
       // the next round's geometry and tables: issued here (few registers
       // live), in flight during the S^T sweeps and the next evaluate (this
       // round's lattice position is kept: the prefetch overwrites cur)
+      GLS_STAMP(brick, base == 0 ? 3 : 5);
       const int  li_now     = cur.li;
       const bool active_now = cur.active;
       if (base + step < ncell)
@@ -710,6 +714,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
       wave_sync();
     }
   __syncthreads();
+  GLS_STAMP(brick, 6);
 
   // ---- write out: exclusive nodes -> dst, boundary nodes -> partials
 #pragma unroll
@@ -745,6 +750,7 @@ __global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
           store_node<T, nc>(a.dst, tgt, r);
         }
     }
+  GLS_STAMP(brick, 7);
 }
 
 // Sum the per-brick partials of every brick-boundary node (one contiguous
@@ -765,9 +771,25 @@ __global__ void __launch_bounds__(256)
   const int      c      = (int)(gid - s * nc);
   const uint32_t b      = offsets[s], e = offsets[s + 1];
   const uint32_t packed = nodes[s];
-  T              sum    = 0;
-  for (uint32_t i = b; i < e; ++i)
-    sum += partial[(size_t)i * nc + c];
+  // the slot loads of a node are independent: issue them four at a time
+  // (a plain loop waits one memory latency per slot)
+  const T *pp = partial + c;
+  T        sum = 0;
+  uint32_t i   = b;
+  for (; i + 4 <= e; i += 4)
+    {
+      const T x0 = pp[(size_t)i * nc], x1 = pp[(size_t)(i + 1) * nc];
+      const T x2 = pp[(size_t)(i + 2) * nc], x3 = pp[(size_t)(i + 3) * nc];
+      sum += (x0 + x1) + (x2 + x3);
+    }
+  if (i + 2 <= e)
+    {
+      const T x0 = pp[(size_t)i * nc], x1 = pp[(size_t)(i + 1) * nc];
+      sum += x0 + x1;
+      i += 2;
+    }
+  if (i < e)
+    sum += pp[(size_t)i * nc];
   const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
   if ((cm >> c) & 1)
     sum = R ? T(0) : src[(size_t)node * nc + c];

@@ -54,10 +54,10 @@ def main():
     st = buf.reshape(-1, 4, 8)[:nb].astype(np.float64)
     t0 = st[:, :, 0][st[:, :, 0] > 0].min()
     t = np.where(st > 0, (st - t0) * 10.0 / 1000.0, np.nan)  # us (100 MHz clock)
-    names = {0: "brick top", 1: "r0 physics start", 2: "r0 physics end", 4: "r1 physics start",
-             5: "r1 physics end", 7: "rounds done"}
+    names = {0: "top", 1: "prologue done", 2: "r0 evaluate done", 3: "r0 physics done",
+             4: "r1 evaluate done", 5: "r1 physics done", 6: "rounds done", 7: "written"}
     res = {"n_bricks": int(nb), "phases_us": {}}
-    order = [0, 1, 2, 4, 5, 7]
+    order = [0, 1, 2, 3, 4, 5, 6, 7]
     for a, b in zip(order[:-1], order[1:]):
         dd = t[:, :, b] - t[:, :, a]
         res["phases_us"][f"{names[a]} -> {names[b]}"] = [float(np.nanmean(dd)),
