@@ -24,6 +24,7 @@
 // Software-pipelining the next round's loads was measured and gave nothing.
 #pragma once
 
+#include "common.h"
 #include "kernels.h"
 
 
@@ -790,6 +791,52 @@ __global__ void __launch_bounds__(256)
     }
   if (i < e)
     sum += pp[(size_t)i * nc];
+  const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
+  if ((cm >> c) & 1)
+    sum = R ? T(0) : src[(size_t)node * nc + c];
+  dst[(size_t)node * nc + c] = sum;
+}
+
+// Same reduction with the shared nodes ordered by brick multiplicity
+// (build_bricks): the slots of node s of class (first, m, slot0) are
+// slot0 + (s - first) * m + [0, m), computed, not loaded, so the slot loads
+// issue together with the node id load (one memory round trip, not two).
+template <typename T, int nc, bool R>
+__global__ void __launch_bounds__(256)
+  k_shared_reduce_cls(T *__restrict__ dst, const T *__restrict__ src,
+                      const T *__restrict__ partial, const uint32_t *__restrict__ nodes,
+                      const ReduceClasses rc, int64_t n_shared)
+{
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n_shared * nc)
+    return;
+  const uint32_t s = (uint32_t)(gid / nc);
+  const int      c = (int)(gid - (int64_t)s * nc);
+  int            k = 0;
+#pragma unroll
+  for (int j = 1; j < ReduceClasses::MAX; ++j)
+    if (j < rc.n && s >= rc.first[j])
+      k = j;
+  const uint32_t m      = rc.mult[k];
+  const uint32_t b      = rc.slot0[k] + (s - rc.first[k]) * m;
+  const uint32_t packed = nodes[s];
+  const T       *pp     = partial + c;
+  T              sum    = 0;
+  uint32_t       i      = 0;
+  for (; i + 4 <= m; i += 4)
+    {
+      const T x0 = pp[(size_t)(b + i) * nc], x1 = pp[(size_t)(b + i + 1) * nc];
+      const T x2 = pp[(size_t)(b + i + 2) * nc], x3 = pp[(size_t)(b + i + 3) * nc];
+      sum += (x0 + x1) + (x2 + x3);
+    }
+  if (i + 2 <= m)
+    {
+      const T x0 = pp[(size_t)(b + i) * nc], x1 = pp[(size_t)(b + i + 1) * nc];
+      sum += x0 + x1;
+      i += 2;
+    }
+  if (i < m)
+    sum += pp[(size_t)(b + i) * nc];
   const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
   if ((cm >> c) & 1)
     sum = R ? T(0) : src[(size_t)node * nc + c];

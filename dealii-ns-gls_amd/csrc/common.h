@@ -34,6 +34,16 @@ void set_error(const std::string &s);
     }                                             \
   return 0;
 
+// multiplicity classes of the brick-boundary nodes (k_shared_reduce_cls)
+struct ReduceClasses
+{
+  static constexpr int MAX = 16;
+  int                  n   = 0; // classes; -1: too many (offset-table kernel)
+  uint32_t             first[MAX + 1];
+  uint32_t             mult[MAX];
+  uint32_t             slot0[MAX];
+};
+
 // FE_Q(k) on Gauss-Lobatto points, QGauss(k+1), on [0,1]
 struct Basis1D
 {

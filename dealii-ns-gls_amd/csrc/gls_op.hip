@@ -242,9 +242,36 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
           shared_nodes.push_back((uint32_t)node);
         }
     }
+  // order the shared nodes by brick multiplicity (then node): inside a
+  // class of multiplicity m node j's slots start at slot0 + j * m, so
+  // k_shared_reduce computes its slot addresses instead of loading them
+  std::stable_sort(shared_nodes.begin(), shared_nodes.end(),
+                   [&](uint32_t x, uint32_t y) { return mult[x] < mult[y]; });
+  for (size_t s = 0; s < shared_nodes.size(); ++s)
+    shared_index[shared_nodes[s]] = (int64_t)s;
   std::vector<uint32_t> off(shared_nodes.size() + 1, 0);
   for (size_t s = 0; s < shared_nodes.size(); ++s)
     off[s + 1] = off[s] + mult[shared_nodes[s]];
+  ReduceClasses rc{};
+  for (size_t s = 0; s < shared_nodes.size(); ++s)
+    {
+      const uint32_t m = mult[shared_nodes[s]];
+      if (rc.n == 0 || rc.mult[rc.n - 1] != m)
+        {
+          if (rc.n == ReduceClasses::MAX)
+            {
+              rc.n = -1; // too many classes: offsets kernel
+              break;
+            }
+          rc.first[rc.n] = (uint32_t)s;
+          rc.mult[rc.n]  = m;
+          rc.slot0[rc.n] = off[s];
+          rc.n++;
+        }
+    }
+  if (rc.n >= 0)
+    rc.first[rc.n] = (uint32_t)shared_nodes.size();
+  op->reduce_classes = rc;
   const uint64_t n_slot_total = off.back();
   if (n_slot_total >= SHARED_BIT)
     throw std::runtime_error("gls_op_create: too many partial slots");
@@ -555,7 +582,16 @@ struct Impl
         if (op->n_shared > 0)
           {
             const dim3 g2((unsigned)((op->n_shared * (dim + 1) + 255) / 256));
-            if (mode == MODE_RESIDUAL)
+            const ReduceClasses &rc = op->reduce_classes;
+            if (rc.n > 0 && mode == MODE_RESIDUAL)
+              hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, true>), g2, dim3(256), 0, s,
+                                 (T *)dst, (const T *)src, (const T *)op->d_partial,
+                                 op->d_shared_nodes, rc, op->n_shared);
+            else if (rc.n > 0)
+              hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, false>), g2, dim3(256), 0, s,
+                                 (T *)dst, (const T *)src, (const T *)op->d_partial,
+                                 op->d_shared_nodes, rc, op->n_shared);
+            else if (mode == MODE_RESIDUAL)
               hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, true>), g2, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)op->d_partial,
                                  op->d_shared_nodes, op->d_shared_off, op->n_shared);

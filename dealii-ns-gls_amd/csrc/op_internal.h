@@ -45,6 +45,7 @@ struct glsOp_
   uint32_t *d_brick_target = nullptr;
   uint32_t *d_shared_nodes = nullptr;
   uint32_t *d_shared_off   = nullptr;
+  gls::ReduceClasses reduce_classes{}; // multiplicity classes of the shared nodes
   void     *d_partial      = nullptr;
   void     *d_bgeo_cart    = nullptr; // brick path: cell-indexed geometry
   void     *d_bgeo_gen     = nullptr;
