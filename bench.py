@@ -174,11 +174,17 @@ def main():
         if kernel_ms is None:
             kernel_ms = ms
         achieved = bytes_per_vmult / (kernel_ms * 1e-3)
+        # HBM bytes per vmult from the committed rocprofv3 PMC passes of this
+        # workload (scripts/pmc.sh + scripts/pmc_summary.py), when they match
         traffic = None
-        tf = os.environ.get("GLS_TRAFFIC_JSON")
-        if tf and os.path.exists(tf):
+        tf = os.environ.get("GLS_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r01", "pmc",
+                                                             "traffic.json"))
+        if tf and os.path.exists(tf) and world == 1:
             with open(tf) as f:
-                traffic = json.load(f).get("bytes_per_launch")
+                tj = json.load(f)
+            wl = tj.get("workload", {})
+            if wl.get("nref") == n_ref and wl.get("precision") == args.precision:
+                traffic = tj.get("bytes_per_launch")
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
@@ -207,7 +213,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
                          "kernel": "vmult = gls::k_brick<3,2,double,MODE_NEWTON> + "
-                                   "gls::k_shared_reduce (both inside the events)",
+                                   "gls::k_shared_reduce_cls (both inside the events)",
                          "kernel_ms": kernel_ms, "algorithmic_bytes": bytes_per_vmult},
             "cpu_baseline": cpu,
         }

@@ -22,7 +22,9 @@ for k, d in out.items():
     print(k)
     for c, v in d.items():
         print(f"   {c:24s} {v:16.1f}")
-res = {"bytes_per_launch": traffic,
+wl = {"nref": int(sys.argv[2]) if len(sys.argv) > 2 else 2,
+      "precision": sys.argv[3] if len(sys.argv) > 3 else "f64"}
+res = {"bytes_per_launch": traffic, "workload": wl,
        "method": "per vmult: k_brick + k_shared_reduce, 1024*(2*FETCH_SIZE + WRITE_SIZE) "
                  "(gfx950: FETCH_SIZE counts half of wide coalesced reads)",
        "counters": out}
