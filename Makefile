@@ -15,8 +15,8 @@ CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
 HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics \
             -Wall -Wno-unused-parameter -Wno-unused-function
 
-# rocsolver/rocblas: dense LU of the coarse multigrid level only
-AMD_LIBS := -L/opt/rocm/lib -lrocsolver -lrocblas -Wl,-rpath,/opt/rocm/lib
+# rocsolver/rocblas: dense LU of the coarse multigrid level only; rccl: ghost exchange
+AMD_LIBS := -L/opt/rocm/lib -lrocsolver -lrocblas -lrccl -Wl,-rpath,/opt/rocm/lib
 
 MESH_SRC := $(PKG)/host/mesh.cc
 AMD_SRC  := $(wildcard $(PKG)/csrc/*.hip) $(wildcard $(PKG)/csrc/*.cc)

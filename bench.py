@@ -82,7 +82,10 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     dist = None
-    if world > 1:
+    # GLS_BENCH_DIST=1: the partitioned path at world 1 too (a rehearsal of
+    # the multi-GPU code path on a one-GPU box)
+    use_dist = world > 1 or os.environ.get("GLS_BENCH_DIST") == "1"
+    if use_dist:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
@@ -100,12 +103,31 @@ def main():
     hist = gi.history(u_star, params["order"])
     log(f"[bench] mesh {mesh.n_cells} cells, {n_dofs} DoFs ({time.time() - t0:.1f}s)")
 
-    if world > 1:
+    if use_dist:
         import glsdist
         runner = glsdist.DistributedOperator(mesh, cmask, args.precision, dist, rank, world)
         runner.setup(params, u_star, hist, weights)
         src = runner.scatter_global(src_h)
         dst = runner.new_vector()
+        # cross-check the native RCCL path (gls_dist_vmult) against the
+        # torch point-to-point exchange around the same local operator once;
+        # on a mismatch every rank falls back to the latter (reported)
+        exchange = "rccl-native, overlapped with the interior bricks"
+        ref = runner.new_vector()
+        runner.vmult_p2p(ref, src.clone())
+        s2 = src.clone()
+        s2[runner.r.n_owned_dofs:].zero_()
+        runner.vmult(dst, s2)
+        torch.cuda.synchronize()
+        n = runner.r.n_owned_dofs
+        err = torch.tensor([float((dst[:n] - ref[:n]).norm()), float(ref[:n].norm())],
+                           dtype=torch.float64, device="cuda")
+        dist.all_reduce(err)
+        rel = float(err[0]) / max(float(err[1]), 1e-300)
+        log(f"[bench] native vs p2p partitioned vmult: rel err {rel:.2e}")
+        if not rel < 1e-12:
+            runner.native = None
+            exchange = f"torch-p2p (native mismatch {rel:.1e})"
         apply_fn = lambda: runner.vmult(dst, src)  # noqa: E731
         local_cells = runner.n_local_cells
         op = runner.op
@@ -113,7 +135,7 @@ def main():
         def kernel_fn(ev0, ev1):
             # rank-local cell loop (k_brick + k_shared_reduce), no exchange
             ev0.record()
-            op.vmult(dst, src)
+            op.vmult(ref, src)
             ev1.record()
     else:
         brick = tuple(int(x) for x in args.brick.split(",")) if args.brick else None
@@ -125,6 +147,7 @@ def main():
         src = op._dev(src_h)
         dst = op.initialize_dof_vector()
         local_cells = op.n_cells
+        exchange = None
 
         def apply_fn():
             op.vmult(dst, src)
@@ -209,7 +232,8 @@ def main():
                                    f"Q2/Q2, MappingQ2, BDF2, increment form",
                        "cells": mesh.n_cells, "dofs": n_dofs, "cells_per_gpu": local_cells,
                        "general_geometry_cells": n_gen, "cartesian_cells": n_cart,
-                       "parallelism": f"cells x-slab partitioned over {world} GPU(s)"},
+                       "parallelism": f"cells x-slab partitioned over {world} GPU(s)"
+                                      + (f", ghost exchange {exchange}" if exchange else "")},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
                          "kernel": "vmult = gls::k_brick<3,2,double,MODE_NEWTON> + "

@@ -34,6 +34,12 @@ void set_error(const std::string &s);
     }                                             \
   return 0;
 
+enum
+{
+  BRICK_RUN    = 1,
+  BRICK_REDUCE = 2
+};
+
 // multiplicity classes of the brick-boundary nodes (k_shared_reduce_cls)
 struct ReduceClasses
 {

@@ -1,0 +1,529 @@
+// dist.hip — partitioned (one rank per GPU) vmult of the GLS operator with
+// the ghost exchange over RCCL (xGMI), overlapped with the interior bricks.
+//
+// Reference behaviour (deal.II distributed vectors inside
+// MatrixFree::cell_loop, operator_ns.cc:702-721):
+//   src.update_ghost_values()            owner -> ghost copies   (import)
+//   dst = cell loop (ghost rows collect partial sums)
+//   dst.compress(VectorOperation::add)   ghost partials -> owner, added;
+//                                        ghost entries zeroed   (export-add)
+//   dst[c] = src[c] on constrained owned dofs        (identity rows)
+//
+// One gls_dist_vmult on stream s:
+//   pack      k_pack: send buffer <- src[send nodes]                  (s)
+//   import    ncclSend/ncclRecv per peer, the receives land directly in
+//             src's ghost block of that owner                          (comm stream)
+//   interior  k_brick over the work units that read no ghost node      (s, overlaps the import)
+//   boundary  k_brick over the rest, after the import event            (s)
+//   reduce    k_shared_reduce_cls: brick boundaries, ghost rows, identity rows
+//   export    ncclSend of each owner's ghost block of dst, ncclRecv into
+//             the export buffer                                        (s)
+//   unpack    k_unpack_add: owned rows += received partials (fixed order
+//             per node, constrained components skipped: their identity
+//             value stands), then the ghost block of dst is zeroed.
+// The in-process group (gls_dist_create with nccl_id NULL) runs the same
+// phases with device copies in place of RCCL, so the whole orchestration
+// is testable on one GPU (tests/test_dist.py).
+#include "../../include/gls_op.h"
+#include "common.h"
+#include "kernels.h"
+#include "op_internal.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace gls
+{
+void brick_launch(const glsOp_ *op, int mode, void *dst, const void *src, int64_t b0, int64_t b1,
+                  int what, hipStream_t s);
+int  op_vmult_mode(const glsOp_ *op);
+
+// send buffer <- src rows of the send nodes (plain values)
+template <typename T, int nc>
+__global__ void __launch_bounds__(256)
+  k_pack(T *__restrict__ buf, const T *__restrict__ src, const uint32_t *__restrict__ nodes,
+         int64_t n)
+{
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n * nc)
+    return;
+  const int64_t j = gid / nc;
+  const int     c = (int)(gid - j * nc);
+  buf[gid]        = src[(size_t)(nodes[j] & NODE_MASK) * nc + c];
+}
+
+// owned rows += the partial sums the peers computed for them (compress(add));
+// one thread per (receiving node, component), contributions summed in a fixed
+// order, constrained components keep their identity-row value
+template <typename T, int nc>
+__global__ void __launch_bounds__(256)
+  k_unpack_add(T *__restrict__ dst, const T *__restrict__ xrecv,
+               const uint32_t *__restrict__ nodes, const uint32_t *__restrict__ off,
+               const uint32_t *__restrict__ entry, int64_t n)
+{
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n * nc)
+    return;
+  const int64_t  u      = gid / nc;
+  const int      c      = (int)(gid - u * nc);
+  const uint32_t packed = nodes[u];
+  if ((packed >> 28 >> c) & 1)
+    return;
+  T s = 0;
+  for (uint32_t e = off[u]; e < off[u + 1]; ++e)
+    s += xrecv[(size_t)entry[e] * nc + c];
+  dst[(size_t)(packed & NODE_MASK) * nc + c] += s;
+}
+} // namespace gls
+
+namespace
+{
+#define NCCL_THROW(x)                                                                          \
+  do                                                                                           \
+    {                                                                                          \
+      ncclResult_t r_ = (x);                                                                   \
+      if (r_ != ncclSuccess)                                                                   \
+        throw std::runtime_error(std::string("RCCL: ") + ncclGetErrorString(r_) + " at " +   \
+                                 #x);                                                          \
+    }                                                                                          \
+  while (0)
+
+struct Peer
+{
+  int     rank;
+  int64_t send_off, send_cnt;    // in the send / export-receive buffers (nodes)
+  int64_t recv_begin, recv_cnt;  // ghost block of this owner (local nodes)
+};
+
+struct Group; // in-process group (tests)
+} // namespace
+
+struct glsDist_
+{
+  glsOp_           *op = nullptr;
+  int               rank = 0, world = 1;
+  ncclComm_t        comm = nullptr;
+  Group            *group = nullptr;
+  hipStream_t       cs   = nullptr;
+  hipEvent_t        ev_packed = nullptr, ev_imported = nullptr;
+  std::vector<Peer> peers;
+  int64_t           n_send = 0, n_recv_nodes = 0;
+  uint32_t         *d_send_nodes = nullptr; // [n_send] node | cmask << 28
+  void             *d_send_buf   = nullptr; // [n_send][nc]
+  void             *d_xrecv_buf  = nullptr; // [n_send][nc]
+  uint32_t         *d_un_nodes = nullptr, *d_un_off = nullptr, *d_un_entry = nullptr;
+  int64_t           n_un = 0;
+  // vectors of the current call (in-process group: peers read them)
+  void             *cur_dst = nullptr, *cur_src = nullptr;
+};
+
+namespace
+{
+struct Group
+{
+  std::vector<glsDist_ *> members; // by rank
+};
+
+size_t
+row_bytes(const glsOp_ *op)
+{
+  return (size_t)(op->dim + 1) * op->tsize();
+}
+
+const Peer *
+find_peer(const glsDist_ *d, int rank)
+{
+  for (const Peer &p : d->peers)
+    if (p.rank == rank)
+      return &p;
+  return nullptr;
+}
+
+template <typename T>
+void
+launch_pack(glsDist_ *d, const void *src, hipStream_t s)
+{
+  const int nc = d->op->dim + 1;
+  if (d->n_send == 0)
+    return;
+  const dim3 g((unsigned)((d->n_send * nc + 255) / 256));
+  if (nc == 4)
+    hipLaunchKernelGGL((gls::k_pack<T, 4>), g, dim3(256), 0, s, (T *)d->d_send_buf,
+                       (const T *)src, d->d_send_nodes, d->n_send);
+  else
+    hipLaunchKernelGGL((gls::k_pack<T, 3>), g, dim3(256), 0, s, (T *)d->d_send_buf,
+                       (const T *)src, d->d_send_nodes, d->n_send);
+  HIP_THROW(hipGetLastError());
+}
+
+template <typename T>
+void
+launch_unpack(glsDist_ *d, void *dst, hipStream_t s)
+{
+  const int nc = d->op->dim + 1;
+  if (d->n_un == 0)
+    return;
+  const dim3 g((unsigned)((d->n_un * nc + 255) / 256));
+  if (nc == 4)
+    hipLaunchKernelGGL((gls::k_unpack_add<T, 4>), g, dim3(256), 0, s, (T *)dst,
+                       (const T *)d->d_xrecv_buf, d->d_un_nodes, d->d_un_off, d->d_un_entry,
+                       d->n_un);
+  else
+    hipLaunchKernelGGL((gls::k_unpack_add<T, 3>), g, dim3(256), 0, s, (T *)dst,
+                       (const T *)d->d_xrecv_buf, d->d_un_nodes, d->d_un_off, d->d_un_entry,
+                       d->n_un);
+  HIP_THROW(hipGetLastError());
+}
+
+void
+pack(glsDist_ *d, const void *src, hipStream_t s)
+{
+  if (d->op->prec == GLS_F64)
+    launch_pack<double>(d, src, s);
+  else
+    launch_pack<float>(d, src, s);
+}
+
+void
+unpack(glsDist_ *d, void *dst, hipStream_t s)
+{
+  if (d->op->prec == GLS_F64)
+    launch_unpack<double>(d, dst, s);
+  else
+    launch_unpack<float>(d, dst, s);
+}
+
+ncclDataType_t
+nccl_type(const glsOp_ *op)
+{
+  return op->prec == GLS_F64 ? ncclDouble : ncclFloat;
+}
+
+// ---- RCCL transport
+void
+nccl_import(glsDist_ *d, void *src)
+{
+  const size_t rb = row_bytes(d->op);
+  const int    nc = d->op->dim + 1;
+  NCCL_THROW(ncclGroupStart());
+  for (const Peer &p : d->peers)
+    {
+      if (p.recv_cnt > 0)
+        NCCL_THROW(ncclRecv((char *)src + p.recv_begin * rb, (size_t)p.recv_cnt * nc,
+                            nccl_type(d->op), p.rank, d->comm, d->cs));
+      if (p.send_cnt > 0)
+        NCCL_THROW(ncclSend((const char *)d->d_send_buf + p.send_off * rb,
+                            (size_t)p.send_cnt * nc, nccl_type(d->op), p.rank, d->comm, d->cs));
+    }
+  NCCL_THROW(ncclGroupEnd());
+}
+
+void
+nccl_export(glsDist_ *d, void *dst, hipStream_t s)
+{
+  const size_t rb = row_bytes(d->op);
+  const int    nc = d->op->dim + 1;
+  NCCL_THROW(ncclGroupStart());
+  for (const Peer &p : d->peers)
+    {
+      if (p.send_cnt > 0)
+        NCCL_THROW(ncclRecv((char *)d->d_xrecv_buf + p.send_off * rb, (size_t)p.send_cnt * nc,
+                            nccl_type(d->op), p.rank, d->comm, s));
+      if (p.recv_cnt > 0)
+        NCCL_THROW(ncclSend((const char *)dst + p.recv_begin * rb, (size_t)p.recv_cnt * nc,
+                            nccl_type(d->op), p.rank, d->comm, s));
+    }
+  NCCL_THROW(ncclGroupEnd());
+}
+
+// ---- in-process transport: the same data movement as device copies (all
+// members of the group share one device and run the phases in lockstep)
+void
+local_import(glsDist_ *d, hipStream_t s)
+{
+  const size_t rb = row_bytes(d->op);
+  for (const Peer &p : d->peers)
+    {
+      if (p.recv_cnt == 0)
+        continue;
+      const glsDist_ *q  = d->group->members.at(p.rank);
+      const Peer     *qp = find_peer(q, d->rank);
+      if (!qp || qp->send_cnt != p.recv_cnt)
+        throw std::runtime_error("gls_dist: inconsistent exchange lists");
+      HIP_THROW(hipMemcpyAsync((char *)d->cur_src + p.recv_begin * rb,
+                               (const char *)q->d_send_buf + qp->send_off * rb,
+                               (size_t)p.recv_cnt * rb, hipMemcpyDeviceToDevice, s));
+    }
+}
+
+void
+local_export(glsDist_ *d, hipStream_t s)
+{
+  const size_t rb = row_bytes(d->op);
+  for (const Peer &p : d->peers)
+    {
+      if (p.send_cnt == 0)
+        continue;
+      const glsDist_ *q  = d->group->members.at(p.rank);
+      const Peer     *qp = find_peer(q, d->rank);
+      if (!qp || qp->recv_cnt != p.send_cnt)
+        throw std::runtime_error("gls_dist: inconsistent exchange lists");
+      HIP_THROW(hipMemcpyAsync((char *)d->d_xrecv_buf + p.send_off * rb,
+                               (const char *)q->cur_dst + qp->recv_begin * rb,
+                               (size_t)p.send_cnt * rb, hipMemcpyDeviceToDevice, s));
+    }
+}
+
+void
+zero_ghosts(glsDist_ *d, void *dst, hipStream_t s)
+{
+  const glsOp_ *op = d->op;
+  const size_t  g  = (size_t)(op->n_dofs - op->n_owned_dofs) * op->tsize();
+  if (g)
+    HIP_THROW(hipMemsetAsync((char *)dst + (size_t)op->n_owned_dofs * op->tsize(), 0, g, s));
+}
+
+void
+check_vectors(glsDist_ *d, void *dst, void *src)
+{
+  if (!d || !dst || !src || dst == src)
+    throw std::runtime_error("gls_dist_vmult: bad arguments");
+  if (!d->op->have_lin)
+    throw std::runtime_error("gls_dist_vmult before set_linearization_point");
+  if (!d->op->use_brick)
+    throw std::runtime_error("gls_dist_vmult needs the brick decomposition (glsOpDesc.brick)");
+}
+} // namespace
+
+extern "C" {
+
+glsStatus
+gls_dist_unique_id(void *id_out)
+{
+  GLS_TRY
+  if (!id_out)
+    throw std::runtime_error("gls_dist_unique_id: null argument");
+  ncclUniqueId id;
+  NCCL_THROW(ncclGetUniqueId(&id));
+  std::memcpy(id_out, &id, sizeof(id));
+  GLS_CATCH
+}
+
+glsStatus
+gls_dist_create(glsOp op, const glsDistDesc *desc, glsDist *out)
+{
+  GLS_TRY
+  if (!op || !desc || !out)
+    throw std::runtime_error("gls_dist_create: null argument");
+  if (desc->world < 1 || desc->rank < 0 || desc->rank >= desc->world)
+    throw std::runtime_error("gls_dist_create: bad rank / world");
+  HIP_THROW(hipSetDevice(op->device));
+  auto d   = std::make_unique<glsDist_>();
+  d->op    = op;
+  d->rank  = desc->rank;
+  d->world = desc->world;
+  int64_t off = 0;
+  for (int i = 0; i < desc->n_peers; ++i)
+    {
+      Peer p;
+      p.rank       = desc->peers[i];
+      p.send_off   = off;
+      p.send_cnt   = desc->send_count[i];
+      p.recv_begin = desc->recv_begin[i];
+      p.recv_cnt   = desc->recv_count[i];
+      if (p.rank < 0 || p.rank >= d->world || p.rank == d->rank)
+        throw std::runtime_error("gls_dist_create: bad peer rank");
+      if (p.recv_cnt > 0 && (p.recv_begin < op->n_owned_nodes ||
+                             p.recv_begin + p.recv_cnt > op->n_nodes))
+        throw std::runtime_error("gls_dist_create: ghost block outside the ghost range");
+      off += p.send_cnt;
+      d->n_recv_nodes += p.recv_cnt;
+      d->peers.push_back(p);
+    }
+  d->n_send = off;
+  // send nodes (cmask bits attached) and the per-node CSR of the export-add
+  std::vector<uint32_t> sn((size_t)d->n_send);
+  for (int64_t j = 0; j < d->n_send; ++j)
+    {
+      const uint32_t node = desc->send_nodes[j];
+      if ((int64_t)node >= op->n_owned_nodes)
+        throw std::runtime_error("gls_dist_create: send node is not owned");
+      sn[j] = node | (uint32_t)(op->h_cmask[node] & 0xF) << 28;
+    }
+  std::vector<uint32_t> idx((size_t)d->n_send);
+  for (int64_t j = 0; j < d->n_send; ++j)
+    idx[j] = (uint32_t)j;
+  std::stable_sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) {
+    return (sn[x] & gls::NODE_MASK) < (sn[y] & gls::NODE_MASK);
+  });
+  std::vector<uint32_t> un, uoff{0}, uent;
+  for (int64_t j = 0; j < d->n_send; ++j)
+    {
+      const uint32_t e = idx[j];
+      if (un.empty() || (un.back() & gls::NODE_MASK) != (sn[e] & gls::NODE_MASK))
+        {
+          if (!un.empty())
+            uoff.push_back((uint32_t)uent.size());
+          un.push_back(sn[e]);
+        }
+      uent.push_back(e);
+    }
+  if (!un.empty())
+    uoff.push_back((uint32_t)uent.size());
+  d->n_un      = (int64_t)un.size();
+  const size_t rb = row_bytes(op);
+  auto up = [](void **p, const void *h, size_t bytes) {
+    HIP_THROW(hipMalloc(p, std::max<size_t>(bytes, 16)));
+    if (bytes)
+      HIP_THROW(hipMemcpy(*p, h, bytes, hipMemcpyHostToDevice));
+  };
+  up((void **)&d->d_send_nodes, sn.data(), sn.size() * 4);
+  up((void **)&d->d_un_nodes, un.data(), un.size() * 4);
+  up((void **)&d->d_un_off, uoff.data(), uoff.size() * 4);
+  up((void **)&d->d_un_entry, uent.data(), uent.size() * 4);
+  HIP_THROW(hipMalloc(&d->d_send_buf, std::max<size_t>(16, (size_t)d->n_send * rb)));
+  HIP_THROW(hipMalloc(&d->d_xrecv_buf, std::max<size_t>(16, (size_t)d->n_send * rb)));
+  HIP_THROW(hipStreamCreateWithFlags(&d->cs, hipStreamNonBlocking));
+  HIP_THROW(hipEventCreateWithFlags(&d->ev_packed, hipEventDisableTiming));
+  HIP_THROW(hipEventCreateWithFlags(&d->ev_imported, hipEventDisableTiming));
+  if (desc->nccl_id)
+    {
+      ncclUniqueId id;
+      std::memcpy(&id, desc->nccl_id, sizeof(id));
+      NCCL_THROW(ncclCommInitRank(&d->comm, d->world, id, d->rank));
+    }
+  else
+    {
+      // in-process group: the members find each other through the group
+      // handle passed as desc->group (NULL for the first member)
+      Group *g = desc->group ? reinterpret_cast<glsDist_ *>(desc->group)->group : new Group;
+      if ((int)g->members.size() < d->world)
+        g->members.resize((size_t)d->world, nullptr);
+      if (g->members[d->rank])
+        throw std::runtime_error("gls_dist_create: rank already in the group");
+      g->members[d->rank] = d.get();
+      d->group            = g;
+    }
+  *out = d.release();
+  GLS_CATCH
+}
+
+void
+gls_dist_destroy(glsDist d)
+{
+  if (!d)
+    return;
+  if (d->comm)
+    (void)ncclCommDestroy(d->comm);
+  if (d->group)
+    {
+      d->group->members[d->rank] = nullptr;
+      bool empty                 = true;
+      for (auto *m : d->group->members)
+        empty = empty && !m;
+      if (empty)
+        delete d->group;
+    }
+  (void)hipFree(d->d_send_nodes);
+  (void)hipFree(d->d_un_nodes);
+  (void)hipFree(d->d_un_off);
+  (void)hipFree(d->d_un_entry);
+  (void)hipFree(d->d_send_buf);
+  (void)hipFree(d->d_xrecv_buf);
+  if (d->ev_packed)
+    (void)hipEventDestroy(d->ev_packed);
+  if (d->ev_imported)
+    (void)hipEventDestroy(d->ev_imported);
+  if (d->cs)
+    (void)hipStreamDestroy(d->cs);
+  delete d;
+}
+
+glsStatus
+gls_dist_vmult(glsDist d, void *dst, void *src, void *stream)
+{
+  GLS_TRY
+  check_vectors(d, dst, src);
+  if (!d->comm)
+    throw std::runtime_error("gls_dist_vmult: in-process group members run gls_dist_vmult_group");
+  hipStream_t   s    = (hipStream_t)stream;
+  glsOp_       *op   = d->op;
+  const int     mode = gls::op_vmult_mode(op);
+  // import (comm stream) || interior bricks (s)
+  pack(d, src, s);
+  HIP_THROW(hipEventRecord(d->ev_packed, s));
+  HIP_THROW(hipStreamWaitEvent(d->cs, d->ev_packed, 0));
+  nccl_import(d, src);
+  HIP_THROW(hipEventRecord(d->ev_imported, d->cs));
+  gls::brick_launch(op, mode, dst, src, 0, op->n_interior_bricks, gls::BRICK_RUN, s);
+  HIP_THROW(hipStreamWaitEvent(s, d->ev_imported, 0));
+  gls::brick_launch(op, mode, dst, src, op->n_interior_bricks, op->n_bricks,
+                    gls::BRICK_RUN | gls::BRICK_REDUCE, s);
+  // compress(add)
+  nccl_export(d, dst, s);
+  unpack(d, dst, s);
+  zero_ghosts(d, dst, s);
+  GLS_CATCH
+}
+
+glsStatus
+gls_dist_vmult_group(glsDist const *members, void *const *dsts, void *const *srcs, int n,
+                     void *stream)
+{
+  GLS_TRY
+  if (!members || !dsts || !srcs || n < 1)
+    throw std::runtime_error("gls_dist_vmult_group: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  for (int r = 0; r < n; ++r)
+    {
+      check_vectors(members[r], dsts[r], srcs[r]);
+      if (!members[r]->group)
+        throw std::runtime_error("gls_dist_vmult_group: not an in-process group");
+      members[r]->cur_dst = dsts[r];
+      members[r]->cur_src = srcs[r];
+    }
+  for (int r = 0; r < n; ++r)
+    pack(members[r], srcs[r], s);
+  for (int r = 0; r < n; ++r)
+    {
+      glsOp_ *op = members[r]->op;
+      gls::brick_launch(op, gls::op_vmult_mode(op), dsts[r], srcs[r], 0, op->n_interior_bricks,
+                        gls::BRICK_RUN, s);
+    }
+  for (int r = 0; r < n; ++r)
+    local_import(members[r], s);
+  for (int r = 0; r < n; ++r)
+    {
+      glsOp_ *op = members[r]->op;
+      gls::brick_launch(op, gls::op_vmult_mode(op), dsts[r], srcs[r], op->n_interior_bricks,
+                        op->n_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE, s);
+    }
+  for (int r = 0; r < n; ++r)
+    local_export(members[r], s);
+  for (int r = 0; r < n; ++r)
+    unpack(members[r], dsts[r], s);
+  for (int r = 0; r < n; ++r)
+    zero_ghosts(members[r], dsts[r], s);
+  GLS_CATCH
+}
+
+glsStatus
+gls_dist_interior_bricks(glsDist d, int64_t *n_interior, int64_t *n_total)
+{
+  GLS_TRY
+  if (!d)
+    throw std::runtime_error("gls_dist_interior_bricks: null argument");
+  if (n_interior)
+    *n_interior = d->op->n_interior_bricks;
+  if (n_total)
+    *n_total = d->op->n_bricks;
+  GLS_CATCH
+}
+
+} // extern "C"

@@ -180,15 +180,31 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
     n_split = 0;
   n_split = std::max<int64_t>(0, std::min(n_split, nb_full));
   const int64_t nb = nb_full + n_split;
+  // brick order: bricks that read no ghost node first, then the ones that
+  // do, so a partitioned vmult runs the former while the ghost import is in
+  // flight (deal.II's overlap of update_ghost_values with interior cells)
+  std::vector<int64_t> order;
+  order.reserve((size_t)nb_full);
+  std::vector<char> ghosted((size_t)nb_full, 0);
+  for (int64_t b = 0; b < nb_full; ++b)
+    for (int64_t j = 0; j < cpb * nq && !ghosted[b]; ++j)
+      ghosted[b] = d->cell_nodes[b * cpb * nq + j] >= (uint64_t)d->n_owned_nodes;
+  for (int pass = 0; pass < 2; ++pass)
+    for (int64_t b = 0; b < nb_full; ++b)
+      if (ghosted[b] == pass)
+        order.push_back(b);
   std::vector<uint32_t> bcell0((size_t)nb), bncell((size_t)nb);
   for (int64_t b = 0; b < nb_full - n_split; ++b)
-    bcell0[b] = (uint32_t)(b * cpb), bncell[b] = (uint32_t)cpb;
+    bcell0[b] = (uint32_t)(order[b] * cpb), bncell[b] = (uint32_t)cpb;
   for (int64_t h = 0; h < 2 * n_split; ++h)
     {
       const int64_t b = nb_full - n_split + h;
-      bcell0[b] = (uint32_t)((nb_full - n_split + h / 2) * cpb + (h % 2) * (cpb / 2));
+      bcell0[b] = (uint32_t)(order[nb_full - n_split + h / 2] * cpb + (h % 2) * (cpb / 2));
       bncell[b] = (uint32_t)(cpb / 2);
     }
+  int64_t n_interior = 0;
+  while (n_interior < nb_full - n_split && !ghosted[order[n_interior]])
+    ++n_interior;
   std::vector<uint32_t> bnodes((size_t)nb * L, UINT32_MAX);
   for (int64_t b = 0; b < nb; ++b)
     for (int64_t lc = 0; lc < (int64_t)bncell[b]; ++lc)
@@ -305,6 +321,7 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
   op->bx = bx, op->by = by, op->bz = bz;
   op->L = L, op->Lx = Lx, op->Ly = Ly;
   op->n_bricks = nb;
+  op->n_interior_bricks = n_interior;
   op->n_slots  = slot;
   op->n_shared = (int64_t)shared_nodes.size();
   op->brick_cell0 = bcell0;
@@ -528,9 +545,12 @@ struct Impl
     hipLaunchKernelGGL(kernel, dim3((unsigned)g), dim3(BLOCK), lds, s, a);
   }
 
-  // brick kernel + shared-node reduction: dst fully (over)written
+  // brick kernel over work units [b0, b1) (what & BRICK_RUN) and the
+  // shared-node reduction (what & BRICK_REDUCE); both over all units: dst
+  // fully (over)written
   static void
-  brick(const glsOp_ *op, int mode, void *dst, const void *src, hipStream_t s)
+  brick(const glsOp_ *op, int mode, void *dst, const void *src, int64_t b0, int64_t b1,
+        int what, hipStream_t s)
   {
     if constexpr (BrickLattice<dim, k>::fits)
       {
@@ -549,8 +569,8 @@ struct Impl
         a.dst           = (T *)dst;
         a.src           = (const T *)src;
         a.partial       = (T *)op->d_partial;
-        a.brick_begin   = 0;
-        a.brick_end     = op->n_bricks;
+        a.brick_begin   = b0;
+        a.brick_end     = b1;
         a.bx            = op->bx;
         a.by            = op->by;
         a.bz            = op->bz;
@@ -572,14 +592,17 @@ struct Impl
         a.have_old_grad = (op->have_old_grad && op->prm.theta != 1.0) ? 1 : 0;
         a.sh            = make_shape<T, n>(op->basis);
         const size_t lds = BrickLDS<dim, k, T>::bytes(a.LP);
-        if (mode == MODE_NEWTON)
-          launch_persistent(k_brick<dim, k, T, MODE_NEWTON>, op->n_bricks, lds, s, a);
-        else if (mode == MODE_FIXED)
-          launch_persistent(k_brick<dim, k, T, MODE_FIXED>, op->n_bricks, lds, s, a);
-        else
-          launch_persistent(k_brick<dim, k, T, MODE_RESIDUAL>, op->n_bricks, lds, s, a);
-        HIP_THROW(hipGetLastError());
-        if (op->n_shared > 0)
+        if ((what & BRICK_RUN) && b1 > b0)
+          {
+            if (mode == MODE_NEWTON)
+              launch_persistent(k_brick<dim, k, T, MODE_NEWTON>, b1 - b0, lds, s, a);
+            else if (mode == MODE_FIXED)
+              launch_persistent(k_brick<dim, k, T, MODE_FIXED>, b1 - b0, lds, s, a);
+            else
+              launch_persistent(k_brick<dim, k, T, MODE_RESIDUAL>, b1 - b0, lds, s, a);
+            HIP_THROW(hipGetLastError());
+          }
+        if ((what & BRICK_REDUCE) && op->n_shared > 0)
           {
             const dim3 g2((unsigned)((op->n_shared * (dim + 1) + 255) / 256));
             const ReduceClasses &rc = op->reduce_classes;
@@ -675,7 +698,8 @@ select(const glsOp_ *op, ApplyFn &af, ProduceFn &pf)
     throw std::runtime_error("no kernel instantiation for this (dim, degree)");
 }
 
-using BrickFn = void (*)(const glsOp_ *, int, void *, const void *, hipStream_t);
+using BrickFn = void (*)(const glsOp_ *, int, void *, const void *, int64_t, int64_t, int,
+                         hipStream_t);
 
 template <typename T>
 BrickFn
@@ -732,6 +756,26 @@ init_dst(const glsOp_ *op, void *dst, const void *src, hipStream_t s)
 }
 
 } // namespace
+
+namespace gls
+{
+// the pieces of vmult dist.hip orchestrates around the ghost exchange
+void
+brick_launch(const glsOp_ *op, int mode, void *dst, const void *src, int64_t b0, int64_t b1,
+             int what, hipStream_t s)
+{
+  BrickFn f = select_brick(op);
+  if (!f)
+    throw std::runtime_error("no brick kernel for this (dim, degree)");
+  f(op, mode, dst, src, b0, b1, what, s);
+}
+
+int
+op_vmult_mode(const glsOp_ *op)
+{
+  return vmult_mode(op);
+}
+} // namespace gls
 
 // ------------------------------------------------------------ C-ABI
 extern "C" {
@@ -1142,7 +1186,7 @@ gls_op_vmult(glsOp op, void *dst, const void *src, void *stream)
   select(op, af, pf);
   hipStream_t s = (hipStream_t)stream;
   if (op->use_brick)
-    select_brick(op)(op, vmult_mode(op), dst, src, s);
+    select_brick(op)(op, vmult_mode(op), dst, src, 0, op->n_bricks, BRICK_RUN | BRICK_REDUCE, s);
   else
     {
       init_dst(op, dst, src, s);
@@ -1164,7 +1208,8 @@ gls_op_evaluate_residual(glsOp op, void *dst, const void *src, void *stream)
   select(op, af, pf);
   hipStream_t s = (hipStream_t)stream;
   if (op->use_brick)
-    select_brick(op)(op, MODE_RESIDUAL, dst, src, s);
+    select_brick(op)(op, MODE_RESIDUAL, dst, src, 0, op->n_bricks, BRICK_RUN | BRICK_REDUCE,
+                     s);
   else
     {
       HIP_THROW(hipMemsetAsync(dst, 0, (size_t)op->n_dofs * op->tsize(), s));

@@ -41,6 +41,7 @@ struct glsOp_
   bool      use_brick = false;
   int       bx = 1, by = 1, bz = 1, L = 0, Lx = 0, Ly = 0;
   int64_t   n_bricks = 0, n_slots = 0, n_shared = 0;
+  int64_t   n_interior_bricks = 0; // leading work units that read no ghost node
   uint32_t *d_brick_nodes  = nullptr;
   uint32_t *d_brick_target = nullptr;
   uint32_t *d_shared_nodes = nullptr;

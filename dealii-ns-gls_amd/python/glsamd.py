@@ -30,6 +30,8 @@ EXPORTS = [
     "gls_op_geometry_counts", "gls_op_vmult_bytes", "gls_mg_create", "gls_mg_destroy",
     "gls_mg_setup", "gls_mg_get_relaxation", "gls_mg_vcycle", "gls_mg_prolongate_add",
     "gls_mg_restrict_add", "gls_mg_interpolate", "gls_mg_smooth", "gls_last_error",
+    "gls_dist_unique_id", "gls_dist_create", "gls_dist_destroy", "gls_dist_vmult",
+    "gls_dist_vmult_group", "gls_dist_interior_bricks",
 ]
 
 
@@ -51,6 +53,13 @@ class MGDesc(C.Structure):
     _fields_ = [("n_levels", C.c_int), ("smoothing_n_iterations", C.c_int),
                 ("smoothing_eig_n_iterations", C.c_int), ("smoothing_range", C.c_double),
                 ("coarse_n_iterations", C.c_int), ("outer_precision", C.c_int)]
+
+
+class DistDesc(C.Structure):
+    _fields_ = [("rank", C.c_int), ("world", C.c_int), ("nccl_id", C.c_void_p),
+                ("group", C.c_void_p), ("n_peers", C.c_int), ("peers", C.c_void_p),
+                ("send_count", C.c_void_p), ("send_nodes", C.c_void_p),
+                ("recv_begin", C.c_void_p), ("recv_count", C.c_void_p)]
 
 
 def lib_path():
@@ -93,6 +102,12 @@ def lib():
         for f in ("gls_mg_prolongate_add", "gls_mg_restrict_add", "gls_mg_interpolate"):
             getattr(L, f).argtypes = [vp, C.c_int, vp, vp, vp]
         L.gls_mg_smooth.argtypes = [vp, C.c_int, vp, vp, C.c_int, vp]
+        L.gls_dist_unique_id.argtypes = [vp]
+        L.gls_dist_create.argtypes = [vp, C.POINTER(DistDesc), C.POINTER(vp)]
+        L.gls_dist_destroy.argtypes = [vp]
+        L.gls_dist_vmult.argtypes = [vp, vp, vp, vp]
+        L.gls_dist_vmult_group.argtypes = [vp, vp, vp, C.c_int, vp]
+        L.gls_dist_interior_bricks.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)]
         L.gls_last_error.restype = C.c_char_p
         _lib = L
     return _lib
@@ -239,6 +254,72 @@ class NavierStokesOperator:
 
     def vmult_bytes(self):
         return lib().gls_op_vmult_bytes(self.h)
+
+
+def dist_unique_id():
+    """128-byte RCCL unique id (one rank creates it, all ranks use it)."""
+    b = (C.c_char * 128)()
+    _check(lib().gls_dist_unique_id(C.cast(b, C.c_void_p)))
+    return bytes(b)
+
+
+class PartitionedOperator:
+    """The rank-local half of a partitioned NavierStokesOperator: ghost
+    import / compress(add) over RCCL (nccl_id given) or inside an in-process
+    group of ranks on one device (nccl_id None, `group` = a member created
+    before).  op: the rank-local NavierStokesOperator; recv blocks: per peer
+    the [begin, begin + count) local ghost nodes it owns; send_nodes: per peer
+    the owned local nodes that are ghosts there, in the peer's ghost order."""
+
+    def __init__(self, op, rank, world, peers, send_nodes, recv_blocks, nccl_id=None,
+                 group=None):
+        self.op = op
+        peers = [int(q) for q in peers]
+        self._keep = [np.ascontiguousarray(peers, dtype=np.int32),
+                      np.ascontiguousarray([len(send_nodes[q]) for q in peers], dtype=np.int64),
+                      np.ascontiguousarray(np.concatenate([np.asarray(send_nodes[q], np.int64)
+                                                           for q in peers])
+                                           if peers else np.zeros(0), dtype=np.uint32),
+                      np.ascontiguousarray([recv_blocks[q][0] for q in peers], dtype=np.int64),
+                      np.ascontiguousarray([recv_blocks[q][1] for q in peers], dtype=np.int64)]
+        k = self._keep
+        idb = None
+        if nccl_id is not None:
+            idb = (C.c_char * 128).from_buffer_copy(bytes(nccl_id))
+            self._keep.append(idb)
+        d = DistDesc(rank, world, None if idb is None else C.cast(idb, C.c_void_p),
+                     None if group is None else group.h, len(peers), k[0].ctypes.data,
+                     k[1].ctypes.data, k[2].ctypes.data, k[3].ctypes.data, k[4].ctypes.data)
+        h = C.c_void_p()
+        _check(lib().gls_dist_create(op.h, C.byref(d), C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().gls_dist_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def vmult(self, dst, src):
+        _check(lib().gls_dist_vmult(self.h, _ptr(dst), _ptr(src), _stream()))
+        return dst
+
+    def interior_bricks(self):
+        a, b = C.c_int64(), C.c_int64()
+        _check(lib().gls_dist_interior_bricks(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    @staticmethod
+    def vmult_group(members, dsts, srcs):
+        n = len(members)
+        hs = (C.c_void_p * n)(*[m.h.value for m in members])
+        ds = (C.c_void_p * n)(*[d.data_ptr() for d in dsts])
+        ss = (C.c_void_p * n)(*[s.data_ptr() for s in srcs])
+        _check(lib().gls_dist_vmult_group(C.cast(hs, C.c_void_p), C.cast(ds, C.c_void_p),
+                                          C.cast(ss, C.c_void_p), n, _stream()))
+        return dsts
 
 
 class Multigrid:

@@ -19,9 +19,16 @@ owned in mesh order, ghosts grouped by owner so every import lands in one
 contiguous block.  The partition is computed identically on every rank from
 the replicated mesh (no exchange of the plan).
 
-The per-rank logic is split into phases (pack / unpack / local apply / fix)
-so the same code runs (a) over a real process group and (b) in-process over a
-list of ranks (`LocalGroup`) for single-GPU tests of the partitioned path.
+Two transports:
+  * native (the product path on GPUs): libglsamd.so's gls_dist_* — pack
+    kernel, RCCL send/recv of the ghost blocks on a communication stream
+    while the interior bricks (those reading no ghost node) run, boundary
+    bricks after the import event, export-add over RCCL, one unpack-add
+    kernel.  In-process groups (LocalGroup, one device) run the same phases
+    with device copies in place of RCCL.
+  * torch.distributed point-to-point (batch_isend_irecv) with the per-rank
+    phases below (pack / unpack / local apply / fix): the CPU/gloo tests with
+    the oracle engine and the cross-check of the native path.
 """
 from __future__ import annotations
 
@@ -130,6 +137,18 @@ class LocalMesh:
 
 
 # ------------------------------------------------------------------ engines
+def recv_blocks(part: Partition):
+    """Per owner q: (first local ghost node, count) — ghosts of one owner are
+    one contiguous block of the local layout."""
+    out = {}
+    for q, idx in part.recv_nodes.items():
+        idx = np.asarray(idx, dtype=np.int64)
+        if len(idx) and not np.array_equal(idx, np.arange(idx[0], idx[0] + len(idx))):
+            raise ValueError("ghosts of one owner are not contiguous")
+        out[q] = (int(idx[0]) if len(idx) else part.n_owned, len(idx))
+    return out
+
+
 class GpuEngine:
     """Local operator = libglsamd.so (the product path)."""
 
@@ -154,6 +173,15 @@ class GpuEngine:
 
     def identity_rows(self, dst, src):
         self.op.apply_identity_rows(dst, src)
+
+    def partitioned(self, part, nccl_id=None, group=None):
+        import glsamd
+        peers = sorted(set(part.recv_nodes) | set(part.send_nodes))
+        send = {q: part.send_nodes.get(q, np.zeros(0, np.int64)) for q in peers}
+        rb = recv_blocks(part)
+        recv = {q: rb.get(q, (part.n_owned, 0)) for q in peers}
+        return glsamd.PartitionedOperator(self.op, part.rank, part.world, peers, send, recv,
+                                          nccl_id=nccl_id, group=group)
 
 
 class OracleEngine:
@@ -267,12 +295,28 @@ class DistributedOperator:
     distributed operator (set_linearization_point, set_previous_solution,
     vmult), on rank-local [owned | ghost] vectors."""
 
-    def __init__(self, mesh, cmask, precision, dist, rank, world, engine="gpu"):
+    def __init__(self, mesh, cmask, precision, dist, rank, world, engine="gpu", native=None):
         self.dist, self.rank, self.world = dist, rank, world
         self.parts = build_partitions(mesh, world)
         self.r = RankOperator(mesh, cmask, self.parts[rank], precision, engine)
         self.n_local_cells = self.r.part.n_cells
         self.n_global_dofs = mesh.n_dofs
+        self.native = None
+        if native is None:
+            native = engine == "gpu"
+        if native:
+            self.native = self.r.eng.partitioned(self.r.part, nccl_id=self._shared_id())
+
+    def _shared_id(self):
+        """RCCL unique id from rank 0, broadcast over the torch process group."""
+        import torch
+        import glsamd
+        dev = "cuda" if self.dist.get_backend() == "nccl" else "cpu"
+        t = torch.zeros(128, dtype=torch.uint8, device=dev)
+        if self.rank == 0:
+            t.copy_(torch.frombuffer(bytearray(glsamd.dist_unique_id()), dtype=torch.uint8))
+        self.dist.broadcast(t, 0)
+        return bytes(t.cpu().numpy().tobytes())
 
     @property
     def op(self):
@@ -321,6 +365,11 @@ class DistributedOperator:
         return v
 
     def vmult(self, dst, src):
+        if self.native is not None:
+            return self.native.vmult(dst, src)
+        return self.vmult_p2p(dst, src)
+
+    def vmult_p2p(self, dst, src):
         self.update_ghost_values(src)
         self.r.eng.local_vmult(dst, src)
         self.compress_add(dst)
@@ -342,10 +391,16 @@ class LocalGroup:
     with direct buffer delivery instead of point-to-point messages.  Used to
     test the partitioned operator on a single GPU."""
 
-    def __init__(self, mesh, cmask, world, precision="f64", engine="gpu"):
+    def __init__(self, mesh, cmask, world, precision="f64", engine="gpu", native=False):
         self.parts = build_partitions(mesh, world)
         self.ranks = [RankOperator(mesh, cmask, p, precision, engine) for p in self.parts]
         self.n_global_dofs = mesh.n_dofs
+        self.native = None
+        if native:
+            self.native = []
+            for r in self.ranks:
+                g = self.native[0] if self.native else None
+                self.native.append(r.eng.partitioned(r.part, group=g))
 
     def _deliver(self, packs):
         for r, (sends, _) in enumerate(packs):
@@ -381,6 +436,9 @@ class LocalGroup:
         return vs
 
     def vmult(self, dsts, srcs):
+        if self.native is not None:
+            import glsamd
+            return glsamd.PartitionedOperator.vmult_group(self.native, dsts, srcs)
         self.update_ghost_values(srcs)
         for r, d, s in zip(self.ranks, dsts, srcs):
             r.eng.local_vmult(d, s)

@@ -191,6 +191,44 @@ glsStatus gls_mg_interpolate(glsMG mg, int level, void *dst_coarse,
 glsStatus gls_mg_smooth(glsMG mg, int level, void *x, const void *b,
                         int zero_initial_guess, void *stream);
 
+/* ---- partitioned operator: one rank per GPU, ghost exchange over RCCL
+ * (deal.II update_ghost_values / compress(add) inside
+ * MatrixFree::cell_loop, operator_ns.cc:702-721).  The local operator is a
+ * glsOp built on the rank-local mesh with n_owned_nodes < n_nodes, ghosts
+ * grouped by owner ([owned | ghosts of owner q0 | ghosts of q1 | ...]). */
+typedef struct glsDist_ *glsDist;
+typedef struct
+{
+  int             rank, world;
+  const void     *nccl_id;    /* 128-byte ncclUniqueId shared by all ranks
+                                 (gls_dist_unique_id on one rank); NULL: an
+                                 in-process group on one device (tests)      */
+  glsDist         group;      /* in-process group: any member created before,
+                                 NULL for the first                          */
+  int             n_peers;
+  const int      *peers;      /* [n_peers] peer ranks                        */
+  const int64_t  *send_count; /* [n_peers] owned nodes that are ghosts on the
+                                 peer                                        */
+  const uint32_t *send_nodes; /* concatenated, per peer in the peer's ghost
+                                 order (local node ids)                      */
+  const int64_t  *recv_begin; /* [n_peers] first local node of the ghost
+                                 block the peer owns                         */
+  const int64_t  *recv_count; /* [n_peers] its length                        */
+} glsDistDesc;
+
+glsStatus gls_dist_unique_id(void *id_out /* 128 bytes */);
+glsStatus gls_dist_create(glsOp op, const glsDistDesc *desc, glsDist *out);
+void      gls_dist_destroy(glsDist d);
+/* vmult of the partitioned operator on the rank-local [owned | ghost]
+ * vectors: src's ghost block is overwritten by the import (as deal.II's
+ * update_ghost_values), dst's ghost block is zero on return (compress) */
+glsStatus gls_dist_vmult(glsDist d, void *dst, void *src, void *stream);
+/* the same for all members of an in-process group, phases in lockstep */
+glsStatus gls_dist_vmult_group(glsDist const *members, void *const *dsts,
+                               void *const *srcs, int n, void *stream);
+glsStatus gls_dist_interior_bricks(glsDist d, int64_t *n_interior,
+                                   int64_t *n_total);
+
 const char *gls_last_error(void);
 
 #ifdef __cplusplus

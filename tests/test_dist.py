@@ -115,14 +115,63 @@ def test_gloo_world2(name, n_ref):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,n_ref", CASES)
 @pytest.mark.parametrize("world", [2, 4])
-def test_local_group_gpu(name, n_ref, world):
+@pytest.mark.parametrize("native", [False, True])
+def test_local_group_gpu(name, n_ref, world, native):
+    """native: libglsamd's gls_dist phases (pack, interior bricks, import,
+    boundary bricks + reduce, export, unpack-add) with in-process copies in
+    place of RCCL; otherwise the torch-side exchange around gls_op_vmult."""
     import torch
     c = deck_case(name, n_ref)
-    g = glsdist.LocalGroup(c.mesh, c.cmask, world, engine="gpu")
+    g = glsdist.LocalGroup(c.mesh, c.cmask, world, engine="gpu", native=native)
     g.setup(c.params, c.u_star, c.hist, c.weights)
     srcs = g.scatter(c.src)
     dsts = [r.new_vector() for r in g.ranks]
+    if native:
+        for r, sv in zip(g.ranks, srcs):  # ghosts must come from the import
+            sv[r.n_owned_dofs:].zero_()
     g.vmult(dsts, srcs)
     torch.cuda.synchronize()
     out = g.gather(dsts).cpu().numpy()
     assert rel_err(out, _oracle_ref(c)) < 1e-12
+    if native:
+        for r, sv, dv in zip(g.ranks, srcs, dsts):
+            assert torch.equal(sv.cpu(), torch.from_numpy(c.src)[r.global_dofs.cpu()])
+            assert not dv[r.n_owned_dofs:].any()  # compress zeroes the ghosts
+        n_int = [m.interior_bricks() for m in g.native]
+        assert all(0 <= a <= b for a, b in n_int)
+        if world == 2 and name.startswith("input_hoffmann"):
+            assert all(a > 0 for a, _ in n_int)  # something to overlap with
+
+
+@pytest.mark.gpu
+def test_rccl_world1_native():
+    """The RCCL path end to end on one GPU: torch.distributed (nccl = RCCL)
+    world 1, the RCCL unique id broadcast, ncclCommInitRank inside
+    libglsamd, gls_dist_vmult (pack / interior / event wait / boundary /
+    reduce / export / unpack with no peers) against gls_op_vmult."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        c = deck_case("input_hoffmann_3D_Re3900.json", 1)
+        op = glsdist.DistributedOperator(c.mesh, c.cmask, "f64", dist, 0, 1)
+        assert op.native is not None
+        op.setup(c.params, c.u_star, c.hist, c.weights)
+        src = op.scatter_global(c.src)
+        dst = op.new_vector()
+        op.vmult(dst, src)
+        ref = op.new_vector()
+        op.op.vmult(ref, src)
+        torch.cuda.synchronize()
+        # equal up to the LDS-atomic summation order of the brick kernel
+        assert rel_err(dst.cpu().numpy(), ref.cpu().numpy()) < 1e-14
+        assert rel_err(dst.cpu().numpy(), _oracle_ref(c)) < 1e-12
+    finally:
+        dist.destroy_process_group()
