@@ -263,25 +263,18 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
   const int cy       = r.active ? (lcell / a.bx) % a.by : 0;
   const int cz       = r.active ? lcell / (a.bx * a.by) : 0;
   r.li = (cx * k + pa[0]) + a.PLx * ((cy * k + pa[1]) + a.PLy * (cz * k + pa[2]));
+  // inactive lanes (the 64 % nq left-over lanes, cells past the brick's
+  // end) load the brick's first cell instead of zero-filling ~30 registers
+  // per round: finite values, and JxW = 0 below keeps them out of the sums
+  if (!r.active)
+    lcell = 0;
   const int64_t cell = cell0 + lcell;
   const int64_t nqc  = a.n_cells * nq;
-  r.JxW = r.d1 = r.d2 = 0;
 #pragma unroll
   for (int i = 0; i < dim; ++i)
-    {
 #pragma unroll
-      for (int e = 0; e < dim; ++e)
-        {
-          r.inv[i][e] = 0;
-          r.GU[i][e]  = 0;
-        }
-      r.U[i] = r.GP[i] = r.UT[i] = 0;
-    }
-#pragma unroll
-  for (int i = 0; i < LaneData<dim, T, MODE>::NOLD; ++i)
-    r.oldg[i] = 0;
-  if (!r.active)
-    return;
+    for (int e = 0; e < dim; ++e)
+      r.inv[i][e] = 0;
   // geometry (MatrixFree-style compressed: Cartesian per cell, else per q)
   if (general)
     {
@@ -303,6 +296,8 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
         r.inv[i][i] = a.geo_cart[i * a.n_cells + cell];
       r.JxW = a.geo_cart[dim * a.n_cells + cell] * w;
     }
+  if (!r.active)
+    r.JxW = 0;
   // per-q tables (operator_ns.h:120-132): the round's CPW cells form one
   // chunk, each 16-byte field group of it one contiguous wave load; the
   // groups a mode reads are fixed at compile time (fields a runtime flag
@@ -340,6 +335,9 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
       for (int e = 0; e < dim; ++e)
         r.GU[d][e] = tf[F::GU + d * dim + e];
     }
+#pragma unroll
+  for (int i = 0; i < LaneData<dim, T, MODE>::NOLD; ++i)
+    r.oldg[i] = 0;
   if (R && a.have_old_grad)
     {
       const int64_t tq = qindex<dim, n>(cell, p, a.n_cells);

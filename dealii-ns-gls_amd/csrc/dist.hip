@@ -455,6 +455,13 @@ gls_dist_vmult(glsDist d, void *dst, void *src, void *stream)
   hipStream_t   s    = (hipStream_t)stream;
   glsOp_       *op   = d->op;
   const int     mode = gls::op_vmult_mode(op);
+  if (d->peers.empty()) // one rank: nothing to exchange
+    {
+      gls::brick_launch(op, mode, dst, src, 0, op->n_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE,
+                        s);
+      zero_ghosts(d, dst, s);
+      return 0;
+    }
   // import (comm stream) || interior bricks (s)
   pack(d, src, s);
   HIP_THROW(hipEventRecord(d->ev_packed, s));
