@@ -805,6 +805,52 @@ __global__ void __launch_bounds__(256)
                       const T *__restrict__ partial, const uint32_t *__restrict__ nodes,
                       const ReduceClasses rc, int64_t n_shared)
 {
+  // 16-byte packs when a node's row is whole packs (nc = 4): one thread per
+  // (node, pack), vector loads and stores
+  using V            = typename Pack<T>::V;
+  constexpr int W    = Pack<T>::W;
+  constexpr int NPK  = nc % W == 0 ? nc / W : 0;
+  if constexpr (NPK > 0)
+    {
+      const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+      if (gid >= n_shared * NPK)
+        return;
+      const uint32_t s  = (uint32_t)(gid / NPK);
+      const int      kp = (int)(gid - (int64_t)s * NPK);
+      int            k  = 0;
+#pragma unroll
+      for (int j = 1; j < ReduceClasses::MAX; ++j)
+        if (j < rc.n && s >= rc.first[j])
+          k = j;
+      const uint32_t m      = rc.mult[k];
+      const uint32_t b      = rc.slot0[k] + (s - rc.first[k]) * m;
+      const uint32_t packed = nodes[s];
+      const V       *pp     = reinterpret_cast<const V *>(partial) + kp;
+      V              sum    = {};
+      uint32_t       i      = 0;
+      for (; i + 4 <= m; i += 4)
+        {
+          const V x0 = pp[(size_t)(b + i) * NPK], x1 = pp[(size_t)(b + i + 1) * NPK];
+          const V x2 = pp[(size_t)(b + i + 2) * NPK], x3 = pp[(size_t)(b + i + 3) * NPK];
+          sum += (x0 + x1) + (x2 + x3);
+        }
+      if (i + 2 <= m)
+        {
+          const V x0 = pp[(size_t)(b + i) * NPK], x1 = pp[(size_t)(b + i + 1) * NPK];
+          sum += x0 + x1;
+          i += 2;
+        }
+      if (i < m)
+        sum += pp[(size_t)(b + i) * NPK];
+      const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
+      if (cm)
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if ((cm >> (kp * W + w)) & 1)
+            sum[w] = R ? T(0) : src[(size_t)node * nc + kp * W + w];
+      reinterpret_cast<V *>(dst)[(size_t)node * NPK + kp] = sum;
+      return;
+    }
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= n_shared * nc)
     return;

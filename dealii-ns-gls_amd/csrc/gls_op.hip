@@ -605,13 +605,17 @@ struct Impl
         if ((what & BRICK_REDUCE) && op->n_shared > 0)
           {
             const dim3 g2((unsigned)((op->n_shared * (dim + 1) + 255) / 256));
+            // the class kernel runs one thread per 16-byte pack when nc = 4
+            const int  npk = (dim + 1) % (16 / (int)sizeof(T)) == 0 ?
+                               (dim + 1) / (16 / (int)sizeof(T)) : dim + 1;
+            const dim3 g3((unsigned)((op->n_shared * npk + 255) / 256));
             const ReduceClasses &rc = op->reduce_classes;
             if (rc.n > 0 && mode == MODE_RESIDUAL)
-              hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, true>), g2, dim3(256), 0, s,
+              hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, true>), g3, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)op->d_partial,
                                  op->d_shared_nodes, rc, op->n_shared);
             else if (rc.n > 0)
-              hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, false>), g2, dim3(256), 0, s,
+              hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, false>), g3, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)op->d_partial,
                                  op->d_shared_nodes, rc, op->n_shared);
             else if (mode == MODE_RESIDUAL)
