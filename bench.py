@@ -63,6 +63,69 @@ def cpu_baseline(case_mesh, cmask, params, weights, u_star, hist, src, n_dofs, b
                        f"{el:.1f} s")
 
 
+def _timed_vmults(op, dst, src, reps, flush=None):
+    """Median per-vmult duration (ms) with HIP events on the launch stream
+    (torch's current stream); `flush` runs between reps, outside the events."""
+    import torch
+    t = []
+    for _ in range(reps):
+        if flush is not None:
+            flush()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        op.vmult(dst, src)
+        e1.record()
+        torch.cuda.synchronize()
+        t.append(e0.elapsed_time(e1))
+    return float(np.median(t))
+
+
+def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src, reps=50):
+    """The rest of SURVEY §8d's timing protocol, beside the headline line:
+    cold (MALL flushed by a 1 GiB scratch write between reps) vs warm FP64
+    at r2, the FP32 level operator (the smoother's hot path) on the same
+    mesh, and the HBM-bound r+1 mesh (Turek-3D size at r2 = 3).  Medians of
+    `reps` event-timed vmults after 5 warm-ups."""
+    import torch
+    import glsamd
+    out = {}
+    scratch = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    flush = lambda: scratch.fill_(1)  # noqa: E731
+
+    def line(op, dst, src, fl=None, prec="f64"):
+        for _ in range(5):
+            op.vmult(dst, src)
+        ms = _timed_vmults(op, dst, src, reps, fl)
+        b = op.vmult_bytes()
+        return {"ms": ms, "dofs_per_s": op.m() / (ms * 1e-3), "algorithmic_bytes": b,
+                "roofline_frac": b / (ms * 1e-3) / HBM_PEAK, "dtype": prec}
+
+    out[f"r{n_ref}_f64_warm"] = line(hot_op, hot_dst, hot_src)
+    out[f"r{n_ref}_f64_cold"] = line(hot_op, hot_dst, hot_src, flush)
+
+    def build(m, cm, prec):
+        u_star = gi.linearization_point(m.n_nodes, m.dim, d.u_max)
+        op = glsamd.NavierStokesOperator(m, cm, prec)
+        op.set_parameters(**params)
+        op.set_linearization_point(u_star)
+        if params["order"] > 0:
+            op.set_previous_solution(gi.history(u_star, params["order"]), weights)
+        src = op._dev(gi.src_vector(m.n_dofs))
+        return op, op.initialize_dof_vector(), src
+
+    op32, dst32, src32 = build(mesh, cmask, "f32")
+    out[f"r{n_ref}_f32_level_warm"] = line(op32, dst32, src32, prec="f32")
+    del op32, dst32, src32
+    vel, p, slip = d.boundary_descriptor()
+    m3 = d.mesh(n_ref + 1)
+    op3, dst3, src3 = build(m3, m3.constraint_mask(vel, p, slip), "f64")
+    out[f"r{n_ref + 1}_f64_warm"] = line(op3, dst3, src3)
+    out[f"r{n_ref + 1}_f64_warm"]["cells"] = m3.n_cells
+    del op3, dst3, src3, scratch
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -71,6 +134,8 @@ def main():
     ap.add_argument("--nref", type=int, default=None)
     ap.add_argument("--precision", default="f64")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-companions", action="store_true",
+                    help="skip the cold / FP32-level / r+1 companion lines")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--brick", default=None,
                     help="cells per brick 'bx,by,bz' (a sub-brick of the mesh order)")
@@ -208,6 +273,12 @@ def main():
             wl = tj.get("workload", {})
             if wl.get("nref") == n_ref and wl.get("precision") == args.precision:
                 traffic = tj.get("bytes_per_launch")
+        comp = None
+        if not args.no_companions and world == 1 and kernel_fn is not None and not use_dist:
+            try:
+                comp = companions(d, mesh, cmask, params, weights, n_ref, op, dst, src)
+            except Exception as e:  # reported beside the headline, never fatal
+                comp = {"error": str(e)}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
@@ -240,6 +311,7 @@ def main():
                                    "gls::k_shared_reduce_cls (both inside the events)",
                          "kernel_ms": kernel_ms, "algorithmic_bytes": bytes_per_vmult},
             "cpu_baseline": cpu,
+            "companions": comp,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -1,0 +1,249 @@
+// krylov.hip — device-resident right-preconditioned restarted GMRES
+// (SURVEY §8f rank 2): LinearSolverGMRES::solve, solver_l.cc:45-74, over
+// deal.II SolverGMRES(max_n_tmp_vectors = 30, right_preconditioning = true).
+//
+// Every vector (the Krylov basis V, the preconditioned direction, the
+// solution) stays in HBM; per iteration only the j+1 Hessenberg entries and a
+// norm cross to the host (what deal.II's MPI_Allreduce of the dots returns on
+// every rank).  Orthogonalisation is classical Gram-Schmidt with one
+// re-orthogonalisation (CGS2): two GEMVs over the contiguous basis per
+// iteration instead of j+1 dependent dot/axpy pairs — the same projector as
+// deal.II's modified Gram-Schmidt in exact arithmetic, and the stable choice
+// for a streaming device.  The basis GEMVs are plain library GEMVs (rocBLAS);
+// the operator apply and the V-cycle are this library's own kernels.
+#include "../../include/gls_op.h"
+#include "common.h"
+#include "op_internal.h"
+
+#include <rocblas/rocblas.h>
+
+#include <cmath>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace
+{
+#define RB_THROW(expr)                                                                       \
+  do                                                                                         \
+    {                                                                                        \
+      const rocblas_status s_ = (expr);                                                      \
+      if (s_ != rocblas_status_success)                                                      \
+        throw std::runtime_error(std::string(#expr) + ": " + rocblas_status_to_string(s_));   \
+    }                                                                                        \
+  while (0)
+
+struct DevBuf
+{
+  void *p = nullptr;
+  explicit DevBuf(size_t bytes)
+  {
+    HIP_THROW(hipMalloc(&p, bytes > 0 ? bytes : 8));
+  }
+  ~DevBuf()
+  {
+    (void)hipFree(p);
+  }
+  double *
+  d() const
+  {
+    return (double *)p;
+  }
+};
+
+struct Handle
+{
+  rocblas_handle h = nullptr;
+  explicit Handle(hipStream_t s)
+  {
+    RB_THROW(rocblas_create_handle(&h));
+    RB_THROW(rocblas_set_stream(h, s));
+    RB_THROW(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host));
+  }
+  ~Handle()
+  {
+    (void)rocblas_destroy_handle(h);
+  }
+};
+
+// r = b - r (r holds A x on entry)
+__global__ void
+k_residual(double *__restrict__ r, const double *__restrict__ b, int64_t n)
+{
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n)
+    r[i] = b[i] - r[i];
+}
+
+dim3
+grid1(int64_t n)
+{
+  return dim3((unsigned)((n + 255) / 256));
+}
+
+void
+check(glsStatus st, const char *what)
+{
+  if (st != 0)
+    throw std::runtime_error(std::string(what) + ": " + gls_last_error());
+}
+
+} // namespace
+
+extern "C" glsStatus
+gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const void *b_,
+                glsGMRESResult *result, void *stream)
+{
+  GLS_TRY
+  if (!op || !desc || !x_ || !b_)
+    throw std::runtime_error("gls_gmres_solve: null argument");
+  if (op->prec != GLS_F64)
+    throw std::runtime_error("gls_gmres_solve: the outer operator must be FP64 "
+                             "(LinearSolverGMRES works on VectorType<double>)");
+  if (op->n_owned_dofs != op->n_dofs)
+    throw std::runtime_error("gls_gmres_solve: single-domain operators only (a partitioned "
+                             "solve needs all-reduced dots)");
+  if (desc->max_n_tmp_vectors < 3)
+    throw std::runtime_error("gls_gmres_solve: max_n_tmp_vectors must be >= 3");
+  hipStream_t    s = (hipStream_t)stream;
+  const int64_t  n = op->n_dofs;
+  // deal.II SolverGMRES restarts after max_n_tmp_vectors - 2 iterations
+  const int      m = desc->max_n_tmp_vectors - 2;
+  double        *x = (double *)x_;
+  const double  *b = (const double *)b_;
+  Handle         hb(s);
+  rocblas_handle h = hb.h;
+  DevBuf         V((size_t)(m + 1) * n * sizeof(double)), w(n * sizeof(double)),
+    z(n * sizeof(double)), dh(2 * (m + 1) * sizeof(double));
+  auto vcol = [&](int j) { return V.d() + (size_t)j * n; };
+  auto precondition = [&](double *dst, const double *src) {
+    if (mg)
+      check(gls_mg_vcycle(mg, dst, src, s), "preconditioner vmult (gls_mg_vcycle)");
+    else
+      HIP_THROW(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+  };
+  auto nrm2 = [&](const double *v) {
+    double r = 0;
+    RB_THROW(rocblas_dnrm2(h, (rocblas_int)n, v, 1, &r));
+    return r;
+  };
+  if (n > (int64_t)0x7fffffff)
+    throw std::runtime_error("gls_gmres_solve: vector too long for 32-bit rocBLAS sizes");
+
+  // solver_l.cc:52-53: tolerance = max(rel * |b|, abs); dst = 0 (:66)
+  const double bnorm = nrm2(b);
+  const double tol   = std::max(desc->relative_tolerance * bnorm, desc->absolute_tolerance);
+  HIP_THROW(hipMemsetAsync(x, 0, n * sizeof(double), s));
+
+  std::vector<double> H((size_t)(m + 1) * m), g(m + 1), cs(m), sn(m), hc(2 * (m + 1)), y(m);
+  int    it    = 0;
+  double res   = bnorm; // x = 0: r = b
+  bool   conv  = res <= tol;
+  int    n_rst = 0;
+  // r (in column 0 of V) = b - A x
+  HIP_THROW(hipMemcpyAsync(vcol(0), b, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+  while (!conv && it < desc->max_iterations)
+    {
+      const double beta = res;
+      {
+        const double sc = 1.0 / beta;
+        RB_THROW(rocblas_dscal(h, (rocblas_int)n, &sc, vcol(0), 1));
+      }
+      std::fill(g.begin(), g.end(), 0.0);
+      g[0]   = beta;
+      int jd = 0; // columns of this cycle
+      for (int j = 0; j < m && it < desc->max_iterations; ++j)
+        {
+          // w = A M^{-1} v_j
+          precondition(z.d(), vcol(j));
+          check(gls_op_vmult(op, w.d(), z.d(), s), "operator vmult");
+          // CGS2: h = V^T w; w -= V h; twice
+          const double one = 1.0, zero = 0.0, mone = -1.0;
+          for (int pass = 0; pass < 2; ++pass)
+            {
+              double *hp = dh.d() + pass * (m + 1);
+              RB_THROW(rocblas_dgemv(h, rocblas_operation_transpose, (rocblas_int)n, j + 1, &one,
+                                     V.d(), (rocblas_int)n, w.d(), 1, &zero, hp, 1));
+              RB_THROW(rocblas_dgemv(h, rocblas_operation_none, (rocblas_int)n, j + 1, &mone,
+                                     V.d(), (rocblas_int)n, hp, 1, &one, w.d(), 1));
+            }
+          HIP_THROW(hipMemcpyAsync(hc.data(), dh.d(), 2 * (m + 1) * sizeof(double),
+                                   hipMemcpyDeviceToHost, s));
+          const double hn = nrm2(w.d()); // host pointer mode: waits for the stream
+          HIP_THROW(hipStreamSynchronize(s)); // and the D2H copy of hc
+          double      *Hj = &H[(size_t)j * (m + 1)];
+          for (int i = 0; i <= j; ++i)
+            Hj[i] = hc[i] + hc[(m + 1) + i];
+          Hj[j + 1] = hn;
+          if (hn > 0)
+            {
+              const double sc = 1.0 / hn;
+              HIP_THROW(hipMemcpyAsync(vcol(j + 1), w.d(), n * sizeof(double),
+                                       hipMemcpyDeviceToDevice, s));
+              RB_THROW(rocblas_dscal(h, (rocblas_int)n, &sc, vcol(j + 1), 1));
+            }
+          // Givens rotations on the new Hessenberg column
+          for (int i = 0; i < j; ++i)
+            {
+              const double t = cs[i] * Hj[i] + sn[i] * Hj[i + 1];
+              Hj[i + 1]      = -sn[i] * Hj[i] + cs[i] * Hj[i + 1];
+              Hj[i]          = t;
+            }
+          const double rr = std::hypot(Hj[j], Hj[j + 1]);
+          cs[j]           = rr > 0 ? Hj[j] / rr : 1.0;
+          sn[j]           = rr > 0 ? Hj[j + 1] / rr : 0.0;
+          Hj[j]           = rr;
+          Hj[j + 1]       = 0;
+          g[j + 1]        = -sn[j] * g[j];
+          g[j]            = cs[j] * g[j];
+          ++it;
+          ++jd;
+          res = std::fabs(g[j + 1]);
+          // deal.II checks the GMRES residual estimate every iteration; a
+          // lucky breakdown (hn == 0) means the estimate is exact
+          if (res <= tol || hn == 0)
+            break;
+        }
+      // y = H^{-1} g (upper triangular), x += M^{-1} V y
+      for (int i = jd - 1; i >= 0; --i)
+        {
+          double t = g[i];
+          for (int c = i + 1; c < jd; ++c)
+            t -= H[(size_t)c * (m + 1) + i] * y[c];
+          y[i] = t / H[(size_t)i * (m + 1) + i];
+        }
+      HIP_THROW(hipMemcpyAsync(dh.d(), y.data(), jd * sizeof(double), hipMemcpyHostToDevice, s));
+      {
+        const double one = 1.0, zero = 0.0;
+        RB_THROW(rocblas_dgemv(h, rocblas_operation_none, (rocblas_int)n, jd, &one, V.d(),
+                               (rocblas_int)n, dh.d(), 1, &zero, w.d(), 1));
+        precondition(z.d(), w.d());
+        RB_THROW(rocblas_daxpy(h, (rocblas_int)n, &one, z.d(), 1, x, 1));
+      }
+      conv = res <= tol;
+      if (conv || it >= desc->max_iterations)
+        break;
+      // restart: true residual r = b - A x into column 0
+      ++n_rst;
+      check(gls_op_vmult(op, vcol(0), x, s), "operator vmult");
+      hipLaunchKernelGGL(k_residual, grid1(n), dim3(256), 0, s, vcol(0), b, n);
+      HIP_THROW(hipGetLastError());
+      res  = nrm2(vcol(0));
+      conv = res <= tol;
+    }
+  HIP_THROW(hipStreamSynchronize(s));
+  if (result)
+    {
+      result->n_iterations   = it;
+      result->n_restarts     = n_rst;
+      result->initial_residual = bnorm;
+      result->final_residual = res;
+      result->tolerance      = tol;
+      result->converged      = conv ? 1 : 0;
+    }
+  if (!conv)
+    throw std::runtime_error("gls_gmres_solve: no convergence in " + std::to_string(it) +
+                             " iterations (residual " + std::to_string(res) + " > " +
+                             std::to_string(tol) + ")");
+  GLS_CATCH
+}

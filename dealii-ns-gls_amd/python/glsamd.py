@@ -62,6 +62,17 @@ class DistDesc(C.Structure):
                 ("recv_begin", C.c_void_p), ("recv_count", C.c_void_p)]
 
 
+class GMRESDesc(C.Structure):
+    _fields_ = [("max_n_tmp_vectors", C.c_int), ("max_iterations", C.c_int),
+                ("absolute_tolerance", C.c_double), ("relative_tolerance", C.c_double)]
+
+
+class GMRESResult(C.Structure):
+    _fields_ = [("n_iterations", C.c_int), ("n_restarts", C.c_int), ("converged", C.c_int),
+                ("initial_residual", C.c_double), ("final_residual", C.c_double),
+                ("tolerance", C.c_double)]
+
+
 def lib_path():
     return os.path.join(LIBDIR, "libglsamd.so")
 
@@ -108,6 +119,8 @@ def lib():
         L.gls_dist_vmult.argtypes = [vp, vp, vp, vp]
         L.gls_dist_vmult_group.argtypes = [vp, vp, vp, C.c_int, vp]
         L.gls_dist_interior_bricks.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)]
+        L.gls_gmres_solve.argtypes = [vp, vp, C.POINTER(GMRESDesc), vp, vp,
+                                      C.POINTER(GMRESResult), vp]
         L.gls_last_error.restype = C.c_char_p
         _lib = L
     return _lib
@@ -415,3 +428,33 @@ def build_gmg(meshes, cmasks, params, u_star_fine, history_fine=None, weights=No
     torch.cuda.synchronize()
     mg.setup()
     return mg, ops
+
+
+class LinearSolverGMRES:
+    """LinearSolverGMRES (solver_l.h:60-82, solver_l.cc:26-74) over the
+    device-resident gls_gmres_solve: right-preconditioned GMRES with 30
+    temporary vectors, tolerance max(relative * |b|, absolute), dst zeroed
+    first.  `preconditioner` is a Multigrid (one V-cycle per application,
+    PreconditionerGMG::vmult) or None (identity).  solve() raises GlsError on
+    no convergence (deal.II's SolverControl::NoConvergence); the statistics of
+    the last solve are in .last (n_iterations = SolverControl::last_step())."""
+
+    def __init__(self, op, preconditioner=None, n_max_iterations=10000,
+                 absolute_tolerance=1e-12, relative_tolerance=1e-8, max_n_tmp_vectors=30):
+        self.op = op
+        self.preconditioner = preconditioner
+        self.desc = GMRESDesc(max_n_tmp_vectors, n_max_iterations, absolute_tolerance,
+                              relative_tolerance)
+        self.last = None
+
+    def initialize(self):
+        pass  # solver_l.cc:39-43: nothing to do
+
+    def solve(self, dst, src):
+        res = GMRESResult()
+        mg = self.preconditioner.h if self.preconditioner is not None else None
+        rc = lib().gls_gmres_solve(self.op.h, mg, C.byref(self.desc), _ptr(dst), _ptr(src),
+                                   C.byref(res), _stream())
+        self.last = {f: getattr(res, f) for f, _ in GMRESResult._fields_}
+        _check(rc)
+        return dst

@@ -36,6 +36,8 @@
  *   gls_op_upload_tables /
  *   gls_op_download_tables           host-produced / inspected per-q tables
  *                                      (u_star_value ... operator_ns.h:120-132)
+ *   gls_gmres_solve                  LinearSolverGMRES::solve
+ *                                      solver_l.cc:45-74 (device-resident)
  *   gls_mg_*                         PreconditionerGMG (multigrid.h:61-141):
  *                                      relaxation smoother (multigrid.cc:281-351),
  *                                      MGTwoLevelTransfer (main.cc:538-563),
@@ -228,6 +230,33 @@ glsStatus gls_dist_vmult_group(glsDist const *members, void *const *dsts,
                                void *const *srcs, int n, void *stream);
 glsStatus gls_dist_interior_bricks(glsDist d, int64_t *n_interior,
                                    int64_t *n_total);
+
+/* ---- device-resident Krylov solver:
+ * LinearSolverGMRES::solve, solver_l.cc:45-74 — deal.II SolverGMRES with
+ * max_n_tmp_vectors = 30 (restart after 28 iterations) and right
+ * preconditioning; tolerance max(relative * |b|, absolute) (:52-53); x = 0
+ * on entry (:66).  `mg` NULL = identity preconditioner (PreconditionIdentity),
+ * else one V-cycle per application (PreconditionerGMG::vmult,
+ * multigrid.cc:202-220; the MG must be set up with outer_precision F64).
+ * op: FP64, single domain.  b and x are device vectors of op's size.
+ * No convergence within max_iterations = status 1 (SolverControl::
+ * NoConvergence), with *result filled. */
+typedef struct
+{
+  int    max_n_tmp_vectors;  /* 30  solver_l.cc:62                         */
+  int    max_iterations;     /* lin n max iterations  main.cc:97 (10000)   */
+  double absolute_tolerance; /* lin absolute tolerance main.cc:98 (1e-12)  */
+  double relative_tolerance; /* lin relative tolerance main.cc:99 (1e-8)   */
+} glsGMRESDesc;
+typedef struct
+{
+  int    n_iterations;       /* SolverControl::last_step()                 */
+  int    n_restarts;
+  int    converged;
+  double initial_residual, final_residual, tolerance;
+} glsGMRESResult;
+glsStatus gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x,
+                          const void *b, glsGMRESResult *result, void *stream);
 
 const char *gls_last_error(void);
 
