@@ -371,8 +371,11 @@ to_packs(const T (&x)[nc], V (&v)[NP])
 #ifndef GLS_BRICK_OCC
 #define GLS_BRICK_OCC 3
 #endif
+#ifndef GLS_BRICK_OCC32
+#define GLS_BRICK_OCC32 3
+#endif
 template <int dim, int k, typename T, int MODE>
-__global__ void __launch_bounds__(BLOCK, GLS_BRICK_OCC)
+__global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_BRICK_OCC)
   k_brick(BrickArgs<T, dim, k + 1> a)
 {
   using LDS          = BrickLDS<dim, k, T>;

@@ -843,6 +843,7 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
           cbits[i >> 5] |= 1u << (i & 31);
         }
   upload((void **)&op->d_cbits, cbits);
+  upload((void **)&op->d_node_cmask, op->h_cmask);
 
   // MatrixFree-style geometry: Cartesian cells (constant diagonal J) store
   // dim+1 numbers, all others JxW + J^{-1} per quadrature point
@@ -1032,7 +1033,8 @@ gls_op_destroy(glsOp op)
                   op->d_hmin,         op->d_tmp,          op->d_cbits,        op->d_brick_nodes,
                   op->d_brick_target, op->d_shared_nodes, op->d_shared_off,
                   op->d_partial,      op->d_bgeo_cart,    op->d_bgeo_gen,
-                  op->d_brick_geo,    op->d_brick_cell0,  op->d_brick_chunk0, op->d_tab_cbase};
+                  op->d_brick_geo,    op->d_brick_cell0,  op->d_brick_chunk0, op->d_tab_cbase,
+                  op->d_node_cmask,   op->d_inhom};
   for (void *b : bufs)
     if (b)
       (void)hipFree(b);
@@ -1199,12 +1201,126 @@ gls_op_vmult(glsOp op, void *dst, const void *src, void *stream)
   GLS_CATCH
 }
 
+} // extern "C"
+
+// constraints_inhomogeneous.distribute(tmp) on a copy of src (src NULL: a
+// zero vector, evaluate_rhs): constrained components take the inhomogeneity
+// (zero for the homogeneous Dirichlet / slip / pressure rows it shares with
+// constraints_copy, main.cc:879-891), all others src.  One lane per dof.
+template <typename T>
+__global__ void
+k_distribute(T *__restrict__ tmp, const T *__restrict__ src, const uint8_t *__restrict__ cmask,
+             const T *__restrict__ inhom, int64_t n_dofs, int nc)
+{
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n_dofs)
+    return;
+  const int64_t node = i / nc;
+  const int     c    = (int)(i - node * nc);
+  T             v    = src ? src[i] : T(0);
+  if ((cmask[node] >> c) & 1)
+    v = inhom ? inhom[i] : T(0);
+  tmp[i] = v;
+}
+
+static void
+distribute(glsOp op, void *tmp, const void *src, hipStream_t s)
+{
+  const int nc = op->dim + 1;
+  if (op->prec == GLS_F64)
+    hipLaunchKernelGGL(k_distribute<double>, grid1d(op->n_dofs), dim3(256), 0, s,
+                       (double *)tmp, (const double *)src, op->d_node_cmask,
+                       (const double *)op->d_inhom, op->n_dofs, nc);
+  else
+    hipLaunchKernelGGL(k_distribute<float>, grid1d(op->n_dofs), dim3(256), 0, s, (float *)tmp,
+                       (const float *)src, op->d_node_cmask, (const float *)op->d_inhom,
+                       op->n_dofs, nc);
+  HIP_THROW(hipGetLastError());
+}
+
+extern "C" {
+
+glsStatus
+gls_op_set_constraint_values(glsOp op, const void *values, void *stream)
+{
+  GLS_TRY
+  if (!op)
+    throw std::runtime_error("gls_op_set_constraint_values: null operator");
+  hipStream_t s = (hipStream_t)stream;
+  if (!values)
+    {
+      if (op->d_inhom)
+        {
+          HIP_THROW(hipStreamSynchronize(s));
+          HIP_THROW(hipFree(op->d_inhom));
+        }
+      op->d_inhom = nullptr;
+    }
+  else
+    {
+      if (!op->d_inhom)
+        HIP_THROW(hipMalloc(&op->d_inhom, std::max<size_t>(1, (size_t)op->n_dofs * op->tsize())));
+      HIP_THROW(hipMemcpyAsync(op->d_inhom, values, (size_t)op->n_dofs * op->tsize(),
+                               hipMemcpyDefault, s));
+    }
+  GLS_CATCH
+}
+
+} // extern "C"
+
+static void
+residual_cells(glsOp op, void *dst, const void *src, hipStream_t s)
+{
+  ApplyFn   af;
+  ProduceFn pf;
+  select(op, af, pf);
+  if (op->use_brick)
+    select_brick(op)(op, MODE_RESIDUAL, dst, src, 0, op->n_bricks, BRICK_RUN | BRICK_REDUCE,
+                     s);
+  else
+    {
+      HIP_THROW(hipMemsetAsync(dst, 0, (size_t)op->n_dofs * op->tsize(), s));
+      af(op, MODE_RESIDUAL, false, dst, src, 0, op->n_cells, s);
+    }
+}
+
+extern "C" {
+
+glsStatus
+gls_op_evaluate_rhs(glsOp op, void *dst, void *stream)
+{
+  GLS_TRY
+  if (!op || !dst)
+    throw std::runtime_error("gls_op_evaluate_rhs: null argument");
+  if (!op->have_lin)
+    throw std::runtime_error("evaluate_rhs before set_linearization_point");
+  hipStream_t s = (hipStream_t)stream;
+  distribute(op, op->d_tmp, nullptr, s);
+  residual_cells(op, dst, op->d_tmp, s);
+  GLS_CATCH
+}
+
 glsStatus
 gls_op_evaluate_residual(glsOp op, void *dst, const void *src, void *stream)
 {
   GLS_TRY
   if (!op || !dst || !src || dst == src)
     throw std::runtime_error("gls_op_evaluate_residual: bad arguments");
+  if (!op->have_lin)
+    throw std::runtime_error("evaluate_residual before set_linearization_point");
+  hipStream_t s = (hipStream_t)stream;
+  // operator_ns.cc:655-656: tmp = src; constraints_inhomogeneous.distribute(tmp)
+  distribute(op, op->d_tmp, src, s);
+  residual_cells(op, dst, op->d_tmp, s);
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_evaluate_residual_plain(glsOp op, void *dst, const void *src, void *stream)
+{
+  GLS_TRY
+  if (!op || !dst || !src || dst == src)
+    throw std::runtime_error("gls_op_evaluate_residual_plain: bad arguments");
   if (!op->have_lin)
     throw std::runtime_error("evaluate_residual before set_linearization_point");
   ApplyFn   af;

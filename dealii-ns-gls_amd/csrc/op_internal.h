@@ -35,6 +35,9 @@ struct glsOp_
   void     *d_hmin     = nullptr;
   void     *d_tmp      = nullptr;
   uint32_t *d_cbits    = nullptr; // constrained-dof bitmask (owned range)
+  uint8_t  *d_node_cmask = nullptr; // [n_nodes] constrained components (owned + ghost)
+  void     *d_inhom      = nullptr; // [n_dofs] inhomogeneity of constraints_inhomogeneous
+                                    // (values on constrained dofs), or null = all zero
   int       device     = 0;
 
   // brick decomposition (csrc/brick.h)

@@ -25,7 +25,8 @@ EXPORTS = [
     "gls_op_create", "gls_op_destroy", "gls_op_set_parameters", "gls_op_m",
     "gls_op_precision", "gls_op_set_linearization_point", "gls_op_set_previous_solution",
     "gls_op_vmult", "gls_op_vmult_cells", "gls_op_vmult_init", "gls_op_apply_identity_rows",
-    "gls_op_evaluate_residual",
+    "gls_op_evaluate_residual", "gls_op_evaluate_residual_plain", "gls_op_evaluate_rhs",
+    "gls_op_set_constraint_values", "gls_gmres_solve",
     "gls_op_compute_inverse_diagonal", "gls_op_upload_tables", "gls_op_download_tables",
     "gls_op_geometry_counts", "gls_op_vmult_bytes", "gls_mg_create", "gls_mg_destroy",
     "gls_mg_setup", "gls_mg_get_relaxation", "gls_mg_vcycle", "gls_mg_prolongate_add",
@@ -98,6 +99,9 @@ def lib():
         L.gls_op_vmult_init.argtypes = [vp, vp, vp, vp]
         L.gls_op_apply_identity_rows.argtypes = [vp, vp, vp, vp]
         L.gls_op_evaluate_residual.argtypes = [vp, vp, vp, vp]
+        L.gls_op_evaluate_residual_plain.argtypes = [vp, vp, vp, vp]
+        L.gls_op_evaluate_rhs.argtypes = [vp, vp, vp]
+        L.gls_op_set_constraint_values.argtypes = [vp, vp, vp]
         L.gls_op_compute_inverse_diagonal.argtypes = [vp, vp, vp]
         L.gls_op_upload_tables.argtypes = [vp, vp, vp]
         L.gls_op_download_tables.argtypes = [vp, vp, vp]
@@ -239,8 +243,31 @@ class NavierStokesOperator:
                                         _stream()))
 
     def evaluate_residual(self, dst, src):
+        """operator_ns.cc:648-682: distribute the inhomogeneous constraints
+        on a copy of src, residual cell loop, set_zero, *= -1."""
         _check(lib().gls_op_evaluate_residual(self.h, _ptr(dst), _ptr(src), _stream()))
         return dst
+
+    def evaluate_residual_plain(self, dst, src):
+        """The same on src as it is (no distribute)."""
+        _check(lib().gls_op_evaluate_residual_plain(self.h, _ptr(dst), _ptr(src), _stream()))
+        return dst
+
+    def evaluate_rhs(self, dst):
+        """operator_ns.cc:622-646: residual of the zero vector with the
+        inhomogeneous constraints distributed."""
+        _check(lib().gls_op_evaluate_rhs(self.h, _ptr(dst), _stream()))
+        return dst
+
+    def set_constraint_values(self, values):
+        """constraints_inhomogeneous (main.cc:879-891): a dof vector whose
+        constrained components hold the Dirichlet values (None: all zero)."""
+        if values is None:
+            _check(lib().gls_op_set_constraint_values(self.h, None, _stream()))
+            return
+        v = self._dev(values)
+        _check(lib().gls_op_set_constraint_values(self.h, _ptr(v), _stream()))
+        self._inhom_keep = v
 
     def compute_inverse_diagonal(self, diag):
         _check(lib().gls_op_compute_inverse_diagonal(self.h, _ptr(diag), _stream()))

@@ -173,6 +173,7 @@ class Deck:
     no_slip_wall: bool = True
     cylinder_shift: float = 0.005
     u_max: float = 1.0
+    t_init: float = 0.0
     raw: dict = field(default_factory=dict)
 
     @property
@@ -192,6 +193,40 @@ class Deck:
         (vel if self.no_slip_cylinder else slip).append(2)
         p = [1]  # outflow: homogeneous "NBC" constrains the pressure
         return vel, p, slip
+
+    def constraint_values(self, mesh, t=0.0):
+        """The inhomogeneity of constraints_inhomogeneous at time t
+        (main.cc:879-891, 926-942) as a dof vector: the inflow function
+        InflowBoundaryValues::Channel (simulation.cc:25-76, built at
+        simulation.cc:384-392) interpolated at the support points of the
+        velocity components on boundary id 0.  interpolate_boundary_values
+        into an AffineConstraints skips dofs already constrained by
+        constraints_copy (walls, cylinder, slip, outflow pressure), which
+        keep the value 0.  Nonzero only on constrained components."""
+        if self.simulation != "cylinder":
+            raise NotImplementedError(f"simulation {self.simulation!r} (SURVEY §8f next-4)")
+        vel, p, slip = self.boundary_descriptor()
+        full = mesh.constraint_mask(vel, p, slip)
+        copy = mesh.constraint_mask([i for i in vel if i != 0], p, slip)
+        inflow = (mesh.node_boundary & 1) != 0
+        x = mesh.coords
+        factor = np.ones(mesh.n_nodes)
+        if self.t_init != 0:  # ramp up
+            factor *= min(t / self.t_init, 1.0)
+        if self.no_slip_wall:  # parabolic profile
+            H = mesh.params["height"]
+            shift = -H / 2.0 + self.cylinder_shift
+            y = x[:, 1] - shift
+            factor *= 4 * y * (H - y) / H / H
+            if mesh.dim == 3:
+                z = x[:, 2] + H / 2.0
+                factor *= 4 * z * (H - z) / H / H
+        g = np.zeros(mesh.n_dofs)
+        nc = mesh.dim + 1
+        # component 0 carries u_max * factor, the other velocity components 0
+        sel = inflow & ((full & 1) != 0) & ((copy & 1) == 0)
+        g[np.nonzero(sel)[0] * nc] = self.u_max * factor[sel]
+        return g
 
     def time_integrator(self, dt=2.5e-4, n_steps=None):
         """(theta, weights[0..order], order, current_dt) of the deck's
@@ -254,4 +289,5 @@ def read_deck(path):
     d.no_slip_wall = bool(raw.get("simulation no slip wall", True))
     d.cylinder_shift = float(raw.get("simulation geometry cylinder shift", 0.005))
     d.u_max = float(raw.get("simulation u max", 1.0))
+    d.t_init = float(raw.get("simulation t init", 0.0))
     return d

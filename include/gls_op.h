@@ -30,6 +30,11 @@
  *                                      .cc:702-721) for multi-GPU
  *   gls_op_evaluate_residual         OperatorBase::evaluate_residual
  *                                      operator_base.h:44-46, .cc:648-682
+ *   gls_op_evaluate_rhs              OperatorBase::evaluate_rhs
+ *                                      operator_base.h:38-39, .cc:622-646
+ *   gls_op_set_constraint_values     the constraints_inhomogeneous the
+ *                                      operator holds by reference
+ *                                      (operator_ns.h:95, main.cc:879-891)
  *   gls_op_compute_inverse_diagonal  OperatorBase::compute_inverse_diagonal
  *                                      operator_base.h:29-30, .cc:195-225
  *   gls_op_m                         OperatorBase::m  operator_base.h:23-24
@@ -135,8 +140,29 @@ glsStatus gls_op_vmult_init(glsOp op, void *dst, const void *src, void *stream);
  * export-add (compress(add)) of a distributed vmult */
 glsStatus gls_op_apply_identity_rows(glsOp op, void *dst, const void *src, void *stream);
 
+/* evaluate_residual (operator_ns.cc:648-682): tmp = src;
+ * constraints_inhomogeneous.distribute(tmp) (constrained components take the
+ * values set by gls_op_set_constraint_values, zero if none are set); cell
+ * loop with the residual kernel on tmp; set_zero on constrained rows;
+ * dst *= -1. */
 glsStatus gls_op_evaluate_residual(glsOp op, void *dst, const void *src,
                                    void *stream);
+/* the same without the distribute step: constrained components of src are
+ * read as they are (read_dof_values_plain on an already distributed vector,
+ * which is what the Newton loop passes, main.cc:893) */
+glsStatus gls_op_evaluate_residual_plain(glsOp op, void *dst, const void *src,
+                                         void *stream);
+/* evaluate_rhs (operator_ns.cc:622-646): the residual of the zero vector
+ * with the inhomogeneous constraints distributed */
+glsStatus gls_op_evaluate_rhs(glsOp op, void *dst, void *stream);
+/* the inhomogeneity of constraints_inhomogeneous (main.cc:879-891,
+ * 926-942: VectorTools::interpolate_boundary_values of the inflow function
+ * on top of constraints_copy): a vector of the operator's size and
+ * precision (host or device pointer) whose constrained components hold
+ * the Dirichlet values; other components are ignored.  NULL clears it
+ * (all constrained values zero).  Copied; call again when the time-dependent
+ * boundary values change (every time step in the reference). */
+glsStatus gls_op_set_constraint_values(glsOp op, const void *values, void *stream);
 glsStatus gls_op_compute_inverse_diagonal(glsOp op, void *inv_diag,
                                           void *stream);
 

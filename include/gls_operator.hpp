@@ -116,6 +116,27 @@ public:
     check(gls_op_evaluate_residual(h, dst, src, stream), "evaluate_residual");
   }
 
+  // operator_base.h:44-46 without the distribute step
+  void
+  evaluate_residual_plain(void *dst, const void *src, void *stream = nullptr) const
+  {
+    check(gls_op_evaluate_residual_plain(h, dst, src, stream), "evaluate_residual_plain");
+  }
+
+  // operator_base.h:38-39 (operator_ns.cc:622-646)
+  void
+  evaluate_rhs(void *dst, void *stream = nullptr) const
+  {
+    check(gls_op_evaluate_rhs(h, dst, stream), "evaluate_rhs");
+  }
+
+  // constraints_inhomogeneous (main.cc:879-891): values on constrained dofs
+  void
+  set_constraint_values(const void *values, void *stream = nullptr)
+  {
+    check(gls_op_set_constraint_values(h, values, stream), "set_constraint_values");
+  }
+
   // operator_base.h:29-30 (operator_ns.cc:195-225)
   void
   compute_inverse_diagonal(void *diag, void *stream = nullptr) const

@@ -214,7 +214,7 @@ run(int argc, char **argv)
   if (prm.order > 0)
     op.set_previous_solution(hp, w);
   op.vmult(ddst.p, dsrc.p);
-  op.evaluate_residual(dres.p, dsrc.p);
+  op.evaluate_residual_plain(dres.p, dsrc.p);
   op.compute_inverse_diagonal(ddiag.p);
   HIPCHK(hipDeviceSynchronize());
   const std::vector<double> g_dst = ddst.down(), g_res = dres.down(), g_diag = ddiag.down();
