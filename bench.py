@@ -84,7 +84,8 @@ def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src,
     """The rest of SURVEY §8d's timing protocol, beside the headline line:
     cold (MALL flushed by a 1 GiB scratch write between reps) vs warm FP64
     at r2, the FP32 level operator (the smoother's hot path) on the same
-    mesh, and the HBM-bound r+1 mesh (Turek-3D size at r2 = 3).  Medians of
+    mesh, the HBM-bound r+1 mesh (Turek-3D size at r2 = 3) and the
+    unstructured sphere deck at r3 (17.1 M DoFs, all geometry per q).  Medians of
     `reps` event-timed vmults after 5 warm-ups."""
     import torch
     import glsamd
@@ -103,13 +104,13 @@ def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src,
     out[f"r{n_ref}_f64_warm"] = line(hot_op, hot_dst, hot_src)
     out[f"r{n_ref}_f64_cold"] = line(hot_op, hot_dst, hot_src, flush)
 
-    def build(m, cm, prec):
-        u_star = gi.linearization_point(m.n_nodes, m.dim, d.u_max)
+    def build(m, cm, prec, dk=d, prm=params, w=weights):
+        u_star = gi.linearization_point(m.n_nodes, m.dim, dk.u_max)
         op = glsamd.NavierStokesOperator(m, cm, prec)
-        op.set_parameters(**params)
+        op.set_parameters(**prm)
         op.set_linearization_point(u_star)
-        if params["order"] > 0:
-            op.set_previous_solution(gi.history(u_star, params["order"]), weights)
+        if prm["order"] > 0:
+            op.set_previous_solution(gi.history(u_star, prm["order"]), w)
         src = op._dev(gi.src_vector(m.n_dofs))
         return op, op.initialize_dof_vector(), src
 
@@ -121,7 +122,16 @@ def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src,
     op3, dst3, src3 = build(m3, m3.constraint_mask(vel, p, slip), "f64")
     out[f"r{n_ref + 1}_f64_warm"] = line(op3, dst3, src3)
     out[f"r{n_ref + 1}_f64_warm"]["cells"] = m3.n_cells
-    del op3, dst3, src3, scratch
+    del op3, dst3, src3
+    # the unstructured sphere deck (all cells general geometry, order 0)
+    ds = gm.read_deck(os.path.join(gm.DECK_DIR, "input_sphere_amg.json"))
+    ms = ds.mesh()
+    ps, ws = ds.operator_parameters(2.5e-4)
+    ops_, dsts, srcs = build(ms, ms.constraint_mask(*ds.boundary_descriptor()), "f64", ds, ps,
+                             ws)
+    out[f"sphere_r{ds.n_refinements}_f64_warm"] = line(ops_, dsts, srcs)
+    out[f"sphere_r{ds.n_refinements}_f64_warm"]["cells"] = ms.n_cells
+    del ops_, dsts, srcs, scratch
     torch.cuda.empty_cache()
     return out
 

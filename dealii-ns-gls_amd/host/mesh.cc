@@ -72,6 +72,11 @@ struct glsMesh_
   int64_t               n_nodes = 0;
   // slip normal axis per boundary id (-1 = not planar/axis aligned)
   int slip_axis[32];
+  // per axis d: boundary ids of the axis-aligned planar faces with normal d
+  // that touch the node (no-normal-flux constraints of flat walls); bit b of
+  // nonplanar_bids: a face with id b is curved or oblique
+  std::vector<uint32_t> node_axis_bid[3];
+  uint32_t              nonplanar_bids = 0;
   // generator parameters (for child lattice consistency checks)
   std::vector<double> params;
 };
@@ -496,6 +501,7 @@ build_fine(const CoarseMesh &cm, int degree, int n_ref, const CurvedSurface &cs)
   const int nv = 1 << dim;
 
   std::vector<uint32_t> lattice_node((size_t)N * N * Nz);
+  std::vector<uint32_t> axis_bid[3];
 
   for (size_t c = 0; c < cm.cells.size(); ++c)
     {
@@ -662,6 +668,27 @@ build_fine(const CoarseMesh &cm, int degree, int n_ref, const CurvedSurface &cs)
           if (bid < 0)
             continue;
           const int a = f / 2, side = f % 2;
+          // physical normal axis of the (flat, axis-aligned) coarse face
+          int nax = -1;
+          {
+            std::vector<P3> fv;
+            for (int k = 0; k < nv; ++k)
+              if (((k >> a) & 1) == side)
+                fv.push_back(cm.vertices[cm.cells[c][k]]);
+            for (int d = 0; d < dim && nax < 0; ++d)
+              {
+                bool same = true;
+                for (const P3 &q : fv)
+                  same = same && std::abs(q[d] - fv[0][d]) <= 1e-12 * (1.0 + std::abs(fv[0][d]));
+                if (same)
+                  nax = d;
+              }
+            if (nax < 0)
+              {
+                nax = -1;
+                m->nonplanar_bids |= 1u << bid;
+              }
+          }
           for (int l = 0; l < Nz; ++l)
             for (int j = 0; j < N; ++j)
               for (int i = 0; i < N; ++i)
@@ -671,12 +698,23 @@ build_fine(const CoarseMesh &cm, int degree, int n_ref, const CurvedSurface &cs)
                     continue;
                   const uint32_t id = lattice_node[i + N * (j + N * l)];
                   bids[id] |= 1u << bid;
+                  if (nax >= 0)
+                    {
+                      if (axis_bid[nax].size() <= id)
+                        axis_bid[nax].resize((size_t)id + 1, 0u);
+                      axis_bid[nax][id] |= 1u << bid;
+                    }
                 }
         }
     }
   m->coords   = std::move(coords);
   m->node_bid = std::move(bids);
   m->n_nodes  = (int64_t)m->node_bid.size();
+  for (int d = 0; d < 3; ++d)
+    {
+      axis_bid[d].resize((size_t)m->n_nodes, 0u);
+      m->node_axis_bid[d] = std::move(axis_bid[d]);
+    }
   return m;
 }
 
@@ -814,6 +852,74 @@ gls_mesh_hypercube(int dim, int degree, int n_ref, glsMesh **out)
     }
 }
 
+int
+gls_mesh_from_coarse(int dim, int degree, int n_ref, int64_t n_vertices, const double *vertices,
+                     int64_t n_cells, const int32_t *cells, int64_t n_bfaces,
+                     const int32_t *bface_vertices, const int32_t *bface_ids, glsMesh **out)
+{
+  try
+    {
+      if (!out || (dim != 2 && dim != 3) || degree < 1 || degree > 2 || n_ref < 0 ||
+          n_ref > 8 || n_vertices <= 0 || n_cells <= 0 || !vertices || !cells ||
+          (n_bfaces > 0 && (!bface_vertices || !bface_ids)))
+        throw std::runtime_error("gls_mesh_from_coarse: invalid arguments");
+      const int nv = 1 << dim, nvf = nv / 2;
+      CoarseMesh cm;
+      cm.dim = dim;
+      for (int64_t v = 0; v < n_vertices; ++v)
+        cm.vertices.push_back({vertices[v * dim], vertices[v * dim + 1],
+                               dim == 3 ? vertices[v * dim + 2] : 0.0});
+      for (int64_t c = 0; c < n_cells; ++c)
+        {
+          std::array<int, 8> cv{};
+          for (int k = 0; k < nv; ++k)
+            {
+              const int32_t v = cells[c * nv + k];
+              if (v < 0 || v >= n_vertices)
+                throw std::runtime_error("gls_mesh_from_coarse: vertex index out of range");
+              cv[k] = v;
+            }
+          cm.cells.push_back(cv);
+        }
+      // x-ordered coarse cells (contiguous slabs for the partitioner)
+      sort_coarse_cells(cm);
+      // GridIn::read_msh: a boundary face takes the physical tag of the
+      // boundary element on it, 0 when there is none
+      std::map<std::vector<int>, int> tagged;
+      for (int64_t f = 0; f < n_bfaces; ++f)
+        {
+          std::vector<int> key(bface_vertices + f * nvf, bface_vertices + (f + 1) * nvf);
+          std::sort(key.begin(), key.end());
+          if (bface_ids[f] < 0 || bface_ids[f] > 31)
+            throw std::runtime_error("gls_mesh_from_coarse: boundary id outside 0..31");
+          tagged[key] = bface_ids[f];
+        }
+      compute_face_bids(cm, 0, 0, 0, 0, false);
+      for (size_t c = 0; c < cm.cells.size(); ++c)
+        for (int f = 0; f < 2 * dim; ++f)
+          if (cm.face_bid[c][f] >= 0)
+            {
+              std::vector<int> key;
+              for (int k = 0; k < nv; ++k)
+                if (((k >> (f / 2)) & 1) == f % 2)
+                  key.push_back(cm.cells[c][k]);
+              std::sort(key.begin(), key.end());
+              auto it             = tagged.find(key);
+              cm.face_bid[c][f] = it == tagged.end() ? 0 : it->second;
+            }
+      CurvedSurface cs; // flat refinement (see gls_mesh.h)
+      glsMesh_     *m = build_fine(cm, degree, n_ref, cs);
+      m->params       = {2, (double)dim, (double)degree};
+      *out            = m;
+      return 0;
+    }
+  catch (const std::exception &e)
+    {
+      g_err = e.what();
+      return 1;
+    }
+}
+
 void
 gls_mesh_destroy(glsMesh *m)
 {
@@ -883,7 +989,7 @@ gls_mesh_constraint_mask(const glsMesh *m, uint32_t vel_ids, uint32_t p_ids,
     present |= m->node_bid[i];
   slip_ids &= present;
   for (int b = 0; b < 32; ++b)
-    if (((slip_ids >> b) & 1) && m->slip_axis[b] < 0)
+    if (((slip_ids >> b) & 1) && ((m->nonplanar_bids >> b) & 1))
       {
         g_err = "gls_mesh_constraint_mask: slip boundary id " +
                 std::to_string(b) +
@@ -900,11 +1006,13 @@ gls_mesh_constraint_mask(const glsMesh *m, uint32_t vel_ids, uint32_t p_ids,
         mask |= vel_bits;
       if (b & p_ids)
         mask |= (uint8_t)(1u << dim);
-      const uint32_t s = b & slip_ids;
-      if (s)
-        for (int bb = 0; bb < 32; ++bb)
-          if ((s >> bb) & 1)
-            mask |= (uint8_t)(1u << m->slip_axis[bb]);
+      // compute_no_normal_flux_constraints on flat axis-aligned walls: the
+      // normal component of every wall face touching the node (both at an
+      // edge where two walls meet)
+      if (b & slip_ids)
+        for (int d = 0; d < dim; ++d)
+          if (m->node_axis_bid[d][i] & slip_ids)
+            mask |= (uint8_t)(1u << d);
       out[i] = mask;
     }
   return 0;

@@ -30,6 +30,8 @@ def lib():
         L.gls_mesh_cylinder.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
                                         C.c_double, C.c_double, C.c_double, C.POINTER(vp)]
         L.gls_mesh_hypercube.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
+        L.gls_mesh_from_coarse.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int64, vp, C.c_int64,
+                                           vp, C.c_int64, vp, vp, C.POINTER(vp)]
         L.gls_mesh_destroy.argtypes = [vp]
         for name in ("gls_mesh_dim", "gls_mesh_degree"):
             getattr(L, name).argtypes = [vp]
@@ -141,6 +143,108 @@ def cylinder(dim, degree, n_ref, length=None, height=0.41, position=None, diamet
                                           diameter=diameter, shift=shift))
 
 
+# gmsh hexahedron / quadrangle vertex order -> lexicographic (x fastest)
+_GMSH_HEX_LEX = [0, 1, 3, 2, 4, 5, 7, 6]
+_GMSH_QUAD_LEX = [0, 1, 3, 2]
+
+
+def read_msh(path):
+    """GridIn::read_msh for gmsh 4.1 ASCII files with linear hexahedra
+    (simulation.cc:858-872): vertices, cells (lexicographic vertex order,
+    left-handed cells mirrored), boundary quadrilaterals and their physical
+    tags (the boundary ids; an entity without one gives 0).  Returns a dict
+    of numpy arrays (vertices [nv,3], cells [nc,8], bfaces [nf,4], bids [nf])."""
+    with open(path) as f:
+        lines = [ln.strip() for ln in f]
+    pos = {ln: i for i, ln in enumerate(lines) if ln.startswith("$")}
+    fmt = lines[pos["$MeshFormat"] + 1].split()
+    if not fmt[0].startswith("4") or fmt[1] != "0":
+        raise ValueError(f"{path}: only gmsh 4.x ASCII is supported (got {fmt})")
+    # entities -> physical tag
+    i = pos["$Entities"] + 1
+    counts = [int(x) for x in lines[i].split()]
+    i += 1
+    phys = {}
+    for dim_e, n in enumerate(counts):
+        for _ in range(n):
+            t = lines[i].split()
+            i += 1
+            tag = int(t[0])
+            k = 4 if dim_e == 0 else 7
+            nphys = int(t[k])
+            phys[(dim_e, tag)] = abs(int(t[k + 1])) if nphys > 0 else 0
+    # nodes
+    i = pos["$Nodes"] + 1
+    nblocks, nnodes = (int(x) for x in lines[i].split()[:2])
+    i += 1
+    tags, xyz = [], []
+    for _ in range(nblocks):
+        _, _, parametric, nb = (int(x) for x in lines[i].split())
+        i += 1
+        tags.extend(int(lines[i + j]) for j in range(nb))
+        i += nb
+        for j in range(nb):
+            xyz.append([float(x) for x in lines[i + j].split()[:3]])
+        i += nb
+    index = {t: j for j, t in enumerate(tags)}
+    vertices = np.asarray(xyz, dtype=np.float64)
+    # elements
+    i = pos["$Elements"] + 1
+    nblocks = int(lines[i].split()[0])
+    i += 1
+    cells, bfaces, bids = [], [], []
+    for _ in range(nblocks):
+        edim, etag, etype, nb = (int(x) for x in lines[i].split())
+        i += 1
+        for j in range(nb):
+            v = [index[int(x)] for x in lines[i + j].split()[1:]]
+            if etype == 5:
+                cells.append([v[k] for k in _GMSH_HEX_LEX])
+            elif etype == 3:
+                bfaces.append([v[k] for k in _GMSH_QUAD_LEX])
+                bids.append(phys.get((edim, etag), 0))
+        i += nb
+    cells = np.asarray(cells, dtype=np.int32)
+    # mirror left-handed cells (deal.II reorders them to positive measure)
+    p = vertices[cells]
+    jac = np.einsum("ci,ci->c", np.cross(p[:, 1] - p[:, 0], p[:, 2] - p[:, 0]),
+                    p[:, 4] - p[:, 0])
+    neg = jac < 0
+    cells[neg] = cells[neg][:, [1, 0, 3, 2, 5, 4, 7, 6]]
+    return dict(vertices=vertices, cells=cells, bfaces=np.asarray(bfaces, dtype=np.int32),
+                bids=np.asarray(bids, dtype=np.int32))
+
+
+def from_coarse(coarse, degree, n_ref, kind="coarse"):
+    """A refined mesh from a coarse hex mesh (gls_mesh_from_coarse)."""
+    v = np.ascontiguousarray(coarse["vertices"], dtype=np.float64)
+    c = np.ascontiguousarray(coarse["cells"], dtype=np.int32)
+    bf = np.ascontiguousarray(coarse["bfaces"], dtype=np.int32)
+    bi = np.ascontiguousarray(coarse["bids"], dtype=np.int32)
+    dim = v.shape[1]
+    h = C.c_void_p()
+    _check(lib().gls_mesh_from_coarse(dim, degree, n_ref, v.shape[0], v.ctypes.data, c.shape[0],
+                                      c.ctypes.data, bf.shape[0], bf.ctypes.data, bi.ctypes.data,
+                                      C.byref(h)))
+    return Mesh(h.value, kind, dict(dim=dim, degree=degree, n_ref=n_ref))
+
+
+SPHERE_COARSE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "data",
+                             "sphere_coarse.npz")
+
+
+def sphere(degree, n_ref, path=None):
+    """SimulationSphere::create_triangulation (simulation.cc:858-872): the
+    reference's mesh/sphere.msh (or its converted coarse arrays,
+    data/sphere_coarse.npz, scripts/convert_msh.py) refined n_ref times."""
+    if path is not None and path.endswith(".msh"):
+        coarse = read_msh(path)
+    else:
+        with np.load(path or SPHERE_COARSE) as z:
+            coarse = {k: z[k] for k in z.files}
+    return from_coarse(coarse, degree, n_ref, "sphere")
+
+
 def hypercube(dim, degree, n_ref):
     h = C.c_void_p()
     _check(lib().gls_mesh_hypercube(dim, degree, n_ref, C.byref(h)))
@@ -184,6 +288,10 @@ class Deck:
     def boundary_descriptor(self):
         """(vel_ids, p_ids, slip_ids) of constraints_homogeneous
         (simulation.cc:378-431 + main.cc:259-291)."""
+        if self.simulation == "sphere":
+            # simulation.cc:876-893: sphere (0) no-slip, inflow (1) Dirichlet,
+            # walls (2) slip, outflow (3) pressure
+            return [0, 1], [3], [2]
         if self.simulation != "cylinder":
             raise NotImplementedError(f"simulation {self.simulation!r} (SURVEY §8f next-4)")
         vel = [0]  # inflow: inhomogeneous DBC, zero in constraints_homogeneous
@@ -203,12 +311,18 @@ class Deck:
         into an AffineConstraints skips dofs already constrained by
         constraints_copy (walls, cylinder, slip, outflow pressure), which
         keep the value 0.  Nonzero only on constrained components."""
-        if self.simulation != "cylinder":
+        if self.simulation not in ("cylinder", "sphere"):
             raise NotImplementedError(f"simulation {self.simulation!r} (SURVEY §8f next-4)")
         vel, p, slip = self.boundary_descriptor()
+        inflow_id = 1 if self.simulation == "sphere" else 0
         full = mesh.constraint_mask(vel, p, slip)
-        copy = mesh.constraint_mask([i for i in vel if i != 0], p, slip)
-        inflow = (mesh.node_boundary & 1) != 0
+        copy = mesh.constraint_mask([i for i in vel if i != inflow_id], p, slip)
+        inflow = ((mesh.node_boundary >> inflow_id) & 1) != 0
+        if self.simulation == "sphere":  # Channel(0.0, 1.0): uniform, u_max 1
+            g = np.zeros(mesh.n_dofs)
+            sel = inflow & ((full & 1) != 0) & ((copy & 1) == 0)
+            g[np.nonzero(sel)[0] * (mesh.dim + 1)] = 1.0
+            return g
         x = mesh.coords
         factor = np.ones(mesh.n_nodes)
         if self.t_init != 0:  # ramp up
@@ -265,6 +379,8 @@ class Deck:
 
     def mesh(self, n_ref=None):
         n_ref = self.n_refinements if n_ref is None else n_ref
+        if self.simulation == "sphere":
+            return sphere(self.fe_degree, n_ref, self.raw.get("mesh file"))
         return cylinder(self.dim, self.fe_degree, n_ref, shift=self.cylinder_shift)
 
 

@@ -50,6 +50,21 @@ int gls_mesh_cylinder(int dim, int degree, int n_ref, double length,
  * degree k in {1,2,3}; every boundary face has id 0. */
 int gls_mesh_hypercube(int dim, int degree, int n_ref, glsMesh **out);
 
+/* An unstructured coarse hex (quad) mesh refined n_ref times — the sphere
+ * deck's GridIn::read_msh + refine_global (simulation.cc:858-872).
+ * cells: [n_cells][2^dim] vertex indices in lexicographic order (x fastest;
+ * gmsh's hexahedron order 0 1 2 3 4 5 6 7 maps to 0 1 3 2 4 5 7 6);
+ * boundary elements: [n_bfaces][2^(dim-1)] vertex indices with their
+ * physical tags (the boundary ids; untagged boundary faces get 0).
+ * Refinement is flat (multilinear): SphericalManifold is attached to
+ * manifold id 0, which read_msh leaves unset on every object, so it
+ * bends nothing — parity unpinned, see DESIGN.md.  degree k in {1,2}. */
+int gls_mesh_from_coarse(int dim, int degree, int n_ref, int64_t n_vertices,
+                         const double *vertices, int64_t n_cells,
+                         const int32_t *cells, int64_t n_bfaces,
+                         const int32_t *bface_vertices,
+                         const int32_t *bface_ids, glsMesh **out);
+
 void gls_mesh_destroy(glsMesh *m);
 
 int     gls_mesh_dim(const glsMesh *m);
