@@ -131,9 +131,65 @@ def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src,
                              ws)
     out[f"sphere_r{ds.n_refinements}_f64_warm"] = line(ops_, dsts, srcs)
     out[f"sphere_r{ds.n_refinements}_f64_warm"]["cells"] = ms.n_cells
-    del ops_, dsts, srcs, scratch
+    del ops_, dsts, srcs
+    out.update(mg_companions(d, params, weights, n_ref))
+    del scratch
     torch.cuda.empty_cache()
     return out
+
+
+def mg_companions(d, params, weights, n_ref, reps=20):
+    """The preconditioner side of a GMRES iteration:
+    one FP32 V-cycle over the Re3900 hierarchy r0..r{n_ref} (5 damped-Jacobi
+    pre/post steps, relaxation coarse solve), and one full right-preconditioned
+    GMRES iteration (V-cycle + FP64 vmult + CGS2), event-timed medians."""
+    import torch
+    import glsamd
+    meshes = [d.mesh(r) for r in range(n_ref + 1)]
+    vel, p, slip = d.boundary_descriptor()
+    cm = [m.constraint_mask(vel, p, slip) for m in meshes]
+    u = gi.linearization_point(meshes[-1].n_nodes, meshes[-1].dim, d.u_max)
+    hist = gi.history(u, params["order"])
+    mg, _ = glsamd.build_gmg(meshes, cm, params, u, hist, weights, precision="f32",
+                             coarse_n_iterations=10)
+    A = glsamd.NavierStokesOperator(meshes[-1], cm[-1], "f64")
+    A.set_parameters(**params)
+    A.set_linearization_point(u)
+    if params["order"] > 0:
+        A.set_previous_solution(hist, weights)
+    b = A._dev(gi.src_vector(meshes[-1].n_dofs))
+    x = A.initialize_dof_vector()
+    for _ in range(3):
+        mg.vcycle(x, b)
+    torch.cuda.synchronize()
+    t = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        mg.vcycle(x, b)
+        e1.record()
+        torch.cuda.synchronize()
+        t.append(e0.elapsed_time(e1))
+    vc = float(np.median(t))
+    # GMRES: fixed 28 iterations (one restart cycle), wall time per iteration
+    solver = glsamd.LinearSolverGMRES(A, mg, n_max_iterations=28, relative_tolerance=1e-30,
+                                      absolute_tolerance=0.0)
+    times = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        try:
+            solver.solve(x, b)
+        except glsamd.GlsError:
+            pass  # no convergence at tolerance 0 is the point: 28 iterations
+        torch.cuda.synchronize()
+        times.append((time.perf_counter() - t0) / max(1, solver.last["n_iterations"]))
+    return {f"r{n_ref}_vcycle_f32": {"ms": vc, "levels": n_ref + 1,
+                                     "finest_dofs": meshes[-1].n_dofs,
+                                     "vcycles_per_s": 1e3 / vc},
+            f"r{n_ref}_gmres_iteration": {"ms": float(np.median(times)) * 1e3,
+                                          "note": "V-cycle + FP64 vmult + CGS2 + host "
+                                                  "Hessenberg step, wall clock"}}
 
 
 def main():

@@ -31,17 +31,25 @@ namespace
 {
 constexpr int MAXP = 2 * 3 + 1; // (2k+1) for k <= 3
 constexpr int MAXN = 4;
+constexpr uint32_t NOT_OWNER = 0x80000000u;
 
 template <typename T>
 struct TransferArgs
 {
   const uint32_t *coarse_nodes; // [cells_c][nq] node | cmask << 28
-  const uint32_t *child;        // [cells_c][nl] fine node ids
+  const uint32_t *child;        // [cells_c][nl] fine node ids | NOT_OWNER: every fine
+                                // node is owned by one entry (its first coarse cell)
   const T        *weight;       // [n_dofs_f]
   int64_t         n_cells_c;
   T               P[MAXP][MAXN];
 };
 
+// Transfers as sum factorisation over the (2k+1)^dim child lattice of one
+// coarse cell: the 1-D interpolation matrix P [(2k+1) x (k+1)] is staged in
+// LDS and each lane reads its rows into registers, so every tensor index is a
+// compile-time constant of the unrolled sweeps (a dense (2k+1)^dim x
+// (k+1)^dim loop indexing the kernel-argument array at run time went
+// through scratch: 28.7 us per r2 -> r1 restriction).
 template <int dim, int k, typename T>
 __global__ void __launch_bounds__(256)
   k_prolongate(TransferArgs<T> a, T *__restrict__ dst_f, const T *__restrict__ src_c)
@@ -49,8 +57,11 @@ __global__ void __launch_bounds__(256)
   constexpr int n = k + 1, nq = ipow(n, dim), nc = dim + 1, L = 2 * k + 1;
   constexpr int nl = ipow(L, dim);
   __shared__ T  u[nc][nq];
+  __shared__ T  sP[L][n];
   const int64_t c = blockIdx.x;
   const int     t = threadIdx.x;
+  if (t < L * n)
+    sP[t / n][t % n] = a.P[t / n][t % n];
   if (t < nq)
     {
       const uint32_t packed = a.coarse_nodes[c * nq + t];
@@ -62,24 +73,44 @@ __global__ void __launch_bounds__(256)
   __syncthreads();
   for (int I = t; I < nl; I += blockDim.x)
     {
-      const int      Ix = I % L, Iy = (I / L) % L, Iz = dim == 3 ? I / (L * L) : 0;
-      const uint32_t fn = a.child[c * nl + I];
+      const int Ix = I % L, Iy = (I / L) % L, Iz = dim == 3 ? I / (L * L) : 0;
+      T         px[n], py[n], pz[n];
+#pragma unroll
+      for (int i = 0; i < n; ++i)
+        {
+          px[i] = sP[Ix][i];
+          py[i] = sP[Iy][i];
+          pz[i] = dim == 3 ? sP[Iz][i] : T(0);
+        }
+      const uint32_t fe = a.child[c * nl + I];
+      // a fine node shared by several coarse cells is written by its owner
+      // only (conforming interpolation: all give the same value), so the
+      // update is a plain read-modify-write, no atomics
+      if (fe & NOT_OWNER)
+        continue;
+      const uint32_t fn = fe;
 #pragma unroll
       for (int comp = 0; comp < nc; ++comp)
         {
           T s = 0;
 #pragma unroll
-          for (int i = 0; i < nq; ++i)
+          for (int iz = 0; iz < (dim == 3 ? n : 1); ++iz)
             {
-              const int ix = i % n, iy = (i / n) % n, iz = dim == 3 ? i / (n * n) : 0;
-              T         p  = a.P[Ix][ix] * a.P[Iy][iy];
-              if (dim == 3)
-                p *= a.P[Iz][iz];
-              s += p * u[comp][i];
+              T sy = 0;
+#pragma unroll
+              for (int iy = 0; iy < n; ++iy)
+                {
+                  T sx = 0;
+#pragma unroll
+                  for (int ix = 0; ix < n; ++ix)
+                    sx += px[ix] * u[comp][ix + n * (iy + n * iz)];
+                  sy += py[iy] * sx;
+                }
+              s += (dim == 3 ? pz[iz] : T(1)) * sy;
             }
           const T w = a.weight[(size_t)fn * nc + comp];
           if (w != T(0))
-            unsafeAtomicAdd(dst_f + (size_t)fn * nc + comp, w * s);
+            dst_f[(size_t)fn * nc + comp] += w * s;
         }
     }
 }
@@ -91,14 +122,23 @@ __global__ void __launch_bounds__(256)
   constexpr int n = k + 1, nq = ipow(n, dim), nc = dim + 1, L = 2 * k + 1;
   constexpr int nl = ipow(L, dim);
   __shared__ T  v[nc][nl];
+  __shared__ T  sP[L][n];
   const int64_t c = blockIdx.x;
   const int     t = threadIdx.x;
+  if (t < L * n)
+    sP[t / n][t % n] = a.P[t / n][t % n];
   for (int I = t; I < nl; I += blockDim.x)
     {
-      const uint32_t fn = a.child[c * nl + I];
+      // R = P^T of the owner-only prolongation: a shared fine node feeds its
+      // owner's coarse dofs only (its other cells' shape functions that are
+      // nonzero there are the same shared coarse dofs)
+      const uint32_t fe    = a.child[c * nl + I];
+      const bool     owner = !(fe & NOT_OWNER);
+      const uint32_t fn    = fe & ~NOT_OWNER;
 #pragma unroll
       for (int comp = 0; comp < nc; ++comp)
-        v[comp][I] = a.weight[(size_t)fn * nc + comp] * src_f[(size_t)fn * nc + comp];
+        v[comp][I] = owner ? a.weight[(size_t)fn * nc + comp] * src_f[(size_t)fn * nc + comp]
+                           : T(0);
     }
   __syncthreads();
   for (int i = t; i < nq * nc; i += blockDim.x)
@@ -109,14 +149,30 @@ __global__ void __launch_bounds__(256)
       if ((cm >> comp) & 1)
         continue;
       const int ix = ii % n, iy = (ii / n) % n, iz = dim == 3 ? ii / (n * n) : 0;
-      T         s  = 0;
-      for (int I = 0; I < nl; ++I)
+      T         px[L], py[L], pz[L];
+#pragma unroll
+      for (int I = 0; I < L; ++I)
         {
-          const int Ix = I % L, Iy = (I / L) % L, Iz = dim == 3 ? I / (L * L) : 0;
-          T         p  = a.P[Ix][ix] * a.P[Iy][iy];
-          if (dim == 3)
-            p *= a.P[Iz][iz];
-          s += p * v[comp][I];
+          px[I] = sP[I][ix];
+          py[I] = sP[I][iy];
+          pz[I] = dim == 3 ? sP[I][iz] : T(0);
+        }
+      const T *vc = v[comp];
+      T        s  = 0;
+#pragma unroll
+      for (int Iz = 0; Iz < (dim == 3 ? L : 1); ++Iz)
+        {
+          T sy = 0;
+#pragma unroll
+          for (int Iy = 0; Iy < L; ++Iy)
+            {
+              T sx = 0;
+#pragma unroll
+              for (int Ix = 0; Ix < L; ++Ix)
+                sx += px[Ix] * vc[Ix + L * (Iy + L * Iz)];
+              sy += py[Iy] * sx;
+            }
+          s += (dim == 3 ? pz[Iz] : T(1)) * sy;
         }
       unsafeAtomicAdd(dst_c + (size_t)node * nc + comp, s);
     }
@@ -136,7 +192,7 @@ k_interpolate(TransferArgs<T> a, T *__restrict__ dst_c, const T *__restrict__ sr
   const int      i  = (int)(g % nq);
   const int      ix = i % n, iy = (i / n) % n, iz = dim == 3 ? i / (n * n) : 0;
   const int      I  = 2 * ix + L * (2 * iy + L * (dim == 3 ? 2 * iz : 0));
-  const uint32_t fn = a.child[c * nl + I];
+  const uint32_t fn = a.child[c * nl + I] & ~NOT_OWNER;
   const uint32_t cn = a.coarse_nodes[c * nq + i] & NODE_MASK;
 #pragma unroll
   for (int comp = 0; comp < nc; ++comp)
@@ -579,18 +635,19 @@ gls_mg_create(const glsMGDesc *desc, const glsOp *levels, const uint32_t *const 
       glsOp         cop = mg->ops[l - 1], fop = mg->ops[l];
       const int64_t nch = cop->n_cells * nl;
       std::vector<uint32_t> ch(child[l], child[l] + nch);
-      std::vector<double>   val((size_t)fop->n_nodes, 0.0);
-      for (uint32_t fn : ch)
+      std::vector<uint8_t>  seen((size_t)fop->n_nodes, 0);
+      for (uint32_t &fn : ch)
         {
-          if ((int64_t)fn >= fop->n_nodes)
+          if ((int64_t)fn >= fop->n_nodes || fn >= NOT_OWNER)
             throw std::runtime_error("gls_mg_create: child lattice node out of range");
-          val[fn] += 1.0;
+          if (seen[fn])
+            fn |= NOT_OWNER; // the first coarse cell touching a fine node owns it
+          seen[fn & ~NOT_OWNER] = 1;
         }
       std::vector<double> w((size_t)fop->n_dofs, 0.0);
       for (int64_t nd = 0; nd < fop->n_nodes; ++nd)
         for (int c = 0; c < mg->nc; ++c)
-          w[nd * mg->nc + c] =
-            (((fop->h_cmask[nd] >> c) & 1) || val[nd] == 0) ? 0.0 : 1.0 / val[nd];
+          w[nd * mg->nc + c] = (((fop->h_cmask[nd] >> c) & 1) || !seen[nd]) ? 0.0 : 1.0;
       HIP_THROW(hipMalloc((void **)&mg->d_child[l], nch * sizeof(uint32_t)));
       HIP_THROW(hipMemcpy(mg->d_child[l], ch.data(), nch * sizeof(uint32_t),
                           hipMemcpyHostToDevice));
