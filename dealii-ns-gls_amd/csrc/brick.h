@@ -117,6 +117,12 @@ struct BrickArgs
   T              *dst;
   const T        *src;
   T              *partial; // [slot][dim+1], slots of a node contiguous
+  // fused damped-Jacobi step (PreconditionRelaxation::step of the multigrid
+  // smoother): with rb set, dst = src + omega * rd * (rb - A src) instead of
+  // A src (the smoother's separate k_relax pass over n dofs disappears)
+  const T        *rb;
+  const T        *rd;
+  T               romega;
   int64_t         brick_begin, brick_end;
   int             bx, by, bz;
   int             L, Lx, Ly;
@@ -749,6 +755,14 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
               if ((cm >> c) & 1)
                 r[c] = R ? T(0) : a.src[(size_t)tgt * nc + c];
             }
+          if constexpr (!R)
+            if (a.rb)
+#pragma unroll
+              for (int c = 0; c < nc; ++c)
+                {
+                  const size_t j = (size_t)tgt * nc + c;
+                  r[c]           = a.src[j] + a.romega * a.rd[j] * (a.rb[j] - r[c]);
+                }
           store_node<T, nc>(a.dst, tgt, r);
         }
     }
@@ -764,7 +778,9 @@ template <typename T, int nc, bool R>
 __global__ void __launch_bounds__(256)
   k_shared_reduce(T *__restrict__ dst, const T *__restrict__ src,
                   const T *__restrict__ partial, const uint32_t *__restrict__ nodes,
-                  const uint32_t *__restrict__ offsets, int64_t n_shared)
+                  const uint32_t *__restrict__ offsets, int64_t n_shared,
+                  const T *__restrict__ rb = nullptr, const T *__restrict__ rd = nullptr,
+                  T romega = T(0))
 {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= n_shared * nc)
@@ -795,6 +811,11 @@ __global__ void __launch_bounds__(256)
   const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
   if ((cm >> c) & 1)
     sum = R ? T(0) : src[(size_t)node * nc + c];
+  if (!R && rb)
+    {
+      const size_t j = (size_t)node * nc + c;
+      sum            = src[j] + romega * rd[j] * (rb[j] - sum);
+    }
   dst[(size_t)node * nc + c] = sum;
 }
 
@@ -806,7 +827,9 @@ template <typename T, int nc, bool R>
 __global__ void __launch_bounds__(256)
   k_shared_reduce_cls(T *__restrict__ dst, const T *__restrict__ src,
                       const T *__restrict__ partial, const uint32_t *__restrict__ nodes,
-                      const ReduceClasses rc, int64_t n_shared)
+                      const ReduceClasses rc, int64_t n_shared,
+                      const T *__restrict__ rb = nullptr, const T *__restrict__ rd = nullptr,
+                      T romega = T(0))
 {
   // 16-byte packs when a node's row is whole packs (nc = 4): one thread per
   // (node, pack), vector loads and stores
@@ -851,6 +874,13 @@ __global__ void __launch_bounds__(256)
         for (int w = 0; w < W; ++w)
           if ((cm >> (kp * W + w)) & 1)
             sum[w] = R ? T(0) : src[(size_t)node * nc + kp * W + w];
+      if (!R && rb)
+        {
+          const size_t j  = (size_t)node * NPK + kp;
+          const V      xs = reinterpret_cast<const V *>(src)[j];
+          sum = xs + romega * reinterpret_cast<const V *>(rd)[j] *
+                       (reinterpret_cast<const V *>(rb)[j] - sum);
+        }
       reinterpret_cast<V *>(dst)[(size_t)node * NPK + kp] = sum;
       return;
     }
@@ -887,6 +917,11 @@ __global__ void __launch_bounds__(256)
   const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
   if ((cm >> c) & 1)
     sum = R ? T(0) : src[(size_t)node * nc + c];
+  if (!R && rb)
+    {
+      const size_t j = (size_t)node * nc + c;
+      sum            = src[j] + romega * rd[j] * (rb[j] - sum);
+    }
   dst[(size_t)node * nc + c] = sum;
 }
 

@@ -569,6 +569,9 @@ struct Impl
         a.dst           = (T *)dst;
         a.src           = (const T *)src;
         a.partial       = (T *)op->d_partial;
+        a.rb            = (const T *)op->relax_b;
+        a.rd            = (const T *)op->relax_d;
+        a.romega        = (T)op->relax_omega;
         a.brick_begin   = b0;
         a.brick_end     = b1;
         a.bx            = op->bx;
@@ -617,7 +620,7 @@ struct Impl
             else if (rc.n > 0)
               hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, false>), g3, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)op->d_partial,
-                                 op->d_shared_nodes, rc, op->n_shared);
+                                 op->d_shared_nodes, rc, op->n_shared, a.rb, a.rd, a.romega);
             else if (mode == MODE_RESIDUAL)
               hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, true>), g2, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)op->d_partial,
@@ -625,7 +628,8 @@ struct Impl
             else
               hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, false>), g2, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)op->d_partial,
-                                 op->d_shared_nodes, op->d_shared_off, op->n_shared);
+                                 op->d_shared_nodes, op->d_shared_off, op->n_shared, a.rb,
+                                 a.rd, a.romega);
             HIP_THROW(hipGetLastError());
           }
       }

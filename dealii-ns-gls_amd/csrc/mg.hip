@@ -401,10 +401,37 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
       relax(mg, level, x, b, 1, s);
       it = 1;
     }
+  glsOp op = mg->ops[level];
+  if (!op->use_brick || op->n_owned_dofs != op->n_dofs)
+    {
+      for (; it < iters; ++it)
+        {
+          check(gls_op_vmult(op, mg->tmp[level], x, s));
+          relax(mg, level, x, b, 0, s);
+        }
+      return;
+    }
+  // brick operators: the step x + omega D^{-1} (b - A x) is fused into the
+  // vmult's write-out (k_brick, k_shared_reduce_cls), ping-ponging between x
+  // and tmp; an odd count starts with one unfused step so the result lands
+  // in x without a copy
+  if ((iters - it) % 2 == 1)
+    {
+      check(gls_op_vmult(op, mg->tmp[level], x, s));
+      relax(mg, level, x, b, 0, s);
+      ++it;
+    }
+  void *cur = x, *oth = mg->tmp[level];
   for (; it < iters; ++it)
     {
-      check(gls_op_vmult(mg->ops[level], mg->tmp[level], x, s));
-      relax(mg, level, x, b, 0, s);
+      op->relax_b     = b;
+      op->relax_d     = mg->invdiag[level];
+      op->relax_omega = mg->omega[level];
+      const glsStatus st = gls_op_vmult(op, oth, cur, s);
+      op->relax_b = op->relax_d = nullptr;
+      op->relax_omega           = 0.0;
+      check(st);
+      std::swap(cur, oth);
     }
 }
 

@@ -39,6 +39,10 @@ struct glsOp_
   void     *d_inhom      = nullptr; // [n_dofs] inhomogeneity of constraints_inhomogeneous
                                     // (values on constrained dofs), or null = all zero
   int       device     = 0;
+  // fused damped-Jacobi step for the next brick vmult (set by the multigrid
+  // smoother around one gls_op_vmult call, csrc/mg.hip)
+  const void *relax_b = nullptr, *relax_d = nullptr;
+  double      relax_omega = 0.0;
 
   // brick decomposition (csrc/brick.h)
   bool      use_brick = false;
