@@ -20,7 +20,7 @@
 // a wavefront (3D Q2: 2 cells = 54 of 64 lanes), so the LDS sum-factorisation
 // sweeps are ordered by wavefront fences, not workgroup barriers.
 // Occupancy is the lever (the kernel is LDS-latency bound at low wave
-// counts): 3 waves/SIMD (FP64, <= 168 VGPRs, 37 KB LDS per workgroup).
+// counts): 3 waves/SIMD (FP64, 162 VGPRs, 44 KB LDS per workgroup).
 // Software-pipelining the next round's loads was measured and gave nothing.
 #pragma once
 
