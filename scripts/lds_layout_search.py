@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Exhaustive search of the k_brick sweep-buffer strides (PY, PZ, KS, WB in
+16-byte packs) under the ds_read_b128 / ds_write_b128 lane-group bank model of
+MI355X_MICROARCH.md §LDS, for NP packs per point (2: FP64, 1: FP32).
+    python scripts/lds_layout_search.py 1"""
+import itertools
+G128=[list(range(0,4))+list(range(12,16))+list(range(20,28)),
+      list(range(4,12))+list(range(16,20))+list(range(28,32)),
+      list(range(32,36))+list(range(44,48))+list(range(52,60)),
+      list(range(36,44))+list(range(48,52))+list(range(60,64))]
+lanes=[]
+for l in range(64):
+    slot,p=divmod(l,27)
+    if slot<2: lanes.append((l,slot,(p%3,(p//3)%3,p//9)))
+def rd_cost(addrs):  # addrs: lane->pack index (16B units)
+    tot=0
+    for g in G128:
+        banks={}
+        for l in g:
+            if l in addrs:
+                a=addrs[l]
+                for i in range(4):
+                    banks.setdefault((a*4+i)%64,set()).add(a)
+        if banks: tot+=max(len(v) for v in banks.values())
+    return tot
+def wr_cost(addrs):
+    tot=0
+    for g0 in range(0,64,8):
+        banks={}
+        for l in range(g0,g0+8):
+            if l in addrs:
+                a=addrs[l]
+                for i in range(4): banks.setdefault((a*4+i)%32,set()).add(a)
+        if banks: tot+=max(len(v) for v in banks.values())
+    return max(13,tot)
+def cost(PY,PZ,KS,WB,NP):
+    st=[1,PY,PZ]
+    tot=0; n_rd=0
+    for half in (0,1):            # buffer A or B
+        for kp in range(NP):
+            # reads along each axis, j = 0..2
+            for ax in range(3):
+                for j in range(3):
+                    ad={}
+                    for l,slot,pa in lanes:
+                        q=pa[0]+PY*pa[1]+PZ*pa[2]
+                        ad[l]=slot*WB+half*NP*KS+kp*KS+q-pa[ax]*st[ax]+j*st[ax]
+                    tot+=rd_cost(ad); n_rd+=1
+            ad={l:slot*WB+half*NP*KS+kp*KS+pa[0]+PY*pa[1]+PZ*pa[2] for l,slot,pa in lanes}
+            tot+=wr_cost(ad)
+    return tot, n_rd
+import sys
+NP=int(sys.argv[1])
+print('current', cost(3,9,27,54,1) if NP==1 else cost(4,13,37,151,2), 'unpadded', cost(3,9,27,2*NP*27,NP))
+best=[]
+for PY in range(3,9):
+    for PZ in range(3*PY, 3*PY+24):
+        for KS in range(2+2*PY+2*PZ+1, 2+2*PY+2*PZ+20):
+            for WB in range(2*NP*KS, 2*NP*KS+20):
+                c,_=cost(PY,PZ,KS,WB,NP)
+                best.append((c,PY,PZ,KS,WB))
+best.sort(); print(best[:8])
