@@ -235,9 +235,9 @@ struct BrickLDS
            sizeof(T) * 4 * n * CoefRow<T, n>::RP;
   }
   __host__ __device__ static size_t
-  tab_offset(int L) // accumulator bytes rounded up to 16
+  tab_offset(int L) // accumulator bytes (FP64 for both precisions) rounded up to 16
   {
-    return (sizeof(T) * (size_t)nc * L + 15) / 16 * 16;
+    return (sizeof(double) * (size_t)nc * L + 15) / 16 * 16;
   }
 };
 
@@ -410,7 +410,10 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
   const int LP     = a.LP; // padded LDS lattice (bank-conflict-free x sweep)
   V        *s_src  = reinterpret_cast<V *>(smem);   // [NP][LP] brick src values
   V        *s_work = s_src + NP * LP;                // [WPB*CPW][WB]
-  T        *s_acc  = reinterpret_cast<T *>(s_work + WPB * CPW * WB); // [nc][LP]
+  // the accumulator lattice is FP64 for both precisions: ds_add_f32 costs
+  // ~10 us per FP32 vmult on gfx950 (ablation GLS_ABL_NOATOMIC: 38.1 -> 28.2
+  // us), ds_add_f64 next to nothing (40.1 -> 39.7 us)
+  double   *s_acc  = reinterpret_cast<double *>(s_work + WPB * CPW * WB); // [nc][LP]
   constexpr int RP = CoefRow<T, n>::RP;
   T        *s_tab  = reinterpret_cast<T *>(reinterpret_cast<unsigned char *>(s_acc) +
                                      LDS::tab_offset(LP)); // [4][n][RP]
@@ -501,7 +504,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
         {
           if (!R && ((cm >> c) & 1))
             u[it][c] = T(0);
-          s_acc[c * LP + ip] = T(0);
+          s_acc[c * LP + ip] = 0.0;
         }
       V v[NP];
       to_packs<V, T, nc, NP, W>(u[it], v);
@@ -725,7 +728,11 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
 #pragma unroll
             for (int w = 0; w < W; ++w)
               if (kp * W + w < nc)
-                lds_add(s_acc + (kp * W + w) * LP + li_now, r[w]);
+#ifdef GLS_ABL_NOATOMIC // diagnostic timing build only: racy plain adds
+                s_acc[(kp * W + w) * LP + li_now] += (double)r[w];
+#else
+                lds_add(s_acc + (kp * W + w) * LP + li_now, (double)r[w]);
+#endif
           }
       wave_sync();
     }
@@ -749,7 +756,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
           T r[nc];
 #pragma unroll
           for (int c = 0; c < nc; ++c)
-            r[c] = R ? -s_acc[c * LP + ip] : s_acc[c * LP + ip];
+            r[c] = (T)(R ? -s_acc[c * LP + ip] : s_acc[c * LP + ip]);
           store_node<T, nc>(a.partial, tgt & ~SHARED_BIT, r);
         }
       else
@@ -759,7 +766,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
 #pragma unroll
           for (int c = 0; c < nc; ++c)
             {
-              r[c] = R ? -s_acc[c * LP + ip] : s_acc[c * LP + ip];
+              r[c] = (T)(R ? -s_acc[c * LP + ip] : s_acc[c * LP + ip]);
               if ((cm >> c) & 1)
                 r[c] = R ? T(0) : a.src[(size_t)tgt * nc + c];
             }
