@@ -51,20 +51,35 @@ struct DevBuf
   }
 };
 
-struct Handle
+// one rocBLAS handle per host thread and device, created on first use
+// (creating one per solve cost milliseconds in a Newton loop); bound to the
+// caller's stream on every solve
+struct HandleCache
 {
-  rocblas_handle h = nullptr;
-  explicit Handle(hipStream_t s)
+  rocblas_handle h[64] = {};
+  ~HandleCache()
   {
-    RB_THROW(rocblas_create_handle(&h));
-    RB_THROW(rocblas_set_stream(h, s));
-    RB_THROW(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host));
-  }
-  ~Handle()
-  {
-    (void)rocblas_destroy_handle(h);
+    for (rocblas_handle x : h)
+      if (x)
+        (void)rocblas_destroy_handle(x);
   }
 };
+
+rocblas_handle
+blas_handle(hipStream_t s)
+{
+  static thread_local HandleCache cache;
+  int                             dev = 0;
+  HIP_THROW(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64)
+    throw std::runtime_error("gls_gmres_solve: device ordinal out of range");
+  rocblas_handle &h = cache.h[dev];
+  if (!h)
+    RB_THROW(rocblas_create_handle(&h));
+  RB_THROW(rocblas_set_stream(h, s));
+  RB_THROW(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host));
+  return h;
+}
 
 // r = b - r (r holds A x on entry)
 __global__ void
@@ -111,8 +126,7 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   const int      m = desc->max_n_tmp_vectors - 2;
   double        *x = (double *)x_;
   const double  *b = (const double *)b_;
-  Handle         hb(s);
-  rocblas_handle h = hb.h;
+  rocblas_handle h = blas_handle(s);
   DevBuf         V((size_t)(m + 1) * n * sizeof(double)), w(n * sizeof(double)),
     z(n * sizeof(double)), dh(2 * (m + 1) * sizeof(double));
   auto vcol = [&](int j) { return V.d() + (size_t)j * n; };
