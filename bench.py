@@ -37,9 +37,12 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(case_mesh, cmask, params, weights, u_star, hist, src, n_dofs, budget_s=12.0):
-    """Oracle (CPU restatement, 'port') timed on the host cores: bounded
-    sample of the same workload (whole vmults of the same mesh)."""
+PARITY_TOL = {"f64": 1e-12, "f32": 2e-5}  # relative l2 vs the oracle (tests/ use the same)
+
+
+def make_oracle(case_mesh, cmask, params, weights, u_star, hist):
+    """The CPU restatement (oracle/, TEST INFRASTRUCTURE) on the bench's own
+    inputs: the checker of the headline result and the cpu_baseline leg."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
@@ -49,6 +52,21 @@ def cpu_baseline(case_mesh, cmask, params, weights, u_star, hist, src, n_dofs, b
     o.set_linearization_point(u_star)
     if params["order"] > 0:
         o.set_previous_solution(hist, weights)
+    o._threads = threads
+    o._mesh = om
+    return o
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def cpu_baseline(o, src, n_dofs, budget_s=12.0):
+    """Oracle (CPU restatement, 'port') timed on the host cores: bounded
+    sample of the same workload (whole vmults of the same mesh)."""
+    threads = o._threads
     o.vmult(src)  # warm-up
     reps, t0 = 0, time.perf_counter()
     while True:
@@ -205,6 +223,11 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--brick", default=None,
                     help="cells per brick 'bx,by,bz' (a sub-brick of the mesh order)")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the oracle check of the headline result (profiling runs)")
+    ap.add_argument("--allow-p2p-fallback", action="store_true",
+                    help="multi-GPU: on a native/P2P mismatch time the torch P2P path "
+                         "instead of failing")
     args = ap.parse_args()
 
     import torch
@@ -257,8 +280,15 @@ def main():
         rel = float(err[0]) / max(float(err[1]), 1e-300)
         log(f"[bench] native vs p2p partitioned vmult: rel err {rel:.2e}")
         if not rel < 1e-12:
+            if not args.allow_p2p_fallback:
+                if rank == 0:
+                    print(json.dumps({"error": "native RCCL partitioned vmult disagrees with "
+                                               "the torch P2P path", "rel_l2": rel}), flush=True)
+                dist.barrier()
+                dist.destroy_process_group()
+                sys.exit(4)
             runner.native = None
-            exchange = f"torch-p2p (native mismatch {rel:.1e})"
+            exchange = f"torch-p2p (native mismatch {rel:.1e}, --allow-p2p-fallback)"
         apply_fn = lambda: runner.vmult(dst, src)  # noqa: E731
         local_cells = runner.n_local_cells
         op = runner.op
@@ -323,6 +353,38 @@ def main():
 
     bytes_per_vmult = op.vmult_bytes()
     n_gen, n_cart = op.geometry_counts()
+    # parity of the timed result: the headline dst (FP64) against the oracle
+    # on the same inputs (and the FP32 level operator at N = 1); a result
+    # outside the tolerance fails the run
+    got = None
+    if not args.no_parity:
+        apply_fn()
+        torch.cuda.synchronize()
+        got = (runner.gather_global(dst) if use_dist else dst).double().cpu().numpy()
+    o = None
+    if rank == 0 and (not args.no_parity or not args.no_cpu_baseline):
+        o = make_oracle(mesh, cmask, params, weights, u_star, hist)
+    parity = None
+    if rank == 0 and not args.no_parity:
+        ref = o.vmult(src_h)
+        parity = {"rel_l2_" + args.precision: rel_l2(got, ref),
+                  "tol_" + args.precision: PARITY_TOL[args.precision],
+                  "oracle": "oracle/gls_oracle.c on the same mesh and inputs"}
+        if world == 1 and not use_dist and args.precision == "f64":
+            op32 = glsamd.NavierStokesOperator(mesh, cmask, "f32")
+            op32.set_parameters(**params)
+            op32.set_linearization_point(u_star)
+            if params["order"] > 0:
+                op32.set_previous_solution(hist, weights)
+            d32 = op32.initialize_dof_vector()
+            op32.vmult(d32, op32._dev(src_h))
+            torch.cuda.synchronize()
+            parity["rel_l2_f32"] = rel_l2(d32.double().cpu().numpy(), ref)
+            parity["tol_f32"] = PARITY_TOL["f32"]
+            del op32, d32
+        parity["ok"] = all(parity["rel_l2_" + p] < parity["tol_" + p]
+                           for p in ("f64", "f32") if "rel_l2_" + p in parity)
+        log(f"[bench] parity vs oracle: {parity}")
     out = None
     if rank == 0:
         if kernel_ms is None:
@@ -348,8 +410,7 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
-                cpu = cpu_baseline(mesh, cmask, params, weights, u_star, hist, src_h, n_dofs,
-                                   args.cpu_budget)
+                cpu = cpu_baseline(o, src_h, n_dofs, args.cpu_budget)
             except Exception as e:  # baseline is reported, never fatal
                 cpu = dict(value=None, unit="DoF/s", cores=0, kind="port", sample=f"failed: {e}")
         out = {
@@ -377,12 +438,20 @@ def main():
                                    "gls::k_shared_reduce_cls (both inside the events)",
                          "kernel_ms": kernel_ms, "algorithmic_bytes": bytes_per_vmult},
             "cpu_baseline": cpu,
+            "parity": parity,
             "companions": comp,
         }
         print(json.dumps(out), flush=True)
+    ok = parity is None or parity["ok"]
     if dist is not None:
+        t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)
+        ok = float(t.item()) == 0.0
         dist.barrier()
         dist.destroy_process_group()
+    if not ok:
+        log("[bench] FAILED: result outside the parity tolerance")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -40,10 +40,6 @@
 
 namespace gls
 {
-void brick_launch(const glsOp_ *op, int mode, void *dst, const void *src, int64_t b0, int64_t b1,
-                  int what, hipStream_t s);
-int  op_vmult_mode(const glsOp_ *op);
-
 // send buffer <- src rows of the send nodes (plain values)
 template <typename T, int nc>
 __global__ void __launch_bounds__(256)

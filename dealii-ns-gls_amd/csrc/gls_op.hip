@@ -550,7 +550,7 @@ struct Impl
   // fully (over)written
   static void
   brick(const glsOp_ *op, int mode, void *dst, const void *src, int64_t b0, int64_t b1,
-        int what, hipStream_t s)
+        int what, hipStream_t s, const RelaxStep *rx)
   {
     if constexpr (BrickLattice<dim, k>::fits)
       {
@@ -569,9 +569,9 @@ struct Impl
         a.dst           = (T *)dst;
         a.src           = (const T *)src;
         a.partial       = (T *)op->d_partial;
-        a.rb            = (const T *)op->relax_b;
-        a.rd            = (const T *)op->relax_d;
-        a.romega        = (T)op->relax_omega;
+        a.rb            = rx ? (const T *)rx->b : nullptr;
+        a.rd            = rx ? (const T *)rx->d : nullptr;
+        a.romega        = rx ? (T)rx->omega : T(0);
         a.brick_begin   = b0;
         a.brick_end     = b1;
         a.bx            = op->bx;
@@ -707,7 +707,7 @@ select(const glsOp_ *op, ApplyFn &af, ProduceFn &pf)
 }
 
 using BrickFn = void (*)(const glsOp_ *, int, void *, const void *, int64_t, int64_t, int,
-                         hipStream_t);
+                         hipStream_t, const RelaxStep *);
 
 template <typename T>
 BrickFn
@@ -770,12 +770,12 @@ namespace gls
 // the pieces of vmult dist.hip orchestrates around the ghost exchange
 void
 brick_launch(const glsOp_ *op, int mode, void *dst, const void *src, int64_t b0, int64_t b1,
-             int what, hipStream_t s)
+             int what, hipStream_t s, const RelaxStep *rx)
 {
   BrickFn f = select_brick(op);
   if (!f)
     throw std::runtime_error("no brick kernel for this (dim, degree)");
-  f(op, mode, dst, src, b0, b1, what, s);
+  f(op, mode, dst, src, b0, b1, what, s, rx);
 }
 
 int
@@ -1038,7 +1038,7 @@ gls_op_destroy(glsOp op)
                   op->d_brick_target, op->d_shared_nodes, op->d_shared_off,
                   op->d_partial,      op->d_bgeo_cart,    op->d_bgeo_gen,
                   op->d_brick_geo,    op->d_brick_cell0,  op->d_brick_chunk0, op->d_tab_cbase,
-                  op->d_node_cmask,   op->d_inhom};
+                  op->d_node_cmask,   op->d_inhom,        op->gmres_ws};
   for (void *b : bufs)
     if (b)
       (void)hipFree(b);
@@ -1196,7 +1196,8 @@ gls_op_vmult(glsOp op, void *dst, const void *src, void *stream)
   select(op, af, pf);
   hipStream_t s = (hipStream_t)stream;
   if (op->use_brick)
-    select_brick(op)(op, vmult_mode(op), dst, src, 0, op->n_bricks, BRICK_RUN | BRICK_REDUCE, s);
+    select_brick(op)(op, vmult_mode(op), dst, src, 0, op->n_bricks, BRICK_RUN | BRICK_REDUCE, s,
+                     nullptr);
   else
     {
       init_dst(op, dst, src, s);
@@ -1280,7 +1281,7 @@ residual_cells(glsOp op, void *dst, const void *src, hipStream_t s)
   select(op, af, pf);
   if (op->use_brick)
     select_brick(op)(op, MODE_RESIDUAL, dst, src, 0, op->n_bricks, BRICK_RUN | BRICK_REDUCE,
-                     s);
+                     s, nullptr);
   else
     {
       HIP_THROW(hipMemsetAsync(dst, 0, (size_t)op->n_dofs * op->tsize(), s));
@@ -1333,7 +1334,7 @@ gls_op_evaluate_residual_plain(glsOp op, void *dst, const void *src, void *strea
   hipStream_t s = (hipStream_t)stream;
   if (op->use_brick)
     select_brick(op)(op, MODE_RESIDUAL, dst, src, 0, op->n_bricks, BRICK_RUN | BRICK_REDUCE,
-                     s);
+                     s, nullptr);
   else
     {
       HIP_THROW(hipMemsetAsync(dst, 0, (size_t)op->n_dofs * op->tsize(), s));

@@ -33,24 +33,6 @@ namespace
     }                                                                                        \
   while (0)
 
-struct DevBuf
-{
-  void *p = nullptr;
-  explicit DevBuf(size_t bytes)
-  {
-    HIP_THROW(hipMalloc(&p, bytes > 0 ? bytes : 8));
-  }
-  ~DevBuf()
-  {
-    (void)hipFree(p);
-  }
-  double *
-  d() const
-  {
-    return (double *)p;
-  }
-};
-
 // one rocBLAS handle per host thread and device, created on first use
 // (creating one per solve cost milliseconds in a Newton loop); bound to the
 // caller's stream on every solve
@@ -66,11 +48,9 @@ struct HandleCache
 };
 
 rocblas_handle
-blas_handle(hipStream_t s)
+blas_handle(int dev, hipStream_t s)
 {
   static thread_local HandleCache cache;
-  int                             dev = 0;
-  HIP_THROW(hipGetDevice(&dev));
   if (dev < 0 || dev >= 64)
     throw std::runtime_error("gls_gmres_solve: device ordinal out of range");
   rocblas_handle &h = cache.h[dev];
@@ -126,9 +106,36 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   const int      m = desc->max_n_tmp_vectors - 2;
   double        *x = (double *)x_;
   const double  *b = (const double *)b_;
-  rocblas_handle h = blas_handle(s);
-  DevBuf         V((size_t)(m + 1) * n * sizeof(double)), w(n * sizeof(double)),
-    z(n * sizeof(double)), dh(2 * (m + 1) * sizeof(double));
+  // the operator's device, its rocBLAS handle, and the Krylov workspace
+  // [V (m+1) n | w n | z n | dh 2 (m+1)] kept on the operator and grown on
+  // demand (a hipMalloc/hipFree of the basis per solve synchronises the
+  // device and costs more than the solve's setup)
+  HIP_THROW(hipSetDevice(op->device));
+  rocblas_handle h  = blas_handle(op->device, s);
+  const size_t   ws = ((size_t)(m + 3) * n + 2 * (m + 1)) * sizeof(double);
+  if (op->gmres_ws_bytes < ws)
+    {
+      if (op->gmres_ws)
+        {
+          HIP_THROW(hipStreamSynchronize(s));
+          HIP_THROW(hipFree(op->gmres_ws));
+          op->gmres_ws = nullptr;
+        }
+      HIP_THROW(hipMalloc(&op->gmres_ws, ws));
+      op->gmres_ws_bytes = ws;
+    }
+  struct View
+  {
+    double *p;
+    double *
+    d() const
+    {
+      return p;
+    }
+  };
+  double    *wsd = (double *)op->gmres_ws;
+  const View V{wsd}, w{wsd + (size_t)(m + 1) * n}, z{wsd + (size_t)(m + 2) * n},
+    dh{wsd + (size_t)(m + 3) * n};
   auto vcol = [&](int j) { return V.d() + (size_t)j * n; };
   auto precondition = [&](double *dst, const double *src) {
     if (mg)

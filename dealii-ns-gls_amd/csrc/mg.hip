@@ -20,6 +20,7 @@
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 #include <string>
@@ -235,40 +236,85 @@ k_convert(Tout *__restrict__ dst, const Tin *__restrict__ src, int64_t n)
     dst[i] = (Tout)src[i];
 }
 
-// y = d . y ; sums of squares of y (after) and x into acc[0], acc[1]
+// power iteration step (deal.II power_iteration, see power_iteration_t):
+// y = D^{-1} (A x) in place; per-block partial sums of x.y and y.y into
+// part[2 block], part[2 block + 1] (no atomics: k_power_finish adds the
+// blocks in a fixed order)
 template <typename T>
-__global__ void
-k_power_step(T *__restrict__ y, const T *__restrict__ x, const T *__restrict__ d,
-             double *__restrict__ acc, int64_t n)
+__global__ void __launch_bounds__(256)
+  k_power_step(T *__restrict__ y, const T *__restrict__ x, const T *__restrict__ d,
+               double *__restrict__ part, int64_t n)
 {
-  const int64_t i  = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  double        yy = 0, xx = 0;
+  __shared__ double red[2][4];
+  const int64_t     i  = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double            xy = 0, yy = 0;
   if (i < n)
     {
       const T v = d[i] * y[i];
       y[i]      = v;
-      yy        = (double)v * v;
-      xx        = (double)x[i] * x[i];
+      xy        = (double)x[i] * (double)v;
+      yy        = (double)v * (double)v;
     }
   for (int off = 32; off > 0; off >>= 1)
     {
+      xy += __shfl_down(xy, off);
       yy += __shfl_down(yy, off);
-      xx += __shfl_down(xx, off);
     }
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0)
     {
-      unsafeAtomicAdd(acc, yy);
-      unsafeAtomicAdd(acc + 1, xx);
+      red[0][w] = xy;
+      red[1][w] = yy;
+    }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    {
+      part[2 * blockIdx.x]     = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+      part[2 * blockIdx.x + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
     }
 }
 
+// one workgroup: scal[0] = x.y (the Rayleigh quotient of the normalised x),
+// scal[1] = 1 / |y| (0 if y = 0)
+__global__ void __launch_bounds__(256)
+  k_power_finish(const double *__restrict__ part, int64_t n_blocks, double *__restrict__ scal)
+{
+  __shared__ double red[2][256];
+  double            xy = 0, yy = 0;
+  for (int64_t b = threadIdx.x; b < n_blocks; b += 256)
+    {
+      xy += part[2 * b];
+      yy += part[2 * b + 1];
+    }
+  red[0][threadIdx.x] = xy;
+  red[1][threadIdx.x] = yy;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1)
+    {
+      if ((int)threadIdx.x < s)
+        {
+          red[0][threadIdx.x] += red[0][threadIdx.x + s];
+          red[1][threadIdx.x] += red[1][threadIdx.x + s];
+        }
+      __syncthreads();
+    }
+  if (threadIdx.x == 0)
+    {
+      scal[0] = red[0][0];
+      scal[1] = red[1][0] > 0 ? 1.0 / sqrt(red[1][0]) : 0.0;
+    }
+}
+
+// x = scal[1] * y (the scale factor stays on the device: no host round trip
+// per power iteration)
 template <typename T>
 __global__ void
-k_scale(T *__restrict__ x, const T *__restrict__ y, double s, int64_t n)
+k_scale_dev(T *__restrict__ x, const T *__restrict__ y, const double *__restrict__ scal,
+            int64_t n)
 {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n)
-    x[i] = (T)(s * y[i]);
+    x[i] = (T)(scal[1] * (double)y[i]);
 }
 
 dim3
@@ -288,7 +334,8 @@ struct glsMG_
   std::vector<void *>     d_weight; // level l >= 1: [n_dofs(l)]
   std::vector<void *>     invdiag, sol, def, tmp;
   std::vector<double>     omega, lambda;
-  double                 *d_acc = nullptr;
+  double                 *d_acc = nullptr; // power iteration: block partials | 2 scalars
+  int64_t                 acc_blocks = 0;
   double                  P[MAXP][MAXN]{};
   bool                    setup_done = false;
   // dense LU coarse solver (coarse_n_iterations < 0): the substitute for the
@@ -421,16 +468,15 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
       relax(mg, level, x, b, 0, s);
       ++it;
     }
-  void *cur = x, *oth = mg->tmp[level];
+  void          *cur = x, *oth = mg->tmp[level];
+  gls::RelaxStep rx;
+  rx.b     = b;
+  rx.d     = mg->invdiag[level];
+  rx.omega = mg->omega[level];
   for (; it < iters; ++it)
     {
-      op->relax_b     = b;
-      op->relax_d     = mg->invdiag[level];
-      op->relax_omega = mg->omega[level];
-      const glsStatus st = gls_op_vmult(op, oth, cur, s);
-      op->relax_b = op->relax_d = nullptr;
-      op->relax_omega           = 0.0;
-      check(st);
+      gls::brick_launch(op, gls::op_vmult_mode(op), oth, cur, 0, op->n_bricks,
+                        gls::BRICK_RUN | gls::BRICK_REDUCE, s, &rx);
       std::swap(cur, oth);
     }
 }
@@ -561,49 +607,71 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
   smooth(mg, l, mg->sol[l], mg->def[l], false, nit, s);
 }
 
+// Relaxation-factor estimate of PreconditionRelaxation with relaxation = 0
+// and EigenvalueAlgorithm::power_iteration (multigrid.cc:294-305, 353-369).
+// Restates deal.II (>= 9.4, not vendored):
+//   internal::PreconditionChebyshevImplementation::set_initial_guess:
+//     x_i = i % 11 on the global index, minus the mean; then
+//     AdditionalData::constraints.set_zero(x)
+//   power_iteration(matrix, x, D^{-1}, eig_cg_n_iterations):
+//     x /= |x|; repeat: y = D^{-1} A x; lambda = x . y; x = y / |y|;
+//     return |lambda|
+//   estimate_eigenvalues: max_eigenvalue_estimate = 1.2 * lambda (safety
+//     factor), and PreconditionRelaxation::estimate_eigenvalues then sets
+//     omega = 2 / (alpha + max), alpha = max / smoothing_range.
+// The index i is this library's dof numbering (node-major), not deal.II's
+// DoFHandler numbering, so the start vector is the same formula on a
+// different numbering (deviation).  All reductions stay on the
+// device; the host reads lambda once after the last iteration.
 template <typename T>
 double
 power_iteration_t(glsMG_ *mg, int l, hipStream_t s)
 {
   glsOp         op = mg->ops[l];
   const int64_t n  = op->n_dofs;
-  // start vector: deterministic pseudo-random, zero on constrained dofs
-  // (AdditionalData::constraints, multigrid.cc:303-304)
-  std::vector<T> h(n);
-  uint64_t       z = 0x9E3779B97F4A7C15ULL * (uint64_t)(l + 1);
+  std::vector<double> h((size_t)n);
+  double              mean = 0;
   for (int64_t i = 0; i < n; ++i)
     {
-      z += 0x9E3779B97F4A7C15ULL;
-      uint64_t r = z;
-      r          = (r ^ (r >> 30)) * 0xBF58476D1CE4E5B9ULL;
-      r          = (r ^ (r >> 27)) * 0x94D049BB133111EBULL;
-      r ^= r >> 31;
+      h[i] = (double)(i % 11);
+      mean += h[i];
+    }
+  mean /= (double)std::max<int64_t>(1, n);
+  double nrm = 0;
+  for (int64_t i = 0; i < n; ++i)
+    {
       const int64_t node = i / (op->dim + 1);
       const int     comp = (int)(i % (op->dim + 1));
-      const bool    con  = node < op->n_nodes && ((op->h_cmask[node] >> comp) & 1);
-      h[i]               = con ? T(0) : (T)((double)(r >> 11) * 0x1.0p-53 - 0.5);
+      const bool    con  = (op->h_cmask[node] >> comp) & 1;
+      h[i]               = con ? 0.0 : h[i] - mean;
+      nrm += h[i] * h[i];
     }
+  nrm = std::sqrt(nrm);
+  std::vector<T> hx((size_t)n);
+  for (int64_t i = 0; i < n; ++i)
+    hx[i] = (T)(nrm > 0 ? h[i] / nrm : 0.0);
   void *x = mg->sol[l], *y = mg->tmp[l];
-  HIP_THROW(hipMemcpyAsync(x, h.data(), n * sizeof(T), hipMemcpyHostToDevice, s));
-  double lam = 0;
+  HIP_THROW(hipMemcpyAsync(x, hx.data(), n * sizeof(T), hipMemcpyHostToDevice, s));
+  const int64_t nb   = (n + 255) / 256;
+  double       *part = mg->d_acc, *scal = mg->d_acc + 2 * mg->acc_blocks;
+  if (nb > mg->acc_blocks)
+    throw std::runtime_error("power iteration: reduction buffer too small");
+  HIP_THROW(hipMemsetAsync(scal, 0, 2 * sizeof(double), s));
   for (int it = 0; it < mg->desc.smoothing_eig_n_iterations; ++it)
     {
       check(gls_op_vmult(op, y, x, s));
-      HIP_THROW(hipMemsetAsync(mg->d_acc, 0, 2 * sizeof(double), s));
       hipLaunchKernelGGL(k_power_step<T>, g1(n), dim3(256), 0, s, (T *)y, (const T *)x,
-                         (const T *)mg->invdiag[l], mg->d_acc, n);
-      HIP_THROW(hipGetLastError());
-      double acc[2];
-      HIP_THROW(hipMemcpyAsync(acc, mg->d_acc, sizeof(acc), hipMemcpyDeviceToHost, s));
-      HIP_THROW(hipStreamSynchronize(s));
-      if (acc[0] <= 0 || acc[1] <= 0)
-        break;
-      lam = std::sqrt(acc[0] / acc[1]);
-      hipLaunchKernelGGL(k_scale<T>, g1(n), dim3(256), 0, s, (T *)x, (const T *)y,
-                         1.0 / std::sqrt(acc[0]), n);
+                         (const T *)mg->invdiag[l], part, n);
+      hipLaunchKernelGGL(k_power_finish, dim3(1), dim3(256), 0, s, (const double *)part, nb,
+                         scal);
+      hipLaunchKernelGGL(k_scale_dev<T>, g1(n), dim3(256), 0, s, (T *)x, (const T *)y,
+                         (const double *)scal, n);
       HIP_THROW(hipGetLastError());
     }
-  return lam;
+  double lam = 0;
+  HIP_THROW(hipMemcpyAsync(&lam, scal, sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_THROW(hipStreamSynchronize(s));
+  return std::abs(lam);
 }
 
 } // namespace
@@ -703,7 +771,9 @@ gls_mg_create(const glsMGDesc *desc, const glsOp *levels, const uint32_t *const 
     }
   mg->omega.assign(nl_levels, 1.0);
   mg->lambda.assign(nl_levels, 0.0);
-  HIP_THROW(hipMalloc((void **)&mg->d_acc, 2 * sizeof(double)));
+  for (int l = 0; l < nl_levels; ++l)
+    mg->acc_blocks = std::max<int64_t>(mg->acc_blocks, (mg->ops[l]->n_dofs + 255) / 256);
+  HIP_THROW(hipMalloc((void **)&mg->d_acc, (2 * mg->acc_blocks + 2) * sizeof(double)));
   *out = mg;
   GLS_CATCH
 }
@@ -744,21 +814,34 @@ gls_mg_setup(glsMG mg, void *stream)
     {
       // compute_inverse_diagonal (multigrid.cc:290-293)
       check(gls_op_compute_inverse_diagonal(mg->ops[l], mg->invdiag[l], s));
-      // relaxation = 0: omega from a power-iteration estimate of
-      // lambda_max(D^-1 A), alpha = lambda_max / smoothing_range,
-      // omega = 2 / (alpha + lambda_max)  (multigrid.cc:294-305, 353-369)
-      const double lam = mg->prec == GLS_F64 ? power_iteration_t<double>(mg, (int)l, s) :
-                                               power_iteration_t<float>(mg, (int)l, s);
-      mg->lambda[l]    = lam;
-      if (lam > 0)
+      // relaxation = 0: omega from the power-iteration estimate of
+      // lambda_max(D^-1 A) (power_iteration_t), estimated on the levels
+      // above the coarsest one (multigrid.cc:355-358 with
+      // compute_evs_n_levels = 0); the coarse level's smoother is used only
+      // by the relaxation coarse solve (coarse_n_iterations > 0), which
+      // then gets an estimate too
+      if (l == 0 && mg->ops.size() > 1 && mg->desc.coarse_n_iterations <= 0 &&
+          mg->desc.compute_evs_n_levels <= 0)
         {
-          const double alpha = mg->desc.smoothing_range > 1.0 ?
-                                 lam / mg->desc.smoothing_range :
-                                 0.9 * lam;
-          mg->omega[l] = 2.0 / (alpha + lam);
+          mg->lambda[l] = 0.0;
+          mg->omega[l]  = 1.0;
         }
       else
-        mg->omega[l] = 1.0;
+        {
+          const double lam = mg->prec == GLS_F64 ? power_iteration_t<double>(mg, (int)l, s) :
+                                                   power_iteration_t<float>(mg, (int)l, s);
+          const double ev_max = 1.2 * lam; // estimate_eigenvalues' safety factor
+          mg->lambda[l]       = ev_max;
+          if (ev_max > 0)
+            {
+              const double alpha = mg->desc.smoothing_range > 1.0 ?
+                                     ev_max / mg->desc.smoothing_range :
+                                     0.9 * ev_max;
+              mg->omega[l] = 2.0 / (alpha + ev_max);
+            }
+          else
+            mg->omega[l] = 1.0;
+        }
       HIP_THROW(hipMemsetAsync(mg->sol[l], 0, (size_t)mg->ops[l]->n_dofs * mg->ts(), s));
     }
   if (mg->desc.coarse_n_iterations < 0)

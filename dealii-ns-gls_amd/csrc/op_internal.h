@@ -39,10 +39,9 @@ struct glsOp_
   void     *d_inhom      = nullptr; // [n_dofs] inhomogeneity of constraints_inhomogeneous
                                     // (values on constrained dofs), or null = all zero
   int       device     = 0;
-  // fused damped-Jacobi step for the next brick vmult (set by the multigrid
-  // smoother around one gls_op_vmult call, csrc/mg.hip)
-  const void *relax_b = nullptr, *relax_d = nullptr;
-  double      relax_omega = 0.0;
+  // gls_gmres_solve workspace (Krylov basis and vectors), grown on demand
+  void     *gmres_ws       = nullptr;
+  size_t    gmres_ws_bytes = 0;
 
   // brick decomposition (csrc/brick.h)
   bool      use_brick = false;
@@ -74,3 +73,24 @@ struct glsOp_
     return prec == GLS_F64 ? 8 : 4;
   }
 };
+
+namespace gls
+{
+// fused damped-Jacobi step of the multigrid smoother (csrc/mg.hip): with it a
+// brick vmult writes x + omega * d . (b - A x) instead of A x.  Passed per
+// launch, never stored on the handle (a concurrent plain vmult on the same
+// level operator stays a plain vmult).
+struct RelaxStep
+{
+  const void *b     = nullptr;
+  const void *d     = nullptr;
+  double      omega = 0.0;
+};
+
+// the pieces of vmult that dist.hip / mg.hip orchestrate (gls_op.hip):
+// brick kernel over work units [b0, b1) (what & BRICK_RUN) and the
+// shared-node reduction (what & BRICK_REDUCE)
+void brick_launch(const glsOp_ *op, int mode, void *dst, const void *src, int64_t b0,
+                  int64_t b1, int what, hipStream_t s, const RelaxStep *rx = nullptr);
+int  op_vmult_mode(const glsOp_ *op);
+} // namespace gls

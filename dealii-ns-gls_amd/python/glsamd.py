@@ -53,7 +53,8 @@ class OpParams(C.Structure):
 class MGDesc(C.Structure):
     _fields_ = [("n_levels", C.c_int), ("smoothing_n_iterations", C.c_int),
                 ("smoothing_eig_n_iterations", C.c_int), ("smoothing_range", C.c_double),
-                ("coarse_n_iterations", C.c_int), ("outer_precision", C.c_int)]
+                ("coarse_n_iterations", C.c_int), ("outer_precision", C.c_int),
+                ("compute_evs_n_levels", C.c_int)]
 
 
 class DistDesc(C.Structure):
@@ -369,7 +370,7 @@ class Multigrid:
 
     def __init__(self, level_ops, child_lattices, smoothing_n_iterations=5,
                  smoothing_eig_n_iterations=20, smoothing_range=20.0, coarse_n_iterations=20,
-                 outer_precision="f64"):
+                 outer_precision="f64", compute_evs_n_levels=0):
         self.ops = list(level_ops)
         self._child = [None] + [np.ascontiguousarray(c, dtype=np.uint32)
                                 for c in child_lattices]
@@ -378,7 +379,7 @@ class Multigrid:
         ch = (C.c_void_p * n)(*[0 if c is None else c.ctypes.data for c in self._child])
         outer = GLS_F64 if outer_precision in ("f64", GLS_F64) else GLS_F32
         self.desc = MGDesc(n, smoothing_n_iterations, smoothing_eig_n_iterations,
-                           smoothing_range, coarse_n_iterations, outer)
+                           smoothing_range, coarse_n_iterations, outer, compute_evs_n_levels)
         self.outer_dtype = None
         h = C.c_void_p()
         _check(lib().gls_mg_create(C.byref(self.desc), C.cast(arr, C.c_void_p),

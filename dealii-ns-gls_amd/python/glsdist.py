@@ -27,8 +27,9 @@ Two transports:
     kernel.  In-process groups (LocalGroup, one device) run the same phases
     with device copies in place of RCCL.
   * torch.distributed point-to-point (batch_isend_irecv) with the per-rank
-    phases below (pack / unpack / local apply / fix): the CPU/gloo tests with
-    the oracle engine and the cross-check of the native path.
+    phases below (pack / unpack / local apply / fix): the CPU/gloo tests (the
+    tests inject a CPU oracle engine, tests/dist_engines.py) and the
+    cross-check of the native path.
 """
 from __future__ import annotations
 
@@ -184,42 +185,6 @@ class GpuEngine:
                                           nccl_id=nccl_id, group=group)
 
 
-class OracleEngine:
-    """TEST INFRASTRUCTURE: local operator = the CPU oracle on the rank-local
-    mesh, so the partition / exchange logic can be tested with gloo on a
-    machine without a GPU.  Never used by bench.py or the product path."""
-
-    def __init__(self, lmesh, cmask, n_owned, precision="f64"):
-        import torch
-        import oracle as orc
-        self.om = orc.OracleMesh(lmesh, cmask)
-        self.orc = orc
-        self.nc = lmesh.dim + 1
-        self.n_owned_dofs = n_owned * self.nc
-        cm = np.asarray(cmask[:n_owned], dtype=np.uint8)
-        bits = (cm[:, None] >> np.arange(self.nc)[None, :]) & 1
-        self.con = torch.from_numpy(np.flatnonzero(bits.ravel()))
-        self.dtype = torch.float64
-        self.device = "cpu"
-        self.o = None
-
-    def set_parameters(self, **params):
-        self.o = self.orc.Oracle(self.om, **params)
-
-    def set_linearization_point(self, v):
-        self.o.set_linearization_point(v.numpy())
-
-    def set_previous_solution(self, hist, w):
-        self.o.set_previous_solution([h.numpy() for h in hist], w)
-
-    def local_vmult(self, dst, src):
-        import torch
-        dst.copy_(torch.from_numpy(self.o.vmult(src.numpy())))
-
-    def identity_rows(self, dst, src):
-        dst[self.con] = src[self.con]
-
-
 # ------------------------------------------------------------------ rank state
 class RankOperator:
     """One rank's share of the distributed operator (phases of vmult)."""
@@ -230,7 +195,10 @@ class RankOperator:
         self.nc = mesh.dim + 1
         self.lmesh = LocalMesh(mesh, part)
         lcmask = np.ascontiguousarray(cmask[part.local_nodes], dtype=np.uint8)
-        cls = GpuEngine if engine == "gpu" else OracleEngine
+        # engine: "gpu" (the product path) or a local-operator factory with
+        # GpuEngine's interface (the CPU tests inject the oracle,
+        # tests/dist_engines.py)
+        cls = GpuEngine if engine == "gpu" else engine
         self.eng = cls(self.lmesh, lcmask, part.n_owned, precision)
         self.dtype, self.device = self.eng.dtype, self.eng.device
         self.n_dofs = part.n_nodes * self.nc

@@ -252,7 +252,8 @@ def hypercube(dim, degree, n_ref):
 
 
 # --------------------------------------------------------------------- decks
-DECK_DIR = os.path.normpath(os.path.join(_HERE, "..", "..", "tests", "decks"))
+# the five input decks of the reference (input/*.json), shipped as package data
+DECK_DIR = os.path.normpath(os.path.join(_HERE, "..", "data", "decks"))
 
 
 @dataclass

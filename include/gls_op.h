@@ -16,12 +16,12 @@
  *                                      operator_ns.h:102-114,
  *                                      time_integration.h:10-36
  *   gls_op_set_linearization_point   OperatorBase::set_linearization_point
- *                                      operator_base.h:38-39, .cc:570-620
+ *                                      operator_base.h:35-36, operator_ns.cc:570-620
  *                                      (+ compute_penalty_parameters :322-421)
  *   gls_op_set_previous_solution     OperatorBase::set_previous_solution
- *                                      operator_base.h:35-36, .cc:234-320
+ *                                      operator_base.h:32-33, operator_ns.cc:234-320
  *   gls_op_vmult                     OperatorBase::vmult
- *                                      operator_base.h:47-48, .cc:684-732
+ *                                      operator_base.h:45-46, operator_ns.cc:684-732
  *   gls_op_vmult_init /
  *   gls_op_vmult_cells /
  *   gls_op_apply_identity_rows       the pieces of vmult around the ghost
@@ -29,15 +29,15 @@
  *                                      update_ghost_values / compress(add),
  *                                      .cc:702-721) for multi-GPU
  *   gls_op_evaluate_residual         OperatorBase::evaluate_residual
- *                                      operator_base.h:44-46, .cc:648-682
+ *                                      operator_base.h:41-43, operator_ns.cc:648-682
  *   gls_op_evaluate_rhs              OperatorBase::evaluate_rhs
- *                                      operator_base.h:38-39, .cc:622-646
+ *                                      operator_base.h:38-39, operator_ns.cc:622-646
  *   gls_op_set_constraint_values     the constraints_inhomogeneous the
  *                                      operator holds by reference
  *                                      (operator_ns.h:95, main.cc:879-891)
  *   gls_op_compute_inverse_diagonal  OperatorBase::compute_inverse_diagonal
- *                                      operator_base.h:29-30, .cc:195-225
- *   gls_op_m                         OperatorBase::m  operator_base.h:23-24
+ *                                      operator_base.h:26-27, operator_ns.cc:195-225
+ *   gls_op_m                         OperatorBase::m  operator_base.h:20-21
  *   gls_op_upload_tables /
  *   gls_op_download_tables           host-produced / inspected per-q tables
  *                                      (u_star_value ... operator_ns.h:120-132)
@@ -192,6 +192,9 @@ typedef struct
                                   takes (GLS_F64: copy_to_mg / copy_from_mg
                                   convert to the level precision, as
                                   PreconditionMG does for MGNumber = float)  */
+  int    compute_evs_n_levels; /* "gmg compute evs n levels" (multigrid.cc:
+                                  307, 355-358): > 0 also estimates the
+                                  relaxation factor on the coarsest level    */
 } glsMGDesc;
 
 /* levels[l] are level operators (same precision); child[l] for l >= 1 is the

@@ -701,6 +701,9 @@ orc_compute_inverse_diagonal(const orc_op *op, double *diag)
   const int     nq = op->nq, nc = op->m.dim + 1, nd = nq * nc;
   const int64_t n  = op->m.n_nodes * nc;
   memset(diag, 0, sizeof(double) * (size_t)n);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(g_threads) if (g_threads > 1)
+#endif
   for (int64_t c = 0; c < op->m.n_cells; ++c)
     for (int j = 0; j < nd; ++j)
       {
@@ -711,7 +714,10 @@ orc_compute_inverse_diagonal(const orc_op *op, double *diag)
         double uloc[4][MAXNQ] = {{0}}, out[4][MAXNQ];
         uloc[comp][j / nc]    = 1.0;
         cell_apply(op, c, (const double(*)[MAXNQ])uloc, out, 0);
-        diag[(size_t)node * nc + comp] += out[comp][j / nc];
+        if (g_threads > 1)
+          atomic_add(&diag[(size_t)node * nc + comp], out[comp][j / nc]);
+        else
+          diag[(size_t)node * nc + comp] += out[comp][j / nc];
       }
   for (int64_t node = 0; node < op->m.n_nodes; ++node)
     for (int comp = 0; comp < nc; ++comp)

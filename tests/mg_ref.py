@@ -3,7 +3,8 @@
 
 Restates (deal.II semantics, not vendored; parity unpinned against the
 reference binary):
-  PreconditionRelaxation (relaxation = 0 -> power-iteration omega),
+  PreconditionRelaxation (relaxation = 0 -> power-iteration omega,
+    deal.II's set_initial_guess / power_iteration / 1.2 safety factor),
     multigrid.cc:281-369: vmult (zero start) = x = w D^-1 b then n-1 steps,
     step = n times x += w D^-1 (b - A x)
   Multigrid::level_v_step V-cycle with MGSmootherPrecondition pre/post
@@ -16,21 +17,18 @@ import numpy as np
 import oracle as orc
 
 
-def power_start_vector(n_dofs, level, cmask, dim):
-    """The deterministic start vector csrc/mg.hip uses (constrained -> 0)."""
-    M = (1 << 64) - 1
-    z = (0x9E3779B97F4A7C15 * (level + 1)) & M
-    out = np.empty(n_dofs)
+def power_start_vector(n_dofs, cmask, dim):
+    """deal.II internal::PreconditionChebyshevImplementation::set_initial_guess
+    (x_i = i % 11 on the global index, minus the mean) followed by
+    AdditionalData::constraints.set_zero (multigrid.cc:302-303), normalised as
+    power_iteration's first statement does.  deal.II >= 9.4, not vendored."""
+    x = (np.arange(n_dofs) % 11).astype(np.float64)
+    x -= x.mean()
     nc = dim + 1
-    for i in range(n_dofs):
-        z = (z + 0x9E3779B97F4A7C15) & M
-        r = z
-        r = ((r ^ (r >> 30)) * 0xBF58476D1CE4E5B9) & M
-        r = ((r ^ (r >> 27)) * 0x94D049BB133111EB) & M
-        r ^= r >> 31
-        con = (cmask[i // nc] >> (i % nc)) & 1
-        out[i] = 0.0 if con else (r >> 11) * 2.0 ** -53 - 0.5
-    return out
+    con = ((np.repeat(np.asarray(cmask, dtype=np.int64), nc)
+            >> np.tile(np.arange(nc), len(cmask))) & 1).astype(bool)
+    x[con] = 0.0
+    return x / np.linalg.norm(x)
 
 
 class OracleGMG:
@@ -75,27 +73,28 @@ class OracleGMG:
         orc.restrict_add(self.om[l - 1], self.om[l], self.child[l], dst_c, src_f)
 
     def estimate(self, l):
+        """max_eigenvalue_estimate of PreconditionRelaxation::estimate_eigenvalues
+        with EigenvalueAlgorithm::power_iteration: |x . D^-1 A x| of the
+        normalised iterate after n_eig steps, times the 1.2 safety factor."""
         m = self.meshes[l]
-        x = power_start_vector(m.n_dofs, l, self.om[l].cmask, m.dim)
+        x = power_start_vector(m.n_dofs, self.om[l].cmask, m.dim)
         lam = 0.0
         for _ in range(self.n_eig):
             y = self.invdiag[l] * self.ops[l].vmult(x)
-            ny, nx = np.linalg.norm(y), np.linalg.norm(x)
-            if ny == 0 or nx == 0:
-                break
-            lam = ny / nx
-            x = y / ny
-        return lam
+            lam = float(x @ y)
+            ny = np.linalg.norm(y)
+            x = y / ny if ny > 0 else 0.0 * y
+        return 1.2 * abs(lam)
 
     def set_omega(self, omegas):
         self.omega = list(omegas)
 
     def setup_omega(self):
         for l in range(len(self.ops)):
-            lam = self.estimate(l)
-            self.lam[l] = lam
-            alpha = lam / self.range if self.range > 1 else 0.9 * lam
-            self.omega[l] = 2.0 / (alpha + lam) if lam > 0 else 1.0
+            ev_max = self.estimate(l)
+            self.lam[l] = ev_max
+            alpha = ev_max / self.range if self.range > 1 else 0.9 * ev_max
+            self.omega[l] = 2.0 / (alpha + ev_max) if ev_max > 0 else 1.0
 
     def smooth(self, l, x, b, zero_start, iters):
         w, d, A = self.omega[l], self.invdiag[l], self.ops[l]

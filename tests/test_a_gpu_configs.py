@@ -1,0 +1,118 @@
+"""GPU parity at every BASELINE.json config's CONFIGURED size (the deck's own
+"n global refinements", shift, boundary conditions and time integrator), HIP
+path through the C-ABI vs the CPU oracle on the same mesh and §8d synthetic
+inputs.  The headline Re3900 r2 vmult is covered by test_gpu_parity.py; this
+file adds the larger decks and the headline's full 3-level V-cycle.
+
+Tolerances (relative l2): FP64 1e-12, FP32 2e-5 (operators); the FP32
+V-cycle against the FP64 oracle multigrid 5e-4 (test_gpu_mg.py).
+
+Named test_a_* so that these run first under `pytest -x`."""
+import numpy as np
+import pytest
+
+import glsinputs as gi
+from helpers import deck, deck_case, rel_err
+from mg_ref import OracleGMG
+
+pytestmark = pytest.mark.gpu
+TOL = {"f64": 1e-12, "f32": 2e-5}
+
+
+def _np(t):
+    return t.double().cpu().numpy()
+
+
+def _vmult(case, prec):
+    import torch
+    op = case.gpu(prec)
+    dst = op.initialize_dof_vector()
+    op.vmult(dst, op._dev(case.src))
+    torch.cuda.synchronize()
+    out = _np(dst)
+    del op, dst
+    torch.cuda.empty_cache()
+    return out
+
+
+@pytest.fixture(scope="module")
+def turek3d_r3():
+    # input_turek_3D_Re100.json as configured: r3 (204,800 cells, 6,789,120
+    # DoFs), cylinder shift 0.005, no-slip walls, BDF2
+    d = deck("input_turek_3D_Re100.json")
+    assert d.n_refinements == 3
+    case = deck_case("input_turek_3D_Re100.json")
+    assert case.n_dofs == 6789120
+    o = case.oracle()
+    return case, o.vmult(case.src), o.evaluate_residual(case.u_star)
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_turek3d_r3_vmult(turek3d_r3, prec):
+    case, ref, _ = turek3d_r3
+    assert rel_err(_vmult(case, prec), ref) < TOL[prec]
+
+
+def test_turek3d_r3_residual(turek3d_r3):
+    import torch
+    case, _, ref = turek3d_r3
+    op = case.gpu("f64")
+    res = op.initialize_dof_vector()
+    op.evaluate_residual_plain(res, op._dev(case.u_star))
+    torch.cuda.synchronize()
+    assert rel_err(_np(res), ref) < TOL["f64"]
+
+
+def test_sphere_r3_vmult():
+    # input_sphere_amg.json as configured: mesh/sphere.msh r3 (524,288 cells,
+    # 17,073,608 DoFs), every cell general geometry
+    d = deck("input_sphere_amg.json")
+    assert d.n_refinements == 3
+    case = deck_case("input_sphere_amg.json")
+    assert case.n_dofs == 17073608
+    ref = case.oracle().vmult(case.src)
+    assert rel_err(_vmult(case, "f64"), ref) < TOL["f64"]
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_turek2d_re100_r5_vmult(prec):
+    # input_turek_2D_Re100.json as configured: Q1, r5 (90,112 cells)
+    d = deck("input_turek_2D_Re100.json")
+    assert d.n_refinements == 5
+    case = deck_case("input_turek_2D_Re100.json")
+    ref = case.oracle().vmult(case.src)
+    assert rel_err(_vmult(case, prec), ref) < TOL[prec]
+
+
+def test_vcycle_re3900_r0_r2():
+    """The headline hierarchy (Re3900 r0 -> r1 -> r2, FP32 levels): relaxation
+    factors, one pre-smoothing and one full V-cycle against the oracle
+    multigrid.  Coarse solve: 10 relaxation sweeps — the substitute for the
+    deck's Trilinos direct solver, identical on both sides."""
+    import torch
+    import glsamd
+    d = deck("input_hoffmann_3D_Re3900.json")
+    meshes = [d.mesh(r) for r in range(d.n_refinements + 1)]
+    vel, p, slip = d.boundary_descriptor()
+    cm = [m.constraint_mask(vel, p, slip) for m in meshes]
+    params, w = d.operator_parameters(2.5e-4)
+    u = gi.linearization_point(meshes[-1].n_nodes, 3, d.u_max)
+    hist = gi.history(u, params["order"])
+    mg, ops = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f32",
+                               coarse_n_iterations=10)
+    ref = OracleGMG(meshes, cm, params, u, hist, w, coarse_iters=10)
+    for l in range(len(meshes)):
+        omega, lam = mg.relaxation(l)
+        lam_ref = ref.estimate(l)
+        assert abs(lam - lam_ref) < 1e-3 * lam_ref, (l, lam, lam_ref)
+    ref.set_omega([mg.relaxation(l)[0] for l in range(len(meshes))])
+    L = len(meshes) - 1
+    b = gi.rnd(11, meshes[L].n_dofs)
+    x = ops[L].initialize_dof_vector()
+    mg.smooth(L, x, ops[L]._dev(b), True)
+    src = torch.from_numpy(b).cuda()
+    dst = torch.zeros_like(src)
+    mg.vcycle(dst, src)
+    torch.cuda.synchronize()
+    assert rel_err(_np(x), ref.smooth(L, None, b, True, 5)) < 1e-4
+    assert rel_err(_np(dst), ref.vcycle(b)) < 5e-4

@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import glsdist
+from dist_engines import OracleEngine
 from helpers import deck_case, rel_err
 
 CASES = [("input_hoffmann_3D_Re3900.json", 1), ("input_turek_2D_Re100.json", 2)]
@@ -52,7 +53,7 @@ def _oracle_ref(c):
 def test_local_group_oracle(name, n_ref, world):
     import torch
     c = deck_case(name, n_ref)
-    g = glsdist.LocalGroup(c.mesh, c.cmask, world, engine="oracle")
+    g = glsdist.LocalGroup(c.mesh, c.cmask, world, engine=OracleEngine)
     g.setup(c.params, c.u_star, c.hist, c.weights)
     srcs = g.scatter(c.src)
     dsts = [r.new_vector() for r in g.ranks]
@@ -77,7 +78,7 @@ def _gloo_worker(rank, world, port, name, n_ref, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         c = dc(name, n_ref)
-        op = gd.DistributedOperator(c.mesh, c.cmask, "f64", dist, rank, world, engine="oracle")
+        op = gd.DistributedOperator(c.mesh, c.cmask, "f64", dist, rank, world, engine=OracleEngine)
         op.setup(c.params, c.u_star, c.hist, c.weights)
         src = op.scatter_global(c.src)
         src[op.r.n_owned_dofs:].zero_()  # ghosts must come from the exchange
