@@ -517,6 +517,51 @@ gls_dist_vmult_group(glsDist const *members, void *const *dsts, void *const *src
 }
 
 glsStatus
+gls_dist_update_ghost_values(glsDist d, void *vec, void *stream)
+{
+  GLS_TRY
+  if (!d || !vec)
+    throw std::runtime_error("gls_dist_update_ghost_values: null argument");
+  if (!d->comm)
+    throw std::runtime_error("gls_dist_update_ghost_values: RCCL ranks only");
+  hipStream_t s = (hipStream_t)stream;
+  if (!d->peers.empty())
+    {
+      pack(d, vec, s);
+      HIP_THROW(hipEventRecord(d->ev_packed, s));
+      HIP_THROW(hipStreamWaitEvent(d->cs, d->ev_packed, 0));
+      nccl_import(d, vec);
+      HIP_THROW(hipEventRecord(d->ev_imported, d->cs));
+      HIP_THROW(hipStreamWaitEvent(s, d->ev_imported, 0));
+    }
+  GLS_CATCH
+}
+
+glsStatus
+gls_dist_get_max_u(glsDist d, void *vec, double *u_max, void *stream)
+{
+  GLS_TRY
+  if (!d || !vec || !u_max)
+    throw std::runtime_error("gls_dist_get_max_u: null argument");
+  // operator_ns.cc:540-567: vec.update_ghost_values(); local max over the
+  // locally owned cells; Utilities::MPI::max
+  if (gls_dist_update_ghost_values(d, vec, stream) != 0)
+    throw std::runtime_error(gls_last_error());
+  double local = 0;
+  if (gls_op_get_max_u(d->op, vec, &local, stream) != 0)
+    throw std::runtime_error(gls_last_error());
+  hipStream_t s   = (hipStream_t)stream;
+  double     *buf = nullptr;
+  HIP_THROW(hipMallocAsync((void **)&buf, sizeof(double), s));
+  HIP_THROW(hipMemcpyAsync(buf, &local, sizeof(double), hipMemcpyHostToDevice, s));
+  NCCL_THROW(ncclAllReduce(buf, buf, 1, ncclDouble, ncclMax, d->comm, s));
+  HIP_THROW(hipMemcpyAsync(u_max, buf, sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_THROW(hipFreeAsync(buf, s));
+  HIP_THROW(hipStreamSynchronize(s));
+  GLS_CATCH
+}
+
+glsStatus
 gls_dist_interior_bricks(glsDist d, int64_t *n_interior, int64_t *n_total)
 {
   GLS_TRY

@@ -767,6 +767,24 @@ init_dst(const glsOp_ *op, void *dst, const void *src, hipStream_t s)
 
 namespace gls
 {
+void
+op_vmult_device(glsOp op, void *dst, const void *src, hipStream_t s)
+{
+  if (!op->have_lin)
+    throw std::runtime_error("vmult before set_linearization_point");
+  ApplyFn   af;
+  ProduceFn pf;
+  select(op, af, pf);
+  if (op->use_brick)
+    select_brick(op)(op, vmult_mode(op), dst, src, 0, op->n_bricks, BRICK_RUN | BRICK_REDUCE, s,
+                     nullptr);
+  else
+    {
+      init_dst(op, dst, src, s);
+      af(op, vmult_mode(op), false, dst, src, 0, op->n_cells, s);
+    }
+}
+
 // the pieces of vmult dist.hip orchestrates around the ghost exchange
 void
 brick_launch(const glsOp_ *op, int mode, void *dst, const void *src, int64_t b0, int64_t b1,
@@ -784,6 +802,268 @@ op_vmult_mode(const glsOp_ *op)
   return vmult_mode(op);
 }
 } // namespace gls
+
+
+// ------------------------------------------------------------ caller layout
+namespace
+{
+// op order <- caller order: out[map[i]] = in[i]
+template <typename T>
+__global__ void
+k_permute_in(T *__restrict__ out, const T *__restrict__ in, const int64_t *__restrict__ map,
+             int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    out[map[i]] = in[i];
+}
+
+// caller order <- op order: out[i] = in[map[i]]
+template <typename T>
+__global__ void
+k_permute_out(T *__restrict__ out, const T *__restrict__ in, const int64_t *__restrict__ map,
+              int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    out[i] = in[map[i]];
+}
+
+void
+permute(bool in_dir, size_t ts, void *out, const void *in, const int64_t *map, int64_t n,
+        hipStream_t s)
+{
+  const dim3 g((unsigned)((n + 255) / 256));
+  if (ts == 8)
+    {
+      if (in_dir)
+        hipLaunchKernelGGL(k_permute_in<double>, g, dim3(256), 0, s, (double *)out,
+                           (const double *)in, map, n);
+      else
+        hipLaunchKernelGGL(k_permute_out<double>, g, dim3(256), 0, s, (double *)out,
+                           (const double *)in, map, n);
+    }
+  else
+    {
+      if (in_dir)
+        hipLaunchKernelGGL(k_permute_in<float>, g, dim3(256), 0, s, (float *)out,
+                           (const float *)in, map, n);
+      else
+        hipLaunchKernelGGL(k_permute_out<float>, g, dim3(256), 0, s, (float *)out,
+                           (const float *)in, map, n);
+    }
+  HIP_THROW(hipGetLastError());
+}
+
+void *
+lazy(void *&p, size_t bytes)
+{
+  if (!p)
+    HIP_THROW(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+  return p;
+}
+} // namespace
+
+namespace gls
+{
+void
+VecStage::release()
+{
+  for (void *p : {(void *)d_map, raw, in[0], in[1], in[2], in[3], out})
+    if (p)
+      (void)hipFree(p);
+  d_map = nullptr;
+  raw = out = nullptr;
+  for (auto &p : in)
+    p = nullptr;
+}
+
+void
+VecStage::set(int mem, const int64_t *map, int64_t n_, size_t ts_)
+{
+  if (mem != GLS_MEM_DEVICE && mem != GLS_MEM_HOST)
+    throw std::runtime_error("vector layout: memory must be GLS_MEM_DEVICE or GLS_MEM_HOST");
+  if (map)
+    {
+      std::vector<char> seen((size_t)n_, 0);
+      for (int64_t i = 0; i < n_; ++i)
+        {
+          if (map[i] < 0 || map[i] >= n_ || seen[map[i]])
+            throw std::runtime_error("vector layout: dof_map is not a permutation of [0, m)");
+          seen[map[i]] = 1;
+        }
+    }
+  HIP_THROW(hipDeviceSynchronize());
+  release();
+  memory = mem;
+  n      = n_;
+  ts     = ts_;
+  if (map)
+    {
+      HIP_THROW(hipMalloc((void **)&d_map, std::max<size_t>(16, (size_t)n * sizeof(int64_t))));
+      HIP_THROW(hipMemcpy(d_map, map, (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice));
+    }
+}
+
+const void *
+VecStage::in_vec(const void *v, int slot, hipStream_t s)
+{
+  if (!active() || !v)
+    return v;
+  const size_t bytes = (size_t)n * ts;
+  void        *dst   = lazy(in[slot], bytes);
+  const void  *from  = v;
+  if (memory == GLS_MEM_HOST)
+    {
+      void *to = d_map ? lazy(raw, bytes) : dst;
+      HIP_THROW(hipMemcpyAsync(to, v, bytes, hipMemcpyHostToDevice, s));
+      from = to;
+    }
+  if (d_map)
+    permute(true, ts, dst, from, d_map, n, s);
+  return dst;
+}
+
+void *
+VecStage::out_vec(void *v)
+{
+  if (!active())
+    return v;
+  return lazy(out, (size_t)n * ts);
+}
+
+void
+VecStage::finish_out(void *v, hipStream_t s)
+{
+  if (!active())
+    return;
+  const size_t bytes = (size_t)n * ts;
+  const void  *res   = out;
+  if (d_map)
+    {
+      void *to = memory == GLS_MEM_HOST ? lazy(raw, bytes) : v;
+      permute(false, ts, to, out, d_map, n, s);
+      res = to;
+    }
+  if (memory == GLS_MEM_HOST)
+    HIP_THROW(hipMemcpyAsync(v, res, bytes, hipMemcpyDeviceToHost, s));
+}
+
+void
+VecStage::done(hipStream_t s)
+{
+  if (memory == GLS_MEM_HOST)
+    HIP_THROW(hipStreamSynchronize(s));
+}
+} // namespace gls
+
+// ------------------------------------------------------------ get_max_u
+namespace
+{
+// NavierStokesOperator::get_max_u (operator_ns.cc:530-568): one lane per
+// (cell, q point): velocity at x_q from the cell's plain nodal values
+// (read_dof_values_plain + evaluate(values)), |u|, block max into part[]
+template <int dim, int k, typename T>
+__global__ void __launch_bounds__(256)
+  k_max_u(const uint32_t *__restrict__ nodes, const T *__restrict__ vec, int64_t n_cells,
+          Shape<T, k + 1> sh, double *__restrict__ part)
+{
+  constexpr int n = k + 1, nq = ipow(n, dim), nc = dim + 1;
+  __shared__ double red[4];
+  const int64_t     g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double            m = 0;
+  if (g < n_cells * nq)
+    {
+      const int64_t c  = g / nq;
+      const int     q  = (int)(g - c * nq);
+      const int     qa[3] = {q % n, (q / n) % n, dim == 3 ? q / (n * n) : 0};
+      T             u[dim];
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        u[d] = 0;
+      for (int i = 0; i < nq; ++i)
+        {
+          const int ia[3] = {i % n, (i / n) % n, dim == 3 ? i / (n * n) : 0};
+          T         w     = sh.S[qa[0]][ia[0]] * sh.S[qa[1]][ia[1]];
+          if (dim == 3)
+            w *= sh.S[qa[2]][ia[2]];
+          const size_t node = nodes[c * nq + i] & NODE_MASK;
+#pragma unroll
+          for (int d = 0; d < dim; ++d)
+            u[d] += w * vec[node * nc + d];
+        }
+      T s2 = 0;
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        s2 += u[d] * u[d];
+      m = (double)sqrt(s2);
+    }
+  for (int off = 32; off > 0; off >>= 1)
+    m = fmax(m, __shfl_down(m, off));
+  if ((threadIdx.x & 63) == 0)
+    red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    part[blockIdx.x] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+}
+
+__global__ void __launch_bounds__(256)
+  k_max_finish(const double *__restrict__ part, int64_t nb, double *__restrict__ out)
+{
+  __shared__ double red[256];
+  double            m = 0;
+  for (int64_t b = threadIdx.x; b < nb; b += 256)
+    m = fmax(m, part[b]);
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1)
+    {
+      if ((int)threadIdx.x < st)
+        red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + st]);
+      __syncthreads();
+    }
+  if (threadIdx.x == 0)
+    out[0] = red[0];
+}
+
+template <int dim, int k, typename T>
+double
+max_u_t(const glsOp_ *op, const void *vec, hipStream_t s)
+{
+  constexpr int n = k + 1, nq = ipow(n, dim);
+  const int64_t nb   = (op->n_cells * nq + 255) / 256;
+  double       *part = nullptr;
+  HIP_THROW(hipMallocAsync((void **)&part, (size_t)(nb + 1) * sizeof(double), s));
+  if (nb > 0)
+    hipLaunchKernelGGL((k_max_u<dim, k, T>), dim3((unsigned)nb), dim3(256), 0, s, op->d_nodes,
+                       (const T *)vec, op->n_cells, make_shape<T, n>(op->basis), part);
+  hipLaunchKernelGGL(k_max_finish, dim3(1), dim3(256), 0, s, (const double *)part, nb,
+                     part + nb);
+  HIP_THROW(hipGetLastError());
+  double r = 0;
+  HIP_THROW(hipMemcpyAsync(&r, part + nb, sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_THROW(hipFreeAsync(part, s));
+  HIP_THROW(hipStreamSynchronize(s));
+  return r;
+}
+
+template <typename T>
+double
+max_u_p(const glsOp_ *op, const void *vec, hipStream_t s)
+{
+#define GLS_CASE(D, K)              \
+  if (op->dim == D && op->degree == K) \
+    return max_u_t<D, K, T>(op, vec, s);
+  GLS_CASE(2, 1)
+  GLS_CASE(2, 2)
+  GLS_CASE(2, 3)
+  GLS_CASE(3, 1)
+  GLS_CASE(3, 2)
+  GLS_CASE(3, 3)
+#undef GLS_CASE
+  throw std::runtime_error("get_max_u: no instantiation for this (dim, degree)");
+}
+} // namespace
 
 // ------------------------------------------------------------ C-ABI
 extern "C" {
@@ -1042,6 +1322,7 @@ gls_op_destroy(glsOp op)
   for (void *b : bufs)
     if (b)
       (void)hipFree(b);
+  op->stage.release();
   delete op;
 }
 
@@ -1073,15 +1354,27 @@ gls_op_precision(glsOp op)
 }
 
 glsStatus
+gls_op_set_vector_layout(glsOp op, int memory, const int64_t *dof_map)
+{
+  GLS_TRY
+  if (!op)
+    throw std::runtime_error("gls_op_set_vector_layout: null operator");
+  op->stage.set(memory, dof_map, op->n_dofs, op->tsize());
+  GLS_CATCH
+}
+
+glsStatus
 gls_op_set_linearization_point(glsOp op, const void *vec, void *stream)
 {
   GLS_TRY
   if (!op || !vec)
     throw std::runtime_error("gls_op_set_linearization_point: null argument");
-  ApplyFn   af;
-  ProduceFn pf;
+  ApplyFn     af;
+  ProduceFn   pf;
+  hipStream_t s = (hipStream_t)stream;
   select(op, af, pf);
-  pf(op, 0, vec, (hipStream_t)stream);
+  pf(op, 0, op->stage.in_vec(vec, 0, s), s);
+  op->stage.done(s);
   op->have_lin = true;
   GLS_CATCH
 }
@@ -1106,7 +1399,9 @@ gls_op_set_previous_solution(glsOp op, const void *const *hist, int n_hist,
   double      w[4] = {0, 0, 0, 0};
   for (int i = 1; i <= order; ++i)
     {
-      x[i - 1] = hist[i];
+      if (!hist[i])
+        throw std::runtime_error("gls_op_set_previous_solution: null history vector");
+      x[i - 1] = op->stage.in_vec(hist[i], i - 1, s);
       w[i - 1] = weights[i];
     }
   if (op->prec == GLS_F64)
@@ -1129,9 +1424,10 @@ gls_op_set_previous_solution(glsOp op, const void *const *hist, int n_hist,
           const size_t sz = (size_t)(op->dim * op->dim + op->dim) * op->n_cells * op->nq * op->tsize();
           HIP_THROW(hipMalloc(&op->d_old_grad, std::max<size_t>(1, sz)));
         }
-      pf(op, 2, hist[1], s);
+      pf(op, 2, x[0], s);
       op->have_old_grad = true;
     }
+  op->stage.done(s);
   GLS_CATCH
 }
 
@@ -1189,20 +1485,12 @@ gls_op_vmult(glsOp op, void *dst, const void *src, void *stream)
     throw std::runtime_error("gls_op_vmult: null argument");
   if (dst == src)
     throw std::runtime_error("gls_op_vmult: dst and src must not alias");
-  if (!op->have_lin)
-    throw std::runtime_error("vmult before set_linearization_point");
-  ApplyFn   af;
-  ProduceFn pf;
-  select(op, af, pf);
   hipStream_t s = (hipStream_t)stream;
-  if (op->use_brick)
-    select_brick(op)(op, vmult_mode(op), dst, src, 0, op->n_bricks, BRICK_RUN | BRICK_REDUCE, s,
-                     nullptr);
-  else
-    {
-      init_dst(op, dst, src, s);
-      af(op, vmult_mode(op), false, dst, src, 0, op->n_cells, s);
-    }
+  const void *x = op->stage.in_vec(src, 0, s);
+  void       *y = op->stage.out_vec(dst);
+  gls::op_vmult_device(op, y, x, s);
+  op->stage.finish_out(dst, s);
+  op->stage.done(s);
   GLS_CATCH
 }
 
@@ -1265,8 +1553,12 @@ gls_op_set_constraint_values(glsOp op, const void *values, void *stream)
     {
       if (!op->d_inhom)
         HIP_THROW(hipMalloc(&op->d_inhom, std::max<size_t>(1, (size_t)op->n_dofs * op->tsize())));
-      HIP_THROW(hipMemcpyAsync(op->d_inhom, values, (size_t)op->n_dofs * op->tsize(),
+      // host or device pointer (hipMemcpyDefault); a caller numbering is
+      // permuted through the staging buffers first
+      const void *v = op->stage.d_map ? op->stage.in_vec(values, 1, s) : values;
+      HIP_THROW(hipMemcpyAsync(op->d_inhom, v, (size_t)op->n_dofs * op->tsize(),
                                hipMemcpyDefault, s));
+      op->stage.done(s);
     }
   GLS_CATCH
 }
@@ -1300,8 +1592,11 @@ gls_op_evaluate_rhs(glsOp op, void *dst, void *stream)
   if (!op->have_lin)
     throw std::runtime_error("evaluate_rhs before set_linearization_point");
   hipStream_t s = (hipStream_t)stream;
+  void       *y = op->stage.out_vec(dst);
   distribute(op, op->d_tmp, nullptr, s);
-  residual_cells(op, dst, op->d_tmp, s);
+  residual_cells(op, y, op->d_tmp, s);
+  op->stage.finish_out(dst, s);
+  op->stage.done(s);
   GLS_CATCH
 }
 
@@ -1314,9 +1609,13 @@ gls_op_evaluate_residual(glsOp op, void *dst, const void *src, void *stream)
   if (!op->have_lin)
     throw std::runtime_error("evaluate_residual before set_linearization_point");
   hipStream_t s = (hipStream_t)stream;
+  const void *x = op->stage.in_vec(src, 0, s);
+  void       *y = op->stage.out_vec(dst);
   // operator_ns.cc:655-656: tmp = src; constraints_inhomogeneous.distribute(tmp)
-  distribute(op, op->d_tmp, src, s);
-  residual_cells(op, dst, op->d_tmp, s);
+  distribute(op, op->d_tmp, x, s);
+  residual_cells(op, y, op->d_tmp, s);
+  op->stage.finish_out(dst, s);
+  op->stage.done(s);
   GLS_CATCH
 }
 
@@ -1328,33 +1627,52 @@ gls_op_evaluate_residual_plain(glsOp op, void *dst, const void *src, void *strea
     throw std::runtime_error("gls_op_evaluate_residual_plain: bad arguments");
   if (!op->have_lin)
     throw std::runtime_error("evaluate_residual before set_linearization_point");
-  ApplyFn   af;
-  ProduceFn pf;
-  select(op, af, pf);
   hipStream_t s = (hipStream_t)stream;
-  if (op->use_brick)
-    select_brick(op)(op, MODE_RESIDUAL, dst, src, 0, op->n_bricks, BRICK_RUN | BRICK_REDUCE,
-                     s, nullptr);
-  else
-    {
-      HIP_THROW(hipMemsetAsync(dst, 0, (size_t)op->n_dofs * op->tsize(), s));
-      af(op, MODE_RESIDUAL, false, dst, src, 0, op->n_cells, s);
-    }
+  const void *x = op->stage.in_vec(src, 0, s);
+  void       *y = op->stage.out_vec(dst);
+  residual_cells(op, y, x, s);
+  op->stage.finish_out(dst, s);
+  op->stage.done(s);
   GLS_CATCH
 }
 
 glsStatus
-gls_op_compute_inverse_diagonal(glsOp op, void *diag, void *stream)
+gls_op_get_max_u(glsOp op, const void *vec, double *u_max, void *stream)
 {
   GLS_TRY
-  if (!op || !diag)
+  if (!op || !vec || !u_max)
+    throw std::runtime_error("gls_op_get_max_u: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  const void *x = op->stage.in_vec(vec, 0, s);
+  *u_max        = op->prec == GLS_F64 ? max_u_p<double>(op, x, s) : max_u_p<float>(op, x, s);
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_compute_inverse_diagonal(glsOp op, void *diag_, void *stream)
+{
+  GLS_TRY
+  if (!op || !diag_)
     throw std::runtime_error("gls_op_compute_inverse_diagonal: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  gls::op_inverse_diagonal_device(op, op->stage.out_vec(diag_), s);
+  op->stage.finish_out(diag_, s);
+  op->stage.done(s);
+  GLS_CATCH
+}
+
+} // extern "C"
+
+namespace gls
+{
+void
+op_inverse_diagonal_device(glsOp op, void *diag, hipStream_t s)
+{
   if (!op->have_lin)
     throw std::runtime_error("compute_inverse_diagonal before set_linearization_point");
   ApplyFn   af;
   ProduceFn pf;
   select(op, af, pf);
-  hipStream_t s = (hipStream_t)stream;
   HIP_THROW(hipMemsetAsync(diag, 0, (size_t)op->n_dofs * op->tsize(), s));
   af(op, vmult_mode(op), true, diag, diag, 0, op->n_cells, s);
   if (op->prec == GLS_F64)
@@ -1364,8 +1682,10 @@ gls_op_compute_inverse_diagonal(glsOp op, void *diag, void *stream)
     hipLaunchKernelGGL(k_invert_diag<float>, grid1d(op->n_dofs), dim3(256), 0, s, (float *)diag,
                        op->d_cbits, op->n_owned_dofs, op->n_dofs);
   HIP_THROW(hipGetLastError());
-  GLS_CATCH
 }
+} // namespace gls
+
+extern "C" {
 
 glsStatus
 gls_op_upload_tables(glsOp op, const double *tables, const double *cellwise)

@@ -104,8 +104,10 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   const int64_t  n = op->n_dofs;
   // deal.II SolverGMRES restarts after max_n_tmp_vectors - 2 iterations
   const int      m = desc->max_n_tmp_vectors - 2;
-  double        *x = (double *)x_;
-  const double  *b = (const double *)b_;
+  // caller layout (host memory / dof numbering): b staged in, x written to
+  // a device buffer and copied / permuted back at the end
+  const double  *b = (const double *)op->stage.in_vec(b_, 1, s);
+  double        *x = (double *)op->stage.out_vec(x_);
   // the operator's device, its rocBLAS handle, and the Krylov workspace
   // [V (m+1) n | w n | z n | dh 2 (m+1)] kept on the operator and grown on
   // demand (a hipMalloc/hipFree of the basis per solve synchronises the
@@ -139,7 +141,7 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   auto vcol = [&](int j) { return V.d() + (size_t)j * n; };
   auto precondition = [&](double *dst, const double *src) {
     if (mg)
-      check(gls_mg_vcycle(mg, dst, src, s), "preconditioner vmult (gls_mg_vcycle)");
+      gls::mg_vcycle_device(mg, dst, src, s);
     else
       HIP_THROW(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, s));
   };
@@ -177,7 +179,7 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
         {
           // w = A M^{-1} v_j
           precondition(z.d(), vcol(j));
-          check(gls_op_vmult(op, w.d(), z.d(), s), "operator vmult");
+          gls::op_vmult_device(op, w.d(), z.d(), s);
           // CGS2: h = V^T w; w -= V h; twice
           const double one = 1.0, zero = 0.0, mone = -1.0;
           for (int pass = 0; pass < 2; ++pass)
@@ -246,12 +248,13 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
         break;
       // restart: true residual r = b - A x into column 0
       ++n_rst;
-      check(gls_op_vmult(op, vcol(0), x, s), "operator vmult");
+      gls::op_vmult_device(op, vcol(0), x, s);
       hipLaunchKernelGGL(k_residual, grid1(n), dim3(256), 0, s, vcol(0), b, n);
       HIP_THROW(hipGetLastError());
       res  = nrm2(vcol(0));
       conv = res <= tol;
     }
+  op->stage.finish_out(x_, s);
   HIP_THROW(hipStreamSynchronize(s));
   if (result)
     {

@@ -338,6 +338,7 @@ struct glsMG_
   int64_t                 acc_blocks = 0;
   double                  P[MAXP][MAXN]{};
   bool                    setup_done = false;
+  gls::VecStage           stage; // caller layout of gls_mg_vcycle's vectors
   // dense LU coarse solver (coarse_n_iterations < 0): the substitute for the
   // reference's Trilinos direct solver (multigrid.cc:448-455, 477-481)
   rocblas_handle blas   = nullptr;
@@ -453,7 +454,7 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
     {
       for (; it < iters; ++it)
         {
-          check(gls_op_vmult(op, mg->tmp[level], x, s));
+          gls::op_vmult_device(op, mg->tmp[level], x, s);
           relax(mg, level, x, b, 0, s);
         }
       return;
@@ -464,7 +465,7 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
   // in x without a copy
   if ((iters - it) % 2 == 1)
     {
-      check(gls_op_vmult(op, mg->tmp[level], x, s));
+      gls::op_vmult_device(op, mg->tmp[level], x, s);
       relax(mg, level, x, b, 0, s);
       ++it;
     }
@@ -536,7 +537,7 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
   for (int64_t j = 0; j < n; ++j)
     {
       hipLaunchKernelGGL(k_set_unit<T>, g1(n), dim3(256), 0, s, e, j, n, 1);
-      check(gls_op_vmult(op, col, e, s));
+      gls::op_vmult_device(op, col, e, s);
       hipLaunchKernelGGL((k_convert<T, double>), g1(n), dim3(256), 0, s,
                          mg->d_lu + (size_t)j * n, col, n);
       hipLaunchKernelGGL(k_set_unit<T>, g1(n), dim3(256), 0, s, e, j, n, 0);
@@ -595,7 +596,7 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
   // pre-smoothing from a zero initial guess (MGSmootherPrecondition::apply)
   smooth(mg, l, mg->sol[l], mg->def[l], true, nit, s);
   // residual t = defect - A solution
-  check(gls_op_vmult(mg->ops[l], mg->tmp[l], mg->sol[l], s));
+  gls::op_vmult_device(mg->ops[l], mg->tmp[l], mg->sol[l], s);
   residual(mg, l, mg->tmp[l], mg->def[l], s);
   // restrict
   HIP_THROW(hipMemsetAsync(mg->def[l - 1], 0, (size_t)mg->ops[l - 1]->n_dofs * mg->ts(), s));
@@ -659,7 +660,7 @@ power_iteration_t(glsMG_ *mg, int l, hipStream_t s)
   HIP_THROW(hipMemsetAsync(scal, 0, 2 * sizeof(double), s));
   for (int it = 0; it < mg->desc.smoothing_eig_n_iterations; ++it)
     {
-      check(gls_op_vmult(op, y, x, s));
+      gls::op_vmult_device(op, y, x, s);
       hipLaunchKernelGGL(k_power_step<T>, g1(n), dim3(256), 0, s, (T *)y, (const T *)x,
                          (const T *)mg->invdiag[l], part, n);
       hipLaunchKernelGGL(k_power_finish, dim3(1), dim3(256), 0, s, (const double *)part, nb,
@@ -800,6 +801,7 @@ gls_mg_destroy(glsMG mg)
       (void)hipFree(p);
   if (mg->blas)
     rocblas_destroy_handle(mg->blas);
+  mg->stage.release();
   delete mg;
 }
 
@@ -813,7 +815,7 @@ gls_mg_setup(glsMG mg, void *stream)
   for (size_t l = 0; l < mg->ops.size(); ++l)
     {
       // compute_inverse_diagonal (multigrid.cc:290-293)
-      check(gls_op_compute_inverse_diagonal(mg->ops[l], mg->invdiag[l], s));
+      gls::op_inverse_diagonal_device(mg->ops[l], mg->invdiag[l], s);
       // relaxation = 0: omega from the power-iteration estimate of
       // lambda_max(D^-1 A) (power_iteration_t), estimated on the levels
       // above the coarsest one (multigrid.cc:355-358 with
@@ -875,9 +877,35 @@ gls_mg_vcycle(glsMG mg, void *dst, const void *src, void *stream)
   GLS_TRY
   if (!mg || !dst || !src)
     throw std::runtime_error("gls_mg_vcycle: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  const void *x = mg->stage.in_vec(src, 0, s);
+  void       *y = mg->stage.out_vec(dst);
+  gls::mg_vcycle_device(mg, y, x, s);
+  mg->stage.finish_out(dst, s);
+  mg->stage.done(s);
+  GLS_CATCH
+}
+
+glsStatus
+gls_mg_set_vector_layout(glsMG mg, int memory, const int64_t *dof_map)
+{
+  GLS_TRY
+  if (!mg)
+    throw std::runtime_error("gls_mg_set_vector_layout: null handle");
+  const size_t ts = mg->desc.outer_precision == GLS_F64 ? 8 : mg->ts();
+  mg->stage.set(memory, dof_map, mg->ops.back()->n_dofs, ts);
+  GLS_CATCH
+}
+
+} // extern "C"
+
+namespace gls
+{
+void
+mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s)
+{
   if (!mg->setup_done)
     throw std::runtime_error("gls_mg_vcycle before gls_mg_setup");
-  hipStream_t   s   = (hipStream_t)stream;
   const int     top = (int)mg->ops.size() - 1;
   const int64_t n   = mg->ops[top]->n_dofs;
   const bool    cvt = mg->desc.outer_precision == GLS_F64 && mg->prec == GLS_F32;
@@ -896,8 +924,10 @@ gls_mg_vcycle(glsMG mg, void *dst, const void *src, void *stream)
   else
     HIP_THROW(hipMemcpyAsync(dst, mg->sol[top], n * mg->ts(), hipMemcpyDeviceToDevice, s));
   HIP_THROW(hipGetLastError());
-  GLS_CATCH
 }
+} // namespace gls
+
+extern "C" {
 
 glsStatus
 gls_mg_prolongate_add(glsMG mg, int level, void *dst_fine, const void *src_coarse,

@@ -8,6 +8,41 @@
 #include <cstdint>
 #include <vector>
 
+namespace gls
+{
+// Caller-side vector layout of the C-ABI (gls_op_set_vector_layout /
+// gls_mg_set_vector_layout): vectors in host memory (the reference's
+// LinearAlgebra::distributed::Vector<Number> lives in host memory,
+// config.h:9-10) and/or in the caller's dof numbering (deal.II's DoFHandler
+// numbering, dof_map[i] = this library's node-major dof of caller dof i).
+// Inputs are staged into node-major device buffers, outputs written to a
+// device buffer and permuted / copied back; host-memory calls return
+// synchronised (host semantics).  Device memory in node-major order (the
+// default) takes no staging at all.
+struct VecStage
+{
+  int      memory = GLS_MEM_DEVICE;
+  int64_t  n      = 0;
+  size_t   ts     = 8;
+  int64_t *d_map  = nullptr; // [n] or null
+  void    *raw    = nullptr; // [n] caller-order device copy of a host vector
+  void    *in[4]  = {nullptr, nullptr, nullptr, nullptr};
+  void    *out    = nullptr;
+
+  bool
+  active() const
+  {
+    return memory == GLS_MEM_HOST || d_map;
+  }
+  void        set(int memory, const int64_t *map, int64_t n, size_t ts);
+  const void *in_vec(const void *v, int slot, hipStream_t s);
+  void       *out_vec(void *v);
+  void        finish_out(void *v, hipStream_t s);
+  void        done(hipStream_t s);
+  void        release();
+};
+} // namespace gls
+
 struct glsOp_
 {
   int     dim = 3, degree = 2, prec = GLS_F64;
@@ -39,6 +74,7 @@ struct glsOp_
   void     *d_inhom      = nullptr; // [n_dofs] inhomogeneity of constraints_inhomogeneous
                                     // (values on constrained dofs), or null = all zero
   int       device     = 0;
+  gls::VecStage stage; // caller vector layout (host memory / dof permutation)
   // gls_gmres_solve workspace (Krylov basis and vectors), grown on demand
   void     *gmres_ws       = nullptr;
   size_t    gmres_ws_bytes = 0;
@@ -93,4 +129,10 @@ struct RelaxStep
 void brick_launch(const glsOp_ *op, int mode, void *dst, const void *src, int64_t b0,
                   int64_t b1, int what, hipStream_t s, const RelaxStep *rx = nullptr);
 int  op_vmult_mode(const glsOp_ *op);
+// one V-cycle on node-major device vectors of the multigrid's outer
+// precision (gls_mg_vcycle without the caller-layout staging; GMRES calls it)
+void mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s);
+// the same operator pieces without staging (GMRES, multigrid)
+void op_vmult_device(glsOp op, void *dst, const void *src, hipStream_t s);
+void op_inverse_diagonal_device(glsOp op, void *diag, hipStream_t s);
 } // namespace gls

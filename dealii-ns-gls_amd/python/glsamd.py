@@ -32,8 +32,12 @@ EXPORTS = [
     "gls_mg_setup", "gls_mg_get_relaxation", "gls_mg_vcycle", "gls_mg_prolongate_add",
     "gls_mg_restrict_add", "gls_mg_interpolate", "gls_mg_smooth", "gls_last_error",
     "gls_dist_unique_id", "gls_dist_create", "gls_dist_destroy", "gls_dist_vmult",
-    "gls_dist_vmult_group", "gls_dist_interior_bricks",
+    "gls_dist_vmult_group", "gls_dist_interior_bricks", "gls_op_set_vector_layout",
+    "gls_op_get_max_u", "gls_mg_set_vector_layout", "gls_dist_update_ghost_values",
+    "gls_dist_get_max_u",
 ]
+
+GLS_MEM_DEVICE, GLS_MEM_HOST = 0, 1
 
 
 class OpDesc(C.Structure):
@@ -126,6 +130,11 @@ def lib():
         L.gls_dist_interior_bricks.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)]
         L.gls_gmres_solve.argtypes = [vp, vp, C.POINTER(GMRESDesc), vp, vp,
                                       C.POINTER(GMRESResult), vp]
+        L.gls_op_set_vector_layout.argtypes = [vp, C.c_int, vp]
+        L.gls_op_get_max_u.argtypes = [vp, vp, C.POINTER(C.c_double), vp]
+        L.gls_mg_set_vector_layout.argtypes = [vp, C.c_int, vp]
+        L.gls_dist_update_ghost_values.argtypes = [vp, vp, vp]
+        L.gls_dist_get_max_u.argtypes = [vp, vp, C.POINTER(C.c_double), vp]
         L.gls_last_error.restype = C.c_char_p
         _lib = L
     return _lib
@@ -147,6 +156,14 @@ def _stream():
 
 def _ptr(t):
     return C.c_void_p(t.data_ptr())
+
+
+def _vptr(v):
+    """Device tensor or host numpy array (GLS_MEM_HOST layouts)."""
+    if isinstance(v, np.ndarray):
+        assert v.flags["C_CONTIGUOUS"]
+        return C.c_void_p(v.ctypes.data)
+    return _ptr(v)
 
 
 class NavierStokesOperator:
@@ -217,20 +234,28 @@ class NavierStokesOperator:
             v = torch.from_numpy(v)
         return v.to(device="cuda", dtype=self.dtype).contiguous()
 
+    def _arg(self, v):
+        """A vector argument in the current layout: numpy (host layout) or a
+        device tensor."""
+        if getattr(self, "_memory", "device") == "host":
+            return np.ascontiguousarray(v, dtype=np.float64 if self.prec == GLS_F64
+                                        else np.float32)
+        return self._dev(v)
+
     def set_linearization_point(self, vec):
-        v = self._dev(vec)
-        _check(lib().gls_op_set_linearization_point(self.h, _ptr(v), _stream()))
+        v = self._arg(vec)
+        _check(lib().gls_op_set_linearization_point(self.h, _vptr(v), _stream()))
 
     def set_previous_solution(self, history, weights):
-        hs = [self._dev(h) for h in history]
-        ptrs = (C.c_void_p * len(hs))(*[h.data_ptr() for h in hs])
+        hs = [self._arg(h) for h in history]
+        ptrs = (C.c_void_p * len(hs))(*[_vptr(h).value for h in hs])
         w = np.ascontiguousarray(weights, dtype=np.float64)
         _check(lib().gls_op_set_previous_solution(self.h, C.cast(ptrs, C.c_void_p), len(hs),
                                                   w.ctypes.data, _stream()))
         self._hist_keep = hs
 
     def vmult(self, dst, src):
-        _check(lib().gls_op_vmult(self.h, _ptr(dst), _ptr(src), _stream()))
+        _check(lib().gls_op_vmult(self.h, _vptr(dst), _vptr(src), _stream()))
         return dst
 
     def vmult_init(self, dst, src):
@@ -246,18 +271,18 @@ class NavierStokesOperator:
     def evaluate_residual(self, dst, src):
         """operator_ns.cc:648-682: distribute the inhomogeneous constraints
         on a copy of src, residual cell loop, set_zero, *= -1."""
-        _check(lib().gls_op_evaluate_residual(self.h, _ptr(dst), _ptr(src), _stream()))
+        _check(lib().gls_op_evaluate_residual(self.h, _vptr(dst), _vptr(src), _stream()))
         return dst
 
     def evaluate_residual_plain(self, dst, src):
         """The same on src as it is (no distribute)."""
-        _check(lib().gls_op_evaluate_residual_plain(self.h, _ptr(dst), _ptr(src), _stream()))
+        _check(lib().gls_op_evaluate_residual_plain(self.h, _vptr(dst), _vptr(src), _stream()))
         return dst
 
     def evaluate_rhs(self, dst):
         """operator_ns.cc:622-646: residual of the zero vector with the
         inhomogeneous constraints distributed."""
-        _check(lib().gls_op_evaluate_rhs(self.h, _ptr(dst), _stream()))
+        _check(lib().gls_op_evaluate_rhs(self.h, _vptr(dst), _stream()))
         return dst
 
     def set_constraint_values(self, values):
@@ -271,8 +296,25 @@ class NavierStokesOperator:
         self._inhom_keep = v
 
     def compute_inverse_diagonal(self, diag):
-        _check(lib().gls_op_compute_inverse_diagonal(self.h, _ptr(diag), _stream()))
+        _check(lib().gls_op_compute_inverse_diagonal(self.h, _vptr(diag), _stream()))
         return diag
+
+    def get_max_u(self, vec):
+        """OperatorBase::get_max_u (operator_ns.cc:530-568): max |u(x_q)|."""
+        out = C.c_double()
+        _check(lib().gls_op_get_max_u(self.h, _vptr(vec), C.byref(out), _stream()))
+        return out.value
+
+    def set_vector_layout(self, memory="device", dof_map=None):
+        """Caller vector layout (gls_op_set_vector_layout): memory "host"
+        (numpy arrays, staged) or "device" (torch tensors); dof_map[i] = the
+        node-major dof of caller dof i (deal.II numbering), or None."""
+        m = np.ascontiguousarray(dof_map, dtype=np.int64) if dof_map is not None else None
+        _check(lib().gls_op_set_vector_layout(self.h, GLS_MEM_HOST if memory == "host"
+                                              else GLS_MEM_DEVICE,
+                                              None if m is None else m.ctypes.data))
+        self._map_keep = m
+        self._memory = memory
 
     def download_tables(self):
         nq = (self.degree + 1) ** self.dim
@@ -347,6 +389,16 @@ class PartitionedOperator:
         _check(lib().gls_dist_vmult(self.h, _ptr(dst), _ptr(src), _stream()))
         return dst
 
+    def update_ghost_values(self, vec):
+        _check(lib().gls_dist_update_ghost_values(self.h, _ptr(vec), _stream()))
+
+    def get_max_u(self, vec):
+        """get_max_u of the partitioned operator: ghost import, local max,
+        RCCL all-reduce max (operator_ns.cc:540-567)."""
+        out = C.c_double()
+        _check(lib().gls_dist_get_max_u(self.h, _ptr(vec), C.byref(out), _stream()))
+        return out.value
+
     def interior_bricks(self):
         a, b = C.c_int64(), C.c_int64()
         _check(lib().gls_dist_interior_bricks(self.h, C.byref(a), C.byref(b)))
@@ -403,8 +455,15 @@ class Multigrid:
         return w.value, lam.value
 
     def vcycle(self, dst, src):
-        _check(lib().gls_mg_vcycle(self.h, _ptr(dst), _ptr(src), _stream()))
+        _check(lib().gls_mg_vcycle(self.h, _vptr(dst), _vptr(src), _stream()))
         return dst
+
+    def set_vector_layout(self, memory="device", dof_map=None):
+        m = np.ascontiguousarray(dof_map, dtype=np.int64) if dof_map is not None else None
+        _check(lib().gls_mg_set_vector_layout(self.h, GLS_MEM_HOST if memory == "host"
+                                              else GLS_MEM_DEVICE,
+                                              None if m is None else m.ctypes.data))
+        self._map_keep = m
 
     def prolongate_add(self, level, dst_fine, src_coarse):
         _check(lib().gls_mg_prolongate_add(self.h, level, _ptr(dst_fine), _ptr(src_coarse),
@@ -481,7 +540,7 @@ class LinearSolverGMRES:
     def solve(self, dst, src):
         res = GMRESResult()
         mg = self.preconditioner.h if self.preconditioner is not None else None
-        rc = lib().gls_gmres_solve(self.op.h, mg, C.byref(self.desc), _ptr(dst), _ptr(src),
+        rc = lib().gls_gmres_solve(self.op.h, mg, C.byref(self.desc), _vptr(dst), _vptr(src),
                                    C.byref(res), _stream())
         self.last = {f: getattr(res, f) for f, _ in GMRESResult._fields_}
         _check(rc)

@@ -78,6 +78,12 @@ enum glsPrecision
   GLS_F32 = 1
 };
 
+enum glsMemory
+{
+  GLS_MEM_DEVICE = 0, /* vectors are device pointers (default)             */
+  GLS_MEM_HOST   = 1  /* vectors are host pointers, staged over PCIe       */
+};
+
 enum glsFlags
 {
   GLS_INCREMENT_FORM           = 1, /* Newton: increment_form, main.cc:331    */
@@ -122,6 +128,23 @@ glsStatus gls_op_set_parameters(glsOp op, const glsOpParams *prm);
 int64_t   gls_op_m(glsOp op); /* number of local dofs */
 int       gls_op_precision(glsOp op);
 
+/* Caller-side vector layout of every vector argument of the gls_op_* calls
+ * below that take whole dof vectors (set_linearization_point,
+ * set_previous_solution, vmult, evaluate_residual(_plain), evaluate_rhs,
+ * set_constraint_values, compute_inverse_diagonal, get_max_u, and x / b of
+ * gls_gmres_solve):
+ *   memory   GLS_MEM_DEVICE (default) or GLS_MEM_HOST: host pointers, as the
+ *            reference's LinearAlgebra::distributed::Vector<Number> in host
+ *            memory (config.h:9-10); staged through device buffers, the
+ *            call returns synchronised;
+ *   dof_map  NULL (node-major: dof = node * (dim+1) + component) or a host
+ *            array [gls_op_m] with dof_map[i] = the node-major dof of the
+ *            caller's local dof i (deal.II DoFHandler numbering); a
+ *            permutation, copied.
+ * The multi-GPU pieces (vmult_cells / vmult_init / apply_identity_rows,
+ * gls_dist_*) always take node-major device vectors. */
+glsStatus gls_op_set_vector_layout(glsOp op, int memory, const int64_t *dof_map);
+
 glsStatus gls_op_set_linearization_point(glsOp op, const void *vec, void *stream);
 /* vec_old = sum_{i=1..order} weights[i] * history[i]  (history[0] unused) */
 glsStatus gls_op_set_previous_solution(glsOp op, const void *const *history,
@@ -165,6 +188,13 @@ glsStatus gls_op_evaluate_rhs(glsOp op, void *dst, void *stream);
 glsStatus gls_op_set_constraint_values(glsOp op, const void *values, void *stream);
 glsStatus gls_op_compute_inverse_diagonal(glsOp op, void *inv_diag,
                                           void *stream);
+/* OperatorBase::get_max_u (operator_base.h:71-72; NavierStokesOperator
+ * operator_ns.cc:530-568): max over the locally processed cells and their
+ * quadrature points of |u(x_q)| of the velocity of `vec` (read plain, no
+ * constraints), into *u_max (host).  Called every time step for the CFL dt
+ * (main.cc:913-920).  Partitioned operators: gls_dist_get_max_u adds the
+ * MPI max. */
+glsStatus gls_op_get_max_u(glsOp op, const void *vec, double *u_max, void *stream);
 
 /* canonical host layout [cell][q][field] (fields: delta1, delta2, U(dim),
  * gradU(dim*dim), gradP(dim), Ut_old(dim)) + cellwise [cell][2] */
@@ -210,6 +240,9 @@ glsStatus gls_mg_get_relaxation(glsMG mg, int level, double *omega,
                                 double *lambda_max);
 /* one V-cycle on the finest level: dst = V(src) (PreconditionMG::vmult) */
 glsStatus gls_mg_vcycle(glsMG mg, void *dst, const void *src, void *stream);
+/* caller vector layout of gls_mg_vcycle's dst / src (as gls_op_set_vector_
+ * layout; n = the finest level's dofs) */
+glsStatus gls_mg_set_vector_layout(glsMG mg, int memory, const int64_t *dof_map);
 /* transfer on level pair (l-1, l): prolongate_and_add / restrict_and_add */
 glsStatus gls_mg_prolongate_add(glsMG mg, int level, void *dst_fine,
                                 const void *src_coarse, void *stream);
@@ -259,6 +292,12 @@ glsStatus gls_dist_vmult_group(glsDist const *members, void *const *dsts,
                                void *const *srcs, int n, void *stream);
 glsStatus gls_dist_interior_bricks(glsDist d, int64_t *n_interior,
                                    int64_t *n_total);
+/* update_ghost_values of a rank-local [owned | ghost] vector (the import
+ * half of gls_dist_vmult), RCCL ranks only */
+glsStatus gls_dist_update_ghost_values(glsDist d, void *vec, void *stream);
+/* get_max_u of the partitioned operator (operator_ns.cc:530-568): ghost
+ * import, local max (gls_op_get_max_u), RCCL all-reduce max */
+glsStatus gls_dist_get_max_u(glsDist d, void *vec, double *u_max, void *stream);
 
 /* ---- device-resident Krylov solver:
  * LinearSolverGMRES::solve, solver_l.cc:45-74 — deal.II SolverGMRES with

@@ -7,7 +7,10 @@
 // RAII handles; a nonzero status becomes gls::Error (std::runtime_error)
 // carrying gls_last_error() — the reference's AssertThrow convention.
 // Vectors are device pointers in the operator's precision, local layout
-// [owned | ghost], dof = node * (dim+1) + component.  Calls are
+// [owned | ghost], dof = node * (dim+1) + component — or, after
+// set_vector_layout(GLS_MEM_HOST, dof_map), host pointers in the caller's
+// (deal.II DoFHandler) numbering, as the reference's
+// LinearAlgebra::distributed::Vector<Number> (config.h:9-10).  Calls are
 // stream-ordered (hipStream_t passed as void*, nullptr = default stream)
 // and, like the reference's const-but-mutable operator, not reentrant per
 // handle.
@@ -74,7 +77,16 @@ public:
 
   glsOp handle() const { return h; }
 
-  // OperatorBase::m()  operator_base.h:23-24
+  // vector arguments: host or device memory, caller dof numbering
+  // (dof_map[i] = node-major dof of caller dof i; empty = node-major)
+  void
+  set_vector_layout(int memory, const std::vector<int64_t> &dof_map = {})
+  {
+    check(gls_op_set_vector_layout(h, memory, dof_map.empty() ? nullptr : dof_map.data()),
+          "set_vector_layout");
+  }
+
+  // OperatorBase::m()  operator_base.h:20-21
   int64_t m() const { return gls_op_m(h); }
 
   void
@@ -84,14 +96,14 @@ public:
     check(gls_op_set_parameters(h, &q), "gls_op_set_parameters");
   }
 
-  // operator_base.h:38-39 (operator_ns.cc:570-620)
+  // operator_base.h:35-36 (operator_ns.cc:570-620)
   void
   set_linearization_point(const void *src, void *stream = nullptr)
   {
     check(gls_op_set_linearization_point(h, src, stream), "set_linearization_point");
   }
 
-  // operator_base.h:35-36 (operator_ns.cc:234-320): history[0] unused,
+  // operator_base.h:32-33 (operator_ns.cc:234-320): history[0] unused,
   // weights[i] the BDF weights of TimeIntegratorData::get_weights()
   void
   set_previous_solution(const std::vector<const void *> &history,
@@ -102,21 +114,21 @@ public:
           "set_previous_solution");
   }
 
-  // operator_base.h:47-48 (operator_ns.cc:684-732)
+  // operator_base.h:45-46 (operator_ns.cc:684-732)
   void
   vmult(void *dst, const void *src, void *stream = nullptr) const
   {
     check(gls_op_vmult(h, dst, src, stream), "vmult");
   }
 
-  // operator_base.h:44-46 (operator_ns.cc:648-682)
+  // operator_base.h:41-43 (operator_ns.cc:648-682)
   void
   evaluate_residual(void *dst, const void *src, void *stream = nullptr) const
   {
     check(gls_op_evaluate_residual(h, dst, src, stream), "evaluate_residual");
   }
 
-  // operator_base.h:44-46 without the distribute step
+  // operator_base.h:41-43 without the distribute step
   void
   evaluate_residual_plain(void *dst, const void *src, void *stream = nullptr) const
   {
@@ -137,11 +149,20 @@ public:
     check(gls_op_set_constraint_values(h, values, stream), "set_constraint_values");
   }
 
-  // operator_base.h:29-30 (operator_ns.cc:195-225)
+  // operator_base.h:26-27 (operator_ns.cc:195-225)
   void
   compute_inverse_diagonal(void *diag, void *stream = nullptr) const
   {
     check(gls_op_compute_inverse_diagonal(h, diag, stream), "compute_inverse_diagonal");
+  }
+
+  // OperatorBase::get_max_u operator_base.h:71-72 (operator_ns.cc:530-568)
+  double
+  get_max_u(const void *src, void *stream = nullptr) const
+  {
+    double u = 0;
+    check(gls_op_get_max_u(h, src, &u, stream), "get_max_u");
+    return u;
   }
 
   // identity rows after a ghost export-add (distributed vmult)
@@ -182,6 +203,13 @@ public:
   Multigrid(const Multigrid &)            = delete;
   Multigrid &operator=(const Multigrid &) = delete;
   Multigrid(Multigrid &&o) noexcept : h(std::exchange(o.h, nullptr)) {}
+
+  void
+  set_vector_layout(int memory, const std::vector<int64_t> &dof_map = {})
+  {
+    check(gls_mg_set_vector_layout(h, memory, dof_map.empty() ? nullptr : dof_map.data()),
+          "gls_mg_set_vector_layout");
+  }
 
   // PreconditionerGMG::initialize (multigrid.cc:247-370)
   void initialize(void *stream = nullptr) { check(gls_mg_setup(h, stream), "gls_mg_setup"); }

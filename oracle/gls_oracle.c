@@ -727,6 +727,35 @@ orc_compute_inverse_diagonal(const orc_op *op, double *diag)
     diag[i] = fabs(diag[i]) > 1.0e-10 ? 1.0 / diag[i] : 1.0;
 }
 
+/* NavierStokesOperator::get_max_u, operator_ns.cc:530-568: read_dof_values_plain,
+ * evaluate(values), max over cells and q points of |u(x_q)| (velocity only) */
+double
+orc_get_max_u(const orc_op *op, const double *vec)
+{
+  const int dim = op->m.dim, nq = op->nq, nc = dim + 1;
+  double    m   = 0.0;
+  for (int64_t c = 0; c < op->m.n_cells; ++c)
+    {
+      double val[3][MAXNQ], gr[3][MAXNQ];
+      for (int d = 0; d < dim; ++d)
+        {
+          double u[MAXNQ];
+          for (int i = 0; i < nq; ++i)
+            u[i] = vec[(size_t)op->m.cell_nodes[c * nq + i] * nc + d];
+          eval_scalar(dim, &op->b, u, val[d], &gr[0][0]);
+        }
+      for (int q = 0; q < nq; ++q)
+        {
+          double s = 0;
+          for (int d = 0; d < dim; ++d)
+            s += val[d][q] * val[d][q];
+          if (sqrt(s) > m)
+            m = sqrt(s);
+        }
+    }
+  return m;
+}
+
 int
 orc_get_tables(const orc_op *op, double *tables, double *cellwise)
 {

@@ -78,6 +78,8 @@ void orc_vmult(const orc_op *op, double *dst, const double *src);
 void orc_evaluate_residual(const orc_op *op, double *dst, const double *src);
 /* operator_ns.cc:195-225 */
 void orc_compute_inverse_diagonal(const orc_op *op, double *inv_diag);
+/* get_max_u, operator_ns.cc:530-568 */
+double orc_get_max_u(const orc_op *op, const double *vec);
 /* element matrix of one cell, column j = cell operator applied to unit
  * vector j (what MatrixFreeTools::compute_matrix does), local dof order
  * (node, component) -> node * (dim+1) + c.  mat is [ndof][ndof] row major. */

@@ -46,6 +46,8 @@ def lib():
         L.orc_vmult.argtypes = [vp, vp, vp]
         L.orc_evaluate_residual.argtypes = [vp, vp, vp]
         L.orc_compute_inverse_diagonal.argtypes = [vp, vp]
+        L.orc_get_max_u.argtypes = [vp, vp]
+        L.orc_get_max_u.restype = C.c_double
         L.orc_cell_matrix.argtypes = [vp, C.c_int64, vp]
         L.orc_get_tables.argtypes = [vp, vp, vp]
         L.orc_get_tables.restype = C.c_int
@@ -129,6 +131,10 @@ class Oracle:
         dst = np.empty_like(src)
         lib().orc_evaluate_residual(self.h, _p(dst), _p(src))
         return dst
+
+    def get_max_u(self, vec):
+        vec = np.ascontiguousarray(vec, dtype=np.float64)
+        return float(lib().orc_get_max_u(self.h, _p(vec)))
 
     def inverse_diagonal(self):
         d = np.empty(self.m.n_dofs)

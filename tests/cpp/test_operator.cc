@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <utility>
 #include <vector>
 
 static uint64_t
@@ -247,7 +248,52 @@ run(int argc, char **argv)
   const double e0 = rel_err(g_dst, c_dst), e1 = rel_err(g_res, c_res), e2 = rel_err(g_diag, c_diag);
   std::printf("cells %lld dofs %zu  vmult %.3e  residual %.3e  inverse_diagonal %.3e\n",
               (long long)nc, ndof, e0, e1, e2);
+
+  // ---- the reference's vector layout: host memory (LA::distributed::Vector
+  // in host memory, config.h:9-10) in a non-node-major numbering (a
+  // deal.II-like DoFHandler numbering: a fixed pseudo-random permutation
+  // perm[i] = node-major dof of caller dof i)
+  std::vector<int64_t> perm(ndof);
+  for (size_t i = 0; i < ndof; ++i)
+    perm[i] = (int64_t)i;
+  for (size_t i = ndof - 1; i > 0; --i)
+    std::swap(perm[i], perm[splitmix64(77 + i) % (i + 1)]);
+  auto to_caller = [&](const std::vector<double> &x) {
+    std::vector<double> y(ndof);
+    for (size_t i = 0; i < ndof; ++i)
+      y[i] = x[(size_t)perm[i]];
+    return y;
+  };
+  gls::Operator hop(d);
+  hop.set_vector_layout(GLS_MEM_HOST, perm);
+  hop.set_parameters(prm);
+  const std::vector<double> u_c = to_caller(u), src_c = to_caller(src);
+  hop.set_linearization_point(u_c.data());
+  std::vector<std::vector<double>> hist_c;
+  std::vector<const void *>        hp_c;
+  for (auto &hv : hist)
+    hist_c.push_back(to_caller(hv));
+  for (auto &hv : hist_c)
+    hp_c.push_back(hv.data());
+  if (prm.order > 0)
+    hop.set_previous_solution(hp_c, w);
+  std::vector<double> h_dst(ndof), h_res(ndof), h_diag(ndof);
+  hop.vmult(h_dst.data(), src_c.data());
+  hop.evaluate_residual_plain(h_res.data(), src_c.data());
+  hop.compute_inverse_diagonal(h_diag.data());
+  const double gmax = hop.get_max_u(u_c.data());
+  orc_op *o2 = orc_create(&om, &oprm);
+  const double cmax = orc_get_max_u(o2, u.data());
+  orc_destroy(o2);
+  const double e3 = rel_err(h_dst, to_caller(c_dst)), e4 = rel_err(h_res, to_caller(c_res)),
+               e5 = rel_err(h_diag, to_caller(c_diag)), e6 = std::fabs(gmax - cmax) / cmax;
+  std::printf("host memory, permuted numbering: vmult %.3e  residual %.3e  inverse_diagonal "
+              "%.3e  get_max_u %.6f vs %.6f (%.1e)\n",
+              e3, e4, e5, gmax, cmax, e6);
   // 1/d amplifies the round-off of near-cancelling diagonal entries:
   // 10x the FP64 bound, as tests/test_gpu_parity.py
-  return (e0 < 1e-12 && e1 < 1e-12 && e2 < 1e-11) ? 0 : 1;
+  return (e0 < 1e-12 && e1 < 1e-12 && e2 < 1e-11 && e3 < 1e-12 && e4 < 1e-12 && e5 < 1e-11 &&
+          e6 < 1e-13) ?
+           0 :
+           1;
 }
