@@ -243,7 +243,6 @@ run(int argc, char **argv)
   orc_evaluate_residual(o, c_res.data(), src.data());
   orc_compute_inverse_diagonal(o, c_diag.data());
   orc_destroy(o);
-  gls_mesh_destroy(mesh);
 
   const double e0 = rel_err(g_dst, c_dst), e1 = rel_err(g_res, c_res), e2 = rel_err(g_diag, c_diag);
   std::printf("cells %lld dofs %zu  vmult %.3e  residual %.3e  inverse_diagonal %.3e\n",
@@ -285,6 +284,7 @@ run(int argc, char **argv)
   orc_op *o2 = orc_create(&om, &oprm);
   const double cmax = orc_get_max_u(o2, u.data());
   orc_destroy(o2);
+  gls_mesh_destroy(mesh); // owns cell_nodes / node_coords of d and om
   const double e3 = rel_err(h_dst, to_caller(c_dst)), e4 = rel_err(h_res, to_caller(c_res)),
                e5 = rel_err(h_diag, to_caller(c_diag)), e6 = std::fabs(gmax - cmax) / cmax;
   std::printf("host memory, permuted numbering: vmult %.3e  residual %.3e  inverse_diagonal "
