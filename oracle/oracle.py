@@ -186,3 +186,65 @@ def interpolate(cm: OracleMesh, fm: OracleMesh, child, dst_c, src_f):
     child = np.ascontiguousarray(child, dtype=np.uint32)
     src_f = np.ascontiguousarray(src_f, dtype=np.float64)
     lib().orc_interpolate(C.byref(cm.s), C.byref(fm.s), _p(child), _p(dst_c), _p(src_f))
+
+
+# ------------------------------------------------------------ batched CPU port
+def cpu_isa():
+    """'avx512' or 'avx2' from the host CPU flags (the batched build to load)."""
+    try:
+        flags = open("/proc/cpuinfo").read()
+    except OSError:
+        flags = ""
+    return "avx512" if " avx512f" in flags and " avx512dq" in flags else "avx2"
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+class BatchedCPU:
+    """The cell-batched SIMD CPU restatement (oracle/gls_cpu_batched.c) of the
+    headline Newton vmult (3D Q2, q-wise stabilisation), built from an Oracle's
+    tables and geometry on the same mesh: bench.py's cpu_baseline."""
+
+    def __init__(self, o: Oracle, threads):
+        m = o.m
+        if m.dim != 3 or m.degree != 2 or not o.prm.increment_form or o.prm.cell_wise_stabilization:
+            raise ValueError("BatchedCPU: 3D Q2 Newton operator with q-wise delta only")
+        self.isa = cpu_isa()
+        L = C.CDLL(os.path.join(_HERE, f"libcpu_batched_{self.isa}.so"))
+        vp = C.c_void_p
+        L.cpu_create.argtypes = [C.c_int64, C.c_int64, vp, vp, vp, vp, C.c_double, C.c_double,
+                                 C.c_int, C.c_int]
+        L.cpu_create.restype = vp
+        L.cpu_vmult.argtypes = [vp, vp, vp]
+        L.cpu_destroy.argtypes = [vp]
+        L.cpu_n_colors.argtypes = [vp]
+        self.L = L
+        t, _ = o.tables()
+        g = o.geometry()
+        td = int(o.prm.consider_time_derivative and o.prm.order > 0)
+        self.threads = int(threads)
+        self.h = L.cpu_create(m.n_cells, m.n_nodes, _p(m.cell_nodes), _p(m.cmask), _p(g), _p(t),
+                              o.prm.nu, o.prm.w0, td, self.threads)
+        self.n_colors = L.cpu_n_colors(self.h)
+        self.n_dofs = m.n_dofs
+
+    def __del__(self):
+        try:
+            self.L.cpu_destroy(self.h)
+        except Exception:
+            pass
+
+    def vmult(self, src, dst=None):
+        src = np.ascontiguousarray(src, dtype=np.float64)
+        if dst is None:
+            dst = np.empty_like(src)
+        self.L.cpu_vmult(self.h, _p(dst), _p(src))
+        return dst
