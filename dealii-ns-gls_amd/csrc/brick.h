@@ -127,7 +127,7 @@ struct BrickArgs
   int             bx, by, bz;
   int             L, Lx, Ly;
   int             PLx, PLy, LP; // padded LDS lattice strides / size (>= L)
-  T               nu, w0, theta;
+  T               nu, w0, theta, stau;
   int             td, cw, have_prev, have_old_grad;
   Shape<T, n>     sh;
 };
@@ -241,15 +241,53 @@ struct BrickLDS
   }
 };
 
+#ifndef GLS_INV_ZERO
+#define GLS_INV_ZERO 1
+#endif
+// Experimental table formulations (measured round 2), off by
+// default so that the brick kernel streams the reference's per-q tables
+// (operator_ns.h:120-132, SURVEY §8d B_tab):
+//   GLS_NEWTON_T1: the Newton vmult streams T1 (Fields::T1, the
+//     linearization-point part of R1) instead of grad P* and Ut_old;
+//   GLS_DELTA_OTF: q-wise delta_1 / delta_2 recomputed from U and h at the
+//     q point (delta_qwise, the producer's expression) instead of streamed.
+// Together: 16 instead of 20 values per q; Re3900 r3 283 -> 272 us, r2
+// unchanged (the kernel is latency-bound, not bandwidth-bound, there).
+#ifndef GLS_NEWTON_T1
+#define GLS_NEWTON_T1 0
+#endif
+#ifndef GLS_DELTA_OTF
+#define GLS_DELTA_OTF 0
+#endif
+// the table fields a brick vmult / residual of MODE streams: Newton U, grad U,
+// T1 and h (or delta_1/2); fixed-point U and h (delta_1/2); residual also
+// Ut_old.  Groups of 16 bytes with none of these are not loaded.
+template <int dim, int MODE>
+__host__ __device__ constexpr bool
+field_read(int f)
+{
+  using F         = Fields<dim>;
+  const bool d12  = f == F::D1 || f == F::D2;
+  const bool u    = f >= F::U && f < F::U + dim;
+  const bool h    = f == F::H;
+  const bool ut   = f >= F::UT && f < F::UT + dim;
+  const bool gu   = f >= F::GU && f < F::GU + dim * dim;
+  const bool gp   = f >= F::GP && f < F::GP + dim;
+  const bool t1   = f >= F::T1 && f < F::T1 + dim;
+  const bool newt = GLS_NEWTON_T1 ? (gu || t1) : (gu || gp || ut);
+  return (GLS_DELTA_OTF ? h : d12) || u || (MODE == MODE_NEWTON && newt) ||
+         (MODE == MODE_RESIDUAL && ut);
+}
+
 // everything one lane needs from HBM for one (cell, q point)
 template <int dim, typename T, int MODE>
 struct LaneData
 {
   static constexpr int NOLD = MODE == MODE_RESIDUAL ? dim * dim + dim : 1;
   T    inv[dim][dim];
-  T    JxW;
-  T    U[dim], GU[dim][dim], GP[dim], UT[dim], oldg[NOLD];
-  T    d1, d2;
+  T    JxW; // as loaded: JxW (curved) or det J (Cartesian); see jxw()
+  T    U[dim], GU[dim][dim], T1[dim], UT[dim], oldg[NOLD];
+  T    h, d1, d2; // h: q-wise delta from U on the fly (GLS_DELTA_OTF)
   int  li;
   bool active;
 };
@@ -284,12 +322,20 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
     lcell = 0;
   const int64_t cell = cell0 + lcell;
   const int64_t nqc  = a.n_cells * nq;
+#if GLS_INV_ZERO
 #pragma unroll
   for (int i = 0; i < dim; ++i)
 #pragma unroll
     for (int e = 0; e < dim; ++e)
       r.inv[i][e] = 0;
-  // geometry (MatrixFree-style compressed: Cartesian per cell, else per q)
+#endif
+  // geometry (MatrixFree-style compressed: Cartesian per cell, else per q).
+  // (GLS_INV_ZERO 0: the off-diagonal inv entries are not written on
+  // Cartesian bricks: that path reads the diagonal only.)
+  // loaded values stay untouched here: any arithmetic on them (the
+  // quadrature weight, the inactive-lane mask) would make the compiler wait
+  // for the loads at the prefetch point (an s_waitcnt vmcnt(0) in the middle
+  // of the round); jxw() applies both at the point of use
   if (general)
     {
       const int64_t gq = qindex<dim, n>(cell, p, a.n_cells);
@@ -302,16 +348,11 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
     }
   else
     {
-      T w = a.sh.w[pa[0]] * a.sh.w[pa[1]];
-      if (dim == 3)
-        w *= a.sh.w[pa[2]];
 #pragma unroll
       for (int i = 0; i < dim; ++i)
         r.inv[i][i] = a.geo_cart[i * a.n_cells + cell];
-      r.JxW = a.geo_cart[dim * a.n_cells + cell] * w;
+      r.JxW = a.geo_cart[dim * a.n_cells + cell];
     }
-  if (!r.active)
-    r.JxW = 0;
   // per-q tables (operator_ns.h:120-132): the round's CPW cells form one
   // chunk, each 16-byte field group of it one contiguous wave load; the
   // groups a mode reads are fixed at compile time (fields a runtime flag
@@ -325,13 +366,7 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
       bool any = false;
 #pragma unroll
       for (int w = 0; w < W; ++w)
-        {
-          const int  f   = g * W + w;
-          const bool d12 = f == F::D1 || f == F::D2;
-          const bool u   = f >= F::U && f < F::U + dim;
-          const bool ut  = f >= F::UT && f < F::N;
-          any = any || d12 || u || (MODE == MODE_NEWTON && f < F::N) || (R && ut);
-        }
+        any = any || field_read<dim, MODE>(g * W + w);
       V v = {};
       if (any)
         v = tv[g * GS];
@@ -343,7 +378,7 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
   for (int d = 0; d < dim; ++d)
     {
       r.U[d]  = tf[F::U + d];
-      r.GP[d] = tf[F::GP + d];
+      r.T1[d] = tf[(GLS_NEWTON_T1 ? F::T1 : F::GP) + d]; // T1, or grad P*
       r.UT[d] = tf[F::UT + d];
 #pragma unroll
       for (int e = 0; e < dim; ++e)
@@ -369,6 +404,21 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
       r.d1 = tf[F::D1];
       r.d2 = tf[F::D2];
     }
+  r.h = tf[F::H];
+}
+
+// JxW of a lane at its quadrature point: the loaded JxW (curved bricks) or
+// det J times the tensor quadrature weight (Cartesian), zero on inactive
+// lanes (they stay out of every sum)
+template <int dim, int k, typename T, int MODE>
+__device__ __forceinline__ T
+jxw(const LaneData<dim, T, MODE> &r, bool general, const Shape<T, k + 1> &sh, const int (&pa)[3])
+{
+  T w = sh.w[pa[0]] * sh.w[pa[1]];
+  if (dim == 3)
+    w *= sh.w[pa[2]];
+  const T j = general ? r.JxW : r.JxW * w;
+  return r.active ? j : T(0);
 }
 
 template <typename V, typename T, int nc, int NP, int W>
@@ -515,8 +565,18 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
   __syncthreads();
   GLS_STAMP(brick, 1);
 
+#ifndef GLS_LATE_PREFETCH
+#define GLS_LATE_PREFETCH 0
+#endif
   for (int base = 0; base < ncell; base += step)
     {
+      // GLS_LATE_PREFETCH: a round's geometry and tables are issued at the
+      // start of that round (in flight during its evaluate sweeps) instead
+      // of before the previous round's integrate sweeps: fewer registers
+      // live across the integrate sweeps
+      if (GLS_LATE_PREFETCH && base > 0)
+        load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, base + wave * CPW + slot,
+                                   in_wave, p, pa, cur);
 
       // ---- evaluate: x sweep straight from the src lattice, then y (, z)
       {
@@ -611,17 +671,31 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
               }
         }
       T vr[nc], gr[nc][dim];
-        qpoint_physics<dim, T, MODE>(val, val[dim], gu, gp, cur.U, cur.GU, cur.GP, cur.UT,
-                                     cur.oldg, cur.d1, cur.d2, a.nu, a.w0, a.theta, a.td,
+      T d1 = cur.d1, d2 = cur.d2;
+      if (GLS_DELTA_OTF && !a.cw)
+        {
+          T u2 = 0;
+#pragma unroll
+          for (int d = 0; d < dim; ++d)
+            u2 += cur.U[d] * cur.U[d];
+          delta_qwise(u2, cur.h, a.nu, a.stau, d1, d2);
+        }
+      if constexpr (MODE == MODE_NEWTON && GLS_NEWTON_T1)
+        qpoint_newton_t1<dim, T>(val, val[dim], gu, gp, cur.U, cur.GU, cur.T1, d1, d2, a.nu,
+                                 a.w0, a.td, vr, gr);
+      else
+        qpoint_physics<dim, T, MODE>(val, val[dim], gu, gp, cur.U, cur.GU, cur.T1, cur.UT,
+                                     cur.oldg, d1, d2, a.nu, a.w0, a.theta, a.td,
                                      a.have_prev, a.have_old_grad, vr, gr);
       // submit_value / submit_gradient (JxW, J^{-T}); inactive lanes: JxW 0
-      T wq[nc], ghat[dim][nc];
+      const T JxW = jxw<dim, k, T, MODE>(cur, general, a.sh, pa);
+      T       wq[nc], ghat[dim][nc];
       if (general)
         {
 #pragma unroll
           for (int c = 0; c < nc; ++c)
             {
-              wq[c] = vr[c] * cur.JxW;
+              wq[c] = vr[c] * JxW;
 #pragma unroll
               for (int i = 0; i < dim; ++i)
                 {
@@ -629,7 +703,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
 #pragma unroll
                   for (int e = 0; e < dim; ++e)
                     s += cur.inv[i][e] * gr[c][e];
-                  ghat[i][c] = s * cur.JxW;
+                  ghat[i][c] = s * JxW;
                 }
             }
         }
@@ -638,11 +712,11 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
           T sc[dim];
 #pragma unroll
           for (int i = 0; i < dim; ++i)
-            sc[i] = cur.inv[i][i] * cur.JxW;
+            sc[i] = cur.inv[i][i] * JxW;
 #pragma unroll
           for (int c = 0; c < nc; ++c)
             {
-              wq[c] = vr[c] * cur.JxW;
+              wq[c] = vr[c] * JxW;
 #pragma unroll
               for (int i = 0; i < dim; ++i)
                 ghat[i][c] = gr[c][i] * sc[i];
@@ -699,7 +773,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       GLS_STAMP(brick, base == 0 ? 3 : 5);
       const int  li_now     = cur.li;
       const bool active_now = cur.active;
-      if (base + step < ncell)
+      if (!GLS_LATE_PREFETCH && base + step < ncell)
         load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, base + step + wave * CPW + slot,
                                    in_wave, p, pa, cur);
       wave_sync();

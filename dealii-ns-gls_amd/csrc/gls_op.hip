@@ -193,6 +193,37 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
     for (int64_t b = 0; b < nb_full; ++b)
       if (ghosted[b] == pass)
         order.push_back(b);
+  int64_t n_interior = 0;
+  while (n_interior < nb_full - n_split && !ghosted[order[n_interior]])
+    ++n_interior;
+  // XCD-aware launch order: workgroup i of a launch is dispatched to XCD
+  // i % 8, each XCD with its own L2.  Consecutive bricks of the mesh order
+  // (the z layers of one refined coarse cell) share a lattice plane of src
+  // nodes, so each XCD gets a contiguous run of bricks: launch slot i holds
+  // brick start(i % 8) + i / 8 of the segment (a bijection for any length).
+  // Applied to the interior and the boundary segment separately (they are
+  // separate launches in the partitioned vmult); the split tail keeps its
+  // LPT order.  GLS_XCD_REMAP=0 disables it.
+  {
+    const char *e     = getenv("GLS_XCD_REMAP");
+    const bool  remap = !e || std::atoi(e) != 0;
+    auto        xcd   = [&](int64_t b0, int64_t b1) {
+      const int64_t G = b1 - b0, q = G / 8, r = G % 8;
+      if (G < 16)
+        return;
+      std::vector<int64_t> seg(order.begin() + b0, order.begin() + b1);
+      for (int64_t i = 0; i < G; ++i)
+        {
+          const int64_t x = i % 8, j = i / 8;
+          order[b0 + i] = seg[x * q + std::min<int64_t>(x, r) + j];
+        }
+    };
+    if (remap)
+      {
+        xcd(0, n_interior);
+        xcd(n_interior, nb_full - n_split);
+      }
+  }
   std::vector<uint32_t> bcell0((size_t)nb), bncell((size_t)nb);
   for (int64_t b = 0; b < nb_full - n_split; ++b)
     bcell0[b] = (uint32_t)(order[b] * cpb), bncell[b] = (uint32_t)cpb;
@@ -202,9 +233,6 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
       bcell0[b] = (uint32_t)(order[nb_full - n_split + h / 2] * cpb + (h % 2) * (cpb / 2));
       bncell[b] = (uint32_t)(cpb / 2);
     }
-  int64_t n_interior = 0;
-  while (n_interior < nb_full - n_split && !ghosted[order[n_interior]])
-    ++n_interior;
   std::vector<uint32_t> bnodes((size_t)nb * L, UINT32_MAX);
   for (int64_t b = 0; b < nb; ++b)
     for (int64_t lc = 0; lc < (int64_t)bncell[b]; ++lc)
@@ -335,7 +363,37 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
                       std::max<size_t>(1, (size_t)slot * (dim + 1) * op->tsize())));
 }
 
-// host twin of gls::tab_index (kernels.h)
+// storage field (kernels.h Fields) of canonical host field f: the host
+// layout of gls_op_upload_tables / download_tables is delta1, delta2,
+// U(dim), gradU(dim^2), gradP(dim), Ut_old(dim)
+template <int dim>
+int
+storage_field_t(int f)
+{
+  using F = Fields<dim>;
+  if (f == 0)
+    return F::D1;
+  if (f == 1)
+    return F::D2;
+  f -= 2;
+  if (f < dim)
+    return F::U + f;
+  f -= dim;
+  if (f < dim * dim)
+    return F::GU + f;
+  f -= dim * dim;
+  if (f < dim)
+    return F::GP + f;
+  return F::UT + (f - dim);
+}
+
+int
+storage_field(const glsOp_ *op, int f)
+{
+  return op->dim == 3 ? storage_field_t<3>(f) : storage_field_t<2>(f);
+}
+
+// host twin of gls::tab_index (kernels.h), f a storage field
 size_t
 host_tab_index(const glsOp_ *op, int64_t c, int q, int f)
 {
@@ -351,7 +409,7 @@ void
 build_table_layout(glsOp_ *op)
 {
   const int     W   = (int)(16 / op->tsize());
-  const int     NG  = (op->nf + W - 1) / W;
+  const int     NG  = (op->nf_store + W - 1) / W;
   const int     nq  = op->nq;
   const int     CPW = std::max(1, 64 / nq);
   const int64_t gs  = (int64_t)CPW * nq * W;
@@ -589,12 +647,29 @@ struct Impl
         a.nu            = (T)op->prm.nu;
         a.w0            = (T)op->prm.w0;
         a.theta         = (T)op->prm.theta;
+        a.stau          = (T)(op->prm.dt == 0.0 ? 0.0 : 1.0 / op->prm.dt);
         a.td            = ((op->prm.flags & GLS_CONSIDER_TIME_DERIVATIVE) && op->prm.order > 0);
         a.cw            = (op->prm.flags & GLS_CELL_WISE_STAB) ? 1 : 0;
         a.have_prev     = op->have_prev ? 1 : 0;
         a.have_old_grad = (op->have_old_grad && op->prm.theta != 1.0) ? 1 : 0;
         a.sh            = make_shape<T, n>(op->basis);
         const size_t lds = BrickLDS<dim, k, T>::bytes(a.LP);
+        if ((what & BRICK_RUN) && b1 > b0 && mode == MODE_NEWTON && GLS_NEWTON_T1)
+          {
+            // T1 (Fields::T1) from the current tables and time weights
+            if (!op->t1_valid || op->t1_w0 != op->prm.w0 || op->t1_td != a.td)
+              {
+                const int64_t nqc = op->n_cells * nq;
+                if (nqc > 0)
+                  hipLaunchKernelGGL((k_finalize_t1<dim, T>), dim3((unsigned)((nqc + 255) / 256)),
+                                     dim3(256), 0, s, (T *)op->d_tab, op->d_tab_cbase,
+                                     op->tab_gs, op->n_cells, nq, (T)op->prm.w0, a.td);
+                HIP_THROW(hipGetLastError());
+                op->t1_valid = true;
+                op->t1_w0    = op->prm.w0;
+                op->t1_td    = a.td;
+              }
+          }
         if ((what & BRICK_RUN) && b1 > b0)
           {
             if (mode == MODE_NEWTON)
@@ -1100,6 +1175,7 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
   const int dim = d->dim, n = d->degree + 1;
   op->nq            = dim == 3 ? n * n * n : n * n;
   op->nf            = 2 + 3 * dim + dim * dim;
+  op->nf_store      = dim == 3 ? Fields<3>::N : Fields<2>::N;
   HIP_THROW(hipGetDevice(&op->device));
   const int nq = op->nq;
 
@@ -1376,6 +1452,7 @@ gls_op_set_linearization_point(glsOp op, const void *vec, void *stream)
   pf(op, 0, op->stage.in_vec(vec, 0, s), s);
   op->stage.done(s);
   op->have_lin = true;
+  op->t1_valid = false;
   GLS_CATCH
 }
 
@@ -1417,6 +1494,7 @@ gls_op_set_previous_solution(glsOp op, const void *const *hist, int n_hist,
   HIP_THROW(hipGetLastError());
   pf(op, 1, op->d_tmp, s);
   op->have_prev = true;
+  op->t1_valid  = false;
   if (op->prm.theta != 1.0)
     {
       if (!op->d_old_grad)
@@ -1697,7 +1775,8 @@ gls_op_upload_tables(glsOp op, const double *tables, const double *cellwise)
   for (int64_t c = 0; c < op->n_cells; ++c)
     for (int q = 0; q < op->nq; ++q)
       for (int f = 0; f < op->nf; ++f)
-        soa[host_tab_index(op, c, q, f)] = tables[((size_t)c * op->nq + q) * op->nf + f];
+        soa[host_tab_index(op, c, q, storage_field(op, f))] =
+          tables[((size_t)c * op->nq + q) * op->nf + f];
   std::vector<double> cw((size_t)2 * op->n_cells, 0.0);
   if (cellwise)
     for (int64_t c = 0; c < op->n_cells; ++c)
@@ -1719,6 +1798,29 @@ gls_op_upload_tables(glsOp op, const double *tables, const double *cellwise)
     }
   op->have_lin  = true;
   op->have_prev = op->prm.order > 0;
+  // the H field from the cell geometry (the uploaded tables carry delta only)
+  {
+    const int64_t nqc = op->n_cells * op->nq;
+    const dim3    g((unsigned)((nqc + 255) / 256));
+    if (nqc > 0)
+      {
+        if (op->prec == GLS_F64 && op->dim == 3)
+          hipLaunchKernelGGL((k_fill_h<3, double>), g, dim3(256), 0, 0, (double *)op->d_tab,
+                             op->d_tab_cbase, op->tab_gs, (const double *)op->d_hq, op->n_cells, op->nq);
+        else if (op->prec == GLS_F64)
+          hipLaunchKernelGGL((k_fill_h<2, double>), g, dim3(256), 0, 0, (double *)op->d_tab,
+                             op->d_tab_cbase, op->tab_gs, (const double *)op->d_hq, op->n_cells, op->nq);
+        else if (op->dim == 3)
+          hipLaunchKernelGGL((k_fill_h<3, float>), g, dim3(256), 0, 0, (float *)op->d_tab,
+                             op->d_tab_cbase, op->tab_gs, (const float *)op->d_hq, op->n_cells, op->nq);
+        else
+          hipLaunchKernelGGL((k_fill_h<2, float>), g, dim3(256), 0, 0, (float *)op->d_tab,
+                             op->d_tab_cbase, op->tab_gs, (const float *)op->d_hq, op->n_cells, op->nq);
+        HIP_THROW(hipGetLastError());
+        HIP_THROW(hipDeviceSynchronize());
+      }
+  }
+  op->t1_valid = false;
   GLS_CATCH
 }
 
@@ -1747,7 +1849,8 @@ gls_op_download_tables(glsOp op, double *tables, double *cellwise)
     for (int64_t c = 0; c < op->n_cells; ++c)
       for (int q = 0; q < op->nq; ++q)
         for (int f = 0; f < op->nf; ++f)
-          tables[((size_t)c * op->nq + q) * op->nf + f] = soa[host_tab_index(op, c, q, f)];
+          tables[((size_t)c * op->nq + q) * op->nf + f] =
+            soa[host_tab_index(op, c, q, storage_field(op, f))];
   if (cellwise)
     for (int64_t c = 0; c < op->n_cells; ++c)
       {
@@ -1775,17 +1878,38 @@ gls_op_vmult_bytes(glsOp op)
 {
   if (!op)
     return 0;
-  // B_tab = s 2N + s C nq n_tab + s [n_gen nq (dim^2+1) +
-  //                     n_cart (dim+1)] + 4 C nq
+  // B = s 2N + s C nq n_tab + s [n_gen nq (dim^2+1) +
+  //                 n_cart (dim+1)] + 4 C nq,
+  // with n_tab the table values per q this build streams: the brick kernel's
+  // Newton vmult reads U, grad U, T1 and h (16 in 3D; delta_1/2 recomputed,
+  // kernels.h Fields), in whole 16-byte groups; the per-cell path the
+  // reference's 20 (operator_ns.h:120-132)
   const double s   = (double)op->tsize();
   const int    dim = op->dim;
   const bool   td  = (op->prm.flags & GLS_CONSIDER_TIME_DERIVATIVE) && op->prm.order > 0;
+  const bool   nt  = (op->prm.flags & GLS_INCREMENT_FORM) != 0;
   int          n_tab;
-  if (op->prm.flags & GLS_INCREMENT_FORM)
+  if (op->use_brick)
+    {
+      const int W = (int)(16 / op->tsize());
+      n_tab       = 0;
+      for (int g = 0; g * W < op->nf_store; ++g)
+        {
+          bool any = false;
+          for (int w = 0; w < W; ++w)
+            {
+              const int f = g * W + w;
+              any = any || (dim == 3 ? (nt ? field_read<3, MODE_NEWTON>(f) : field_read<3, MODE_FIXED>(f))
+                                     : (nt ? field_read<2, MODE_NEWTON>(f) : field_read<2, MODE_FIXED>(f)));
+            }
+          n_tab += any ? W : 0;
+        }
+    }
+  else if (nt)
     n_tab = 2 + dim + dim * dim + dim + (td ? dim : 0);
   else
     n_tab = 2 + dim;
-  if (op->prm.flags & GLS_CELL_WISE_STAB)
+  if (!op->use_brick && (op->prm.flags & GLS_CELL_WISE_STAB))
     n_tab -= 2;
   const double C = (double)op->n_cells, nq = (double)op->nq;
   double b = s * 2.0 * (double)op->n_dofs + s * C * nq * n_tab +

@@ -59,8 +59,22 @@ enum Mode
 template <int dim>
 struct Fields
 {
-  static constexpr int D1 = 0, D2 = 1, U = 2, GU = 2 + dim, GP = 2 + dim + dim * dim,
-                       UT = 2 + 2 * dim + dim * dim, N = 2 + 3 * dim + dim * dim;
+  // Table fields per (cell, q), in the order the brick kernel streams them:
+  //   U = u_star_value, GU = u_star_gradient (operator_ns.h:126-127),
+  //   T1 = the linearization-point part of the Newton SUPG residual R1
+  //        (operator_ns.cc:1146-1151 without delta_1):
+  //        (td ? w0 U + Ut_old : 0) + grad P* + (grad U) U, formed by
+  //        k_finalize_t1 once the producers and the time weights are set,
+  //   H  = the cell's q-wise h (operator_ns.cc:394-405), from which the
+  //        brick kernel recomputes delta_1 / delta_2 (:407-420),
+  //   D1, D2 = delta_1_q, delta_2_q, UT = u_time_derivative_old,
+  //   GP = p_star_gradient (operator_ns.h:123-130).
+  // A Newton vmult of the brick kernel reads U, GU, T1, H only (16 of the
+  // reference's 20 values per q); D1, D2, GP, UT stay for the other paths.
+  static constexpr int U = 0, GU = dim, T1 = dim + dim * dim, H = 2 * dim + dim * dim,
+                       D1 = H + 1, D2 = H + 2, UT = H + 3, GP = H + 3 + dim,
+                       N = H + 3 + 2 * dim;
+  static constexpr int NEWTON = H + 1; // leading fields of a Newton brick vmult
 };
 
 // Per-q tables (set_linearization_point / set_previous_solution outputs,
@@ -177,7 +191,126 @@ contract(const T *in, const T (*M)[n], int pa, int base, int s)
   return acc;
 }
 
+// q-wise stabilisation parameters, operator_ns.cc:407-420 (|U|^2 with the
+// 1e-12 floor): the producer (tables) and the Newton brick kernel (on the
+// fly from U and h) evaluate the same expression
+template <typename T>
+__device__ __forceinline__ void
+delta_qwise(T u2, T h, T nu, T stau, T &d1, T &d2)
+{
+  const T umag2 = T(1e-12) + u2;
+  const T fac   = T(4) * nu / (h * h);
+  d1            = T(1) / sqrt(stau * stau + T(4) * umag2 / h / h + T(9) * fac * fac);
+  d2            = sqrt(umag2) * h * T(0.5);
+}
+
 // ------------------------------------------------------------ q-point physics
+// Newton increment branch (operator_ns.cc:1067-1181) with the
+// linearization-point part of R1 precomputed: T1 = (td ? w0 U + Ut_old : 0)
+// + grad P* + (grad U) U (k_finalize_t1), so R1 = delta_1 T1.  Same values as
+// qpoint_physics<MODE_NEWTON>, fewer table loads and operations.
+template <int dim, typename T>
+__device__ __forceinline__ void
+qpoint_newton_t1(const T *u, T p, const T (*gu)[dim], const T *gp, const T *U,
+                 const T (*GU)[dim], const T *T1, T d1, T d2, T nu, T w0, int td, T *vr,
+                 T (*gr)[dim])
+{
+  T ut[dim], sgu[dim], ugs[dim], divu = 0;
+#pragma unroll
+  for (int d = 0; d < dim; ++d)
+    {
+      ut[d] = u[d] * w0;
+      divu += gu[d][d];
+      sgu[d] = ugs[d] = 0;
+#pragma unroll
+      for (int e = 0; e < dim; ++e)
+        {
+          sgu[d] += gu[d][e] * U[e];
+          ugs[d] += GU[d][e] * u[e];
+        }
+    }
+#pragma unroll
+  for (int d = 0; d < dim; ++d)
+    {
+      vr[d] = ut[d] + sgu[d] + ugs[d];
+#pragma unroll
+      for (int e = 0; e < dim; ++e)
+        gr[d][e] = 0;
+      gr[d][d] = gu[d][d] * (T(2) * nu) - p;
+    }
+#pragma unroll
+  for (int e = 0; e < dim; ++e)
+#pragma unroll
+    for (int d = e + 1; d < dim; ++d)
+      {
+        const T tmp = (gu[d][e] + gu[e][d]) * nu; // symm_scalar_product_add :899-916
+        gr[d][e] += tmp;
+        gr[e][d] += tmp;
+      }
+  T r0[dim], r1[dim];
+#pragma unroll
+  for (int d = 0; d < dim; ++d)
+    {
+      r0[d] = d1 * ((td ? ut[d] : T(0)) + gp[d] + sgu[d] + ugs[d]);
+      r1[d] = d1 * T1[d];
+    }
+#pragma unroll
+  for (int d0 = 0; d0 < dim; ++d0)
+#pragma unroll
+    for (int e = 0; e < dim; ++e)
+      gr[d0][e] += U[e] * r0[d0] + u[e] * r1[d0];
+#pragma unroll
+  for (int d = 0; d < dim; ++d)
+    gr[d][d] += d2 * divu;
+  vr[dim] = divu;
+#pragma unroll
+  for (int d = 0; d < dim; ++d)
+    gr[dim][d] = r0[d];
+}
+
+// T1 = (td ? w0 U + Ut_old : 0) + grad P* + (grad U) U at every (cell, q)
+// of the table (the linearization-point part of R1, operator_ns.cc:1146-1151)
+template <int dim, typename T>
+__global__ void __launch_bounds__(256)
+  k_finalize_t1(T *__restrict__ tab, const int64_t *__restrict__ cbase, int64_t gs,
+                int64_t n_cells, int nq, T w0, int td)
+{
+  using F         = Fields<dim>;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_cells * nq)
+    return;
+  const int64_t cell = g / nq;
+  const int     p    = (int)(g - cell * nq);
+  auto          TI   = [&](int f) { return tab_index<T>(cbase, gs, cell, p, f); };
+  T             U[dim];
+#pragma unroll
+  for (int d = 0; d < dim; ++d)
+    U[d] = tab[TI(F::U + d)];
+#pragma unroll
+  for (int d = 0; d < dim; ++d)
+    {
+      T s = tab[TI(F::GP + d)] + (td ? U[d] * w0 + tab[TI(F::UT + d)] : T(0));
+#pragma unroll
+      for (int e = 0; e < dim; ++e)
+        s += tab[TI(F::GU + d * dim + e)] * U[e];
+      tab[TI(F::T1 + d)] = s;
+    }
+}
+
+// the H field (the cell's q-wise h) of every (cell, q): table uploads
+template <int dim, typename T>
+__global__ void __launch_bounds__(256)
+  k_fill_h(T *__restrict__ tab, const int64_t *__restrict__ cbase, int64_t gs,
+           const T *__restrict__ h_q, int64_t n_cells, int nq)
+{
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_cells * nq)
+    return;
+  const int64_t cell = g / nq;
+  const int     p    = (int)(g - cell * nq);
+  tab[tab_index<T>(cbase, gs, cell, p, Fields<dim>::H)] = h_q[cell];
+}
+
 // do_vmult_cell, operator_ns.cc:949-1182; u/p/gu/gp are trial values and
 // REAL-space gradients at the q point; output value / gradient coefficients
 // (before JxW and J^{-T}).
@@ -840,12 +973,12 @@ __global__ void __launch_bounds__(BLOCK)
                 }
               unorm = sqrt(u2);
               // q-wise stabilisation, operator_ns.cc:394-420
-              const T h      = a.h_q[cell];
-              const T umag2  = T(1e-12) + u2;
-              const T fac    = T(4) * a.nu / (h * h);
-              a.tab[TI(F::D1)] =
-                T(1) / sqrt(a.stau * a.stau + T(4) * umag2 / h / h + T(9) * fac * fac);
-              a.tab[TI(F::D2)] = sqrt(umag2) * h * T(0.5);
+              const T h = a.h_q[cell];
+              T       d1, d2;
+              delta_qwise(u2, h, a.nu, a.stau, d1, d2);
+              a.tab[TI(F::D1)] = d1;
+              a.tab[TI(F::D2)] = d2;
+              a.tab[TI(F::H)]  = h;
             }
         }
     }

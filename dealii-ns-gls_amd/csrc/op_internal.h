@@ -47,7 +47,13 @@ struct glsOp_
 {
   int     dim = 3, degree = 2, prec = GLS_F64;
   int64_t n_cells = 0, n_nodes = 0, n_owned_nodes = 0, n_dofs = 0, n_owned_dofs = 0;
-  int     nq = 0, nf = 0;
+  int     nq = 0, nf = 0; // nf: fields of the canonical host table layout (upload/download)
+  int     nf_store = 0;    // fields stored per (cell, q) on the device (kernels.h Fields)
+  // T1 (Fields::T1) is formed from the producers' tables and the time
+  // weights; recomputed before a Newton brick vmult when either changed
+  mutable bool   t1_valid = false;
+  mutable double t1_w0    = 0.0;
+  mutable int    t1_td    = -1;
   gls::Basis1D basis{1};
 
   glsOpParams prm{};
