@@ -123,6 +123,8 @@ struct BrickArgs
   const T        *rb;
   const T        *rd;
   T               romega;
+  int             rkeep; // 1: src + omega rd (rb - A src); 0: omega rd (rb - A src)
+                         // (rd null: 1) — the multigrid residual b - A x
   int64_t         brick_begin, brick_end;
   int             bx, by, bz;
   int             L, Lx, Ly;
@@ -850,7 +852,8 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
               for (int c = 0; c < nc; ++c)
                 {
                   const size_t j = (size_t)tgt * nc + c;
-                  r[c]           = a.src[j] + a.romega * a.rd[j] * (a.rb[j] - r[c]);
+                  const T  base  = a.rkeep ? a.src[j] : T(0);
+                  r[c]           = base + a.romega * (a.rd ? a.rd[j] : T(1)) * (a.rb[j] - r[c]);
                 }
           store_node<T, nc>(a.dst, tgt, r);
         }
@@ -869,7 +872,7 @@ __global__ void __launch_bounds__(256)
                   const T *__restrict__ partial, const uint32_t *__restrict__ nodes,
                   const uint32_t *__restrict__ offsets, int64_t n_shared,
                   const T *__restrict__ rb = nullptr, const T *__restrict__ rd = nullptr,
-                  T romega = T(0))
+                  T romega = T(0), int keep = 1)
 {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= n_shared * nc)
@@ -903,7 +906,7 @@ __global__ void __launch_bounds__(256)
   if (!R && rb)
     {
       const size_t j = (size_t)node * nc + c;
-      sum            = src[j] + romega * rd[j] * (rb[j] - sum);
+      sum            = (keep ? src[j] : T(0)) + romega * (rd ? rd[j] : T(1)) * (rb[j] - sum);
     }
   dst[(size_t)node * nc + c] = sum;
 }
@@ -918,7 +921,7 @@ __global__ void __launch_bounds__(256)
                       const T *__restrict__ partial, const uint32_t *__restrict__ nodes,
                       const ReduceClasses rc, int64_t n_shared,
                       const T *__restrict__ rb = nullptr, const T *__restrict__ rd = nullptr,
-                      T romega = T(0))
+                      T romega = T(0), int keep = 1)
 {
   // 16-byte packs when a node's row is whole packs (nc = 4): one thread per
   // (node, pack), vector loads and stores
@@ -966,9 +969,9 @@ __global__ void __launch_bounds__(256)
       if (!R && rb)
         {
           const size_t j  = (size_t)node * NPK + kp;
-          const V      xs = reinterpret_cast<const V *>(src)[j];
-          sum = xs + romega * reinterpret_cast<const V *>(rd)[j] *
-                       (reinterpret_cast<const V *>(rb)[j] - sum);
+          const V      xs = keep ? reinterpret_cast<const V *>(src)[j] : V{};
+          const V      dj = rd ? reinterpret_cast<const V *>(rd)[j] : V{} + T(1);
+          sum = xs + romega * dj * (reinterpret_cast<const V *>(rb)[j] - sum);
         }
       reinterpret_cast<V *>(dst)[(size_t)node * NPK + kp] = sum;
       return;
@@ -1009,7 +1012,7 @@ __global__ void __launch_bounds__(256)
   if (!R && rb)
     {
       const size_t j = (size_t)node * nc + c;
-      sum            = src[j] + romega * rd[j] * (rb[j] - sum);
+      sum            = (keep ? src[j] : T(0)) + romega * (rd ? rd[j] : T(1)) * (rb[j] - sum);
     }
   dst[(size_t)node * nc + c] = sum;
 }

@@ -139,8 +139,16 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
   // CUs leave a 32-brick second round) and the padded LDS lattice of a
   // 4x4x1 layer keeps 3 workgroups per CU (measured 59.6 -> 53.7 us before
   // the LDS re-layout)
+  // Small bricks (bx by <= 4: the r1 level of a 2x2x2-refined coarse mesh)
+  // keep up to 8 cells (bz layers) per brick: one round of the workgroup's
+  // 4 waves x 2 cells instead of a 4-cell layer with two idle waves
   if (dim == 3)
-    bz = 1;
+    {
+      int z = 1;
+      while (bx * by * z * 2 <= 8 && bz % (z * 2) == 0)
+        z *= 2;
+      bz = z;
+    }
   const int64_t cpb = (int64_t)bx * by * bz;
   if (d->n_cells % cpb != 0)
     throw std::runtime_error("gls_op_create: n_cells is not a multiple of the brick size");
@@ -148,7 +156,7 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
   const int L  = Lx * Ly * Lz;
   const int side_max = k * (dim == 3 ? 4 : 8) + 1;
   const int lmax     = dim == 3 ? side_max * side_max * (k + 1) : side_max * side_max;
-  if (L > lmax || lmax > 729 || (dim == 3 && (bx > 4 || by > 4 || bz > 1)) ||
+  if (L > lmax || lmax > 729 || (dim == 3 && (bx > 4 || by > 4 || bx * by * bz > 16)) ||
       (dim == 2 && (bx > 8 || by > 8)))
     return; // lattice does not fit the brick kernel's LDS: per-cell path
   const int64_t nb_full = d->n_cells / cpb;
@@ -630,6 +638,7 @@ struct Impl
         a.rb            = rx ? (const T *)rx->b : nullptr;
         a.rd            = rx ? (const T *)rx->d : nullptr;
         a.romega        = rx ? (T)rx->omega : T(0);
+        a.rkeep         = rx ? (rx->keep ? 1 : 0) : 1;
         a.brick_begin   = b0;
         a.brick_end     = b1;
         a.bx            = op->bx;
@@ -695,7 +704,8 @@ struct Impl
             else if (rc.n > 0)
               hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, false>), g3, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)op->d_partial,
-                                 op->d_shared_nodes, rc, op->n_shared, a.rb, a.rd, a.romega);
+                                 op->d_shared_nodes, rc, op->n_shared, a.rb, a.rd, a.romega,
+                                 a.rkeep);
             else if (mode == MODE_RESIDUAL)
               hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, true>), g2, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)op->d_partial,
@@ -704,12 +714,36 @@ struct Impl
               hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, false>), g2, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)op->d_partial,
                                  op->d_shared_nodes, op->d_shared_off, op->n_shared, a.rb,
-                                 a.rd, a.romega);
+                                 a.rd, a.romega, a.rkeep);
             HIP_THROW(hipGetLastError());
           }
       }
     else
       throw std::runtime_error("brick kernel not available for this (dim, degree)");
+  }
+
+  // element-matrix diagonal by direct evaluation (k_diag), assembled into
+  // diag (zeroed by the caller)
+  static void
+  diag(const glsOp_ *op, int mode, double *diag_out, hipStream_t s)
+  {
+    DiagArgs<T, dim, n> da;
+    da.a            = args(op);
+    da.diag         = diag_out;
+    da.a.cell_begin = 0;
+    da.a.cell_end   = op->n_cells;
+    for (int q = 0; q < n; ++q)
+      for (int i = 0; i < n; ++i)
+        da.D[q][i] = (T)op->basis.D[q * n + i];
+    constexpr int CPB = (64 / nq > 0 ? 64 / nq : 1) * (BLOCK / 64);
+    const dim3    grid((unsigned)((op->n_cells + CPB - 1) / CPB));
+    if (op->n_cells == 0)
+      return;
+    if (mode == MODE_NEWTON)
+      hipLaunchKernelGGL((k_diag<dim, k, T, MODE_NEWTON>), grid, dim3(BLOCK), 0, s, da);
+    else
+      hipLaunchKernelGGL((k_diag<dim, k, T, MODE_FIXED>), grid, dim3(BLOCK), 0, s, da);
+    HIP_THROW(hipGetLastError());
   }
 
   static void
@@ -747,6 +781,24 @@ struct Impl
 
 using ApplyFn   = void (*)(const glsOp_ *, int, bool, void *, const void *, int64_t, int64_t,
                          hipStream_t);
+using DiagFn    = void (*)(const glsOp_ *, int, double *, hipStream_t);
+
+template <typename T>
+DiagFn
+select_diag_t(int dim, int k)
+{
+#define GLS_CASE(D, K)     \
+  if (dim == D && k == K)  \
+    return &Impl<D, K, T>::diag;
+  GLS_CASE(2, 1)
+  GLS_CASE(2, 2)
+  GLS_CASE(2, 3)
+  GLS_CASE(3, 1)
+  GLS_CASE(3, 2)
+  GLS_CASE(3, 3)
+#undef GLS_CASE
+  return nullptr;
+}
 using ProduceFn = void (*)(const glsOp_ *, int, const void *, hipStream_t);
 
 template <typename T>
@@ -1414,6 +1466,7 @@ gls_op_set_parameters(glsOp op, const glsOpParams *prm)
     throw std::runtime_error("consider_time_derivative requires theta == 1 "
                              "(operator_ns.cc:126-129)");
   op->prm = *prm;
+  op->version++;
   GLS_CATCH
 }
 
@@ -1453,6 +1506,7 @@ gls_op_set_linearization_point(glsOp op, const void *vec, void *stream)
   op->stage.done(s);
   op->have_lin = true;
   op->t1_valid = false;
+  op->version++;
   GLS_CATCH
 }
 
@@ -1495,6 +1549,7 @@ gls_op_set_previous_solution(glsOp op, const void *const *hist, int n_hist,
   pf(op, 1, op->d_tmp, s);
   op->have_prev = true;
   op->t1_valid  = false;
+  op->version++;
   if (op->prm.theta != 1.0)
     {
       if (!op->d_old_grad)
@@ -1751,6 +1806,33 @@ op_inverse_diagonal_device(glsOp op, void *diag, hipStream_t s)
   ApplyFn   af;
   ProduceFn pf;
   select(op, af, pf);
+  // GLS_DIAG_UNIT=1: the unit-vector cell applies (k_apply<DIAG>, what
+  // MatrixFreeTools::compute_diagonal does) instead of the direct evaluation
+  const char *e = getenv("GLS_DIAG_UNIT");
+  if (!(e && std::atoi(e) != 0))
+    {
+      // direct element diagonals, assembled in FP64 (in place for FP64
+      // operators), inverted into the operator's precision
+      double *d64 = (double *)diag;
+      if (op->prec != GLS_F64)
+        HIP_THROW(hipMallocAsync((void **)&d64, (size_t)op->n_dofs * sizeof(double), s));
+      HIP_THROW(hipMemsetAsync(d64, 0, (size_t)op->n_dofs * sizeof(double), s));
+      (op->prec == GLS_F64 ? select_diag_t<double>(op->dim, op->degree) :
+                             select_diag_t<float>(op->dim, op->degree))(op, vmult_mode(op), d64, s);
+      if (op->prec == GLS_F64)
+        hipLaunchKernelGGL(k_invert_diag64<double>, grid1d(op->n_dofs), dim3(256), 0, s,
+                           (double *)diag, (const double *)d64, op->d_cbits, op->n_owned_dofs,
+                           op->n_dofs);
+      else
+        {
+          hipLaunchKernelGGL(k_invert_diag64<float>, grid1d(op->n_dofs), dim3(256), 0, s,
+                             (float *)diag, (const double *)d64, op->d_cbits, op->n_owned_dofs,
+                             op->n_dofs);
+          HIP_THROW(hipFreeAsync(d64, s));
+        }
+      HIP_THROW(hipGetLastError());
+      return;
+    }
   HIP_THROW(hipMemsetAsync(diag, 0, (size_t)op->n_dofs * op->tsize(), s));
   af(op, vmult_mode(op), true, diag, diag, 0, op->n_cells, s);
   if (op->prec == GLS_F64)
@@ -1821,6 +1903,7 @@ gls_op_upload_tables(glsOp op, const double *tables, const double *cellwise)
       }
   }
   op->t1_valid = false;
+  op->version++;
   GLS_CATCH
 }
 

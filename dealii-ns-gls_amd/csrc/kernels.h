@@ -1073,6 +1073,201 @@ k_lincomb(T *__restrict__ y, const T *x0, const T *x1, const T *x2, const T *x3,
 
 // compute_inverse_diagonal finalisation (:220-224): constrained -> 1, then
 // d <- |d| > 1e-10 ? 1/d : 1
+// compute_inverse_diagonal (operator_ns.cc:195-225) by direct evaluation of
+// the element-matrix diagonal: for the test/trial function phi_i e_c the cell
+// operator (do_vmult_cell<false>, Newton :1067-1181 or fixed point
+// :955-1066) is linear in the trial, and its c-th test row needs only the
+// c-th output row, so
+//   A_ii = sum_q JxW [V_c(phi_i e_c) phi_i + Gr_c(phi_i e_c) . grad phi_i]
+// with (trial u = phi e_c, grad u = e_c (x) grad phi):
+//   Newton  V_c = w0 phi + U.grad phi + phi dU_c/dx_c
+//           Gr_c = nu (grad phi + e_c d_c phi) + U R0_c + e_c phi R1_c
+//                  + e_c delta_2 d_c phi,
+//           R0_c = delta_1 ((td ? w0 phi : 0) + U.grad phi + phi dU_c/dx_c)
+//   fixed   V_c = w0 phi + theta U.grad phi
+//           Gr_c = nu theta (grad phi + e_c d_c phi) + U R0_c
+//                  + e_c delta_2 theta d_c phi,
+//           R0_c = delta_1 ((td ? w0 phi : 0) + theta U.grad phi)
+//   pressure (both): Gr_p = delta_1 grad phi, V_p = 0
+// (R1 = delta_1 ((td ? w0 U + Ut_old : 0) + grad P* + (grad U) U), the
+// trial-independent SUPG residual).  Instead of MatrixFreeTools::
+// compute_diagonal's dpc unit-vector cell applies (and this library's former
+// k_apply<DIAG>: one full q-point physics per (dof, q)): phase 1 stages the
+// per-q data of the workgroup's cells in LDS (one lane per (cell, q)),
+// phase 2 runs one lane per (cell, node) over the q points.  The result is
+// assembled with atomics like distribute_local_to_global (constrained
+// components skipped), then k_invert_diag.
+template <typename T, int dim, int n>
+struct DiagArgs
+{
+  ApplyArgs<T, dim, n> a;
+  T                    D[n][n]; // D[q][i] = phi_i'(x_q) (nodal basis derivative)
+  double              *diag;    // [n_dofs] FP64 accumulator (both precisions)
+};
+
+template <int dim, int k, typename T, int MODE>
+__global__ void __launch_bounds__(BLOCK)
+  k_diag(DiagArgs<T, dim, k + 1> da)
+{
+  constexpr int n   = k + 1;
+  constexpr int nq  = ipow(n, dim);
+  constexpr int nc  = dim + 1;
+  constexpr int CPW = 64 / nq > 0 ? 64 / nq : 1;
+  constexpr int CPB = CPW * (BLOCK / 64);
+  // per (cell, q): JxW, inv (dim^2), U (dim), diag grad U (dim), R1 (dim), d1, d2
+  constexpr int QF = 1 + dim * dim + 3 * dim + 2;
+  using F          = Fields<dim>;
+  const auto &a    = da.a;
+  __shared__ T sq[CPB][nq][QF];
+  __shared__ T sS[n][n], sDn[n][n];
+
+  const int t = threadIdx.x;
+  if (t < n * n)
+    {
+      sS[t / n][t % n]  = a.sh.S[t / n][t % n];
+      sDn[t / n][t % n] = da.D[t / n][t % n];
+    }
+  const int     wave    = t >> 6, lane = t & 63;
+  const int     slot    = lane / nq;
+  const int     p       = lane - slot * nq;
+  const bool    in_wave = slot < CPW;
+  const int     lc      = wave * CPW + (in_wave ? slot : 0);
+  const int64_t cell    = (int64_t)blockIdx.x * CPB + lc;
+  const bool    active  = in_wave && cell < a.cell_end;
+  const int     pa[3]   = {p % n, (p / n) % n, dim == 3 ? p / (n * n) : 0};
+  if (active)
+    {
+      // phase 1: the q point's data
+      QGeo<dim, n, T> g;
+      load_geometry<dim, n, T>(a, cell, p, pa[0], pa[1], pa[2], a.sh.w, g);
+      constexpr int TW = 16 / sizeof(T);
+      const int64_t tb = a.tab_cbase[cell] + (int64_t)p * TW;
+      auto          TI = [&](int f) { return tb + (int64_t)(f / TW) * a.tab_gs + f % TW; };
+      T             U[dim], d1, d2;
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        U[d] = a.tab[TI(F::U + d)];
+      if (a.cw)
+        {
+          d1 = a.cellwise[cell];
+          d2 = a.cellwise[a.n_cells + cell];
+        }
+      else
+        {
+          d1 = a.tab[TI(F::D1)];
+          d2 = a.tab[TI(F::D2)];
+        }
+      T *qd = sq[lc][p];
+      qd[0] = g.JxW;
+#pragma unroll
+      for (int i = 0; i < dim * dim; ++i)
+        qd[1 + i] = g.inv[i / dim][i % dim];
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        {
+          qd[1 + dim * dim + d] = U[d];
+          T gdiag = 0, r1 = 0;
+          if (MODE == MODE_NEWTON)
+            {
+              gdiag = a.tab[TI(F::GU + d * dim + d)];
+              r1    = a.tab[TI(F::GP + d)] + (a.td ? U[d] * a.w0 + a.tab[TI(F::UT + d)] : T(0));
+#pragma unroll
+              for (int e = 0; e < dim; ++e)
+                r1 += a.tab[TI(F::GU + d * dim + e)] * U[e];
+              r1 *= d1;
+            }
+          qd[1 + dim * dim + dim + d]     = gdiag;
+          qd[1 + dim * dim + 2 * dim + d] = r1;
+        }
+      qd[QF - 2] = d1;
+      qd[QF - 1] = d2;
+    }
+  __syncthreads();
+  if (!active)
+    return;
+  // phase 2: lane = (cell, node i); the diagonal entries of its nc dofs
+  const int ia[3] = {pa[0], pa[1], pa[2]};
+  // phase 2 in FP64 for both precisions (the FP32 level operators' diagonals
+  // feed the smoother's D^{-1}: summed in FP64, rounded once)
+  using R = double;
+  R     acc[nc];
+#pragma unroll
+  for (int c = 0; c < nc; ++c)
+    acc[c] = 0;
+  const R nu = a.nu, w0 = a.w0, th = MODE == MODE_NEWTON ? R(1) : R(a.theta);
+  for (int q = 0; q < nq; ++q)
+    {
+      const int qa[3] = {q % n, (q / n) % n, dim == 3 ? q / (n * n) : 0};
+      R         phi = R(1), gref[dim];
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        {
+          phi *= sS[qa[d]][ia[d]];
+          R gd = R(1);
+#pragma unroll
+          for (int e = 0; e < dim; ++e)
+            gd *= e == d ? sDn[qa[e]][ia[e]] : sS[qa[e]][ia[e]];
+          gref[d] = gd;
+        }
+      const T *qd = sq[lc][q];
+      R        gp[dim]; // real-space grad phi = J^{-T} grad_ref phi
+#pragma unroll
+      for (int e = 0; e < dim; ++e)
+        {
+          R s = 0;
+#pragma unroll
+          for (int i = 0; i < dim; ++i)
+            s += qd[1 + i * dim + e] * gref[i];
+          gp[e] = s;
+        }
+      const R  JxW = qd[0], d1 = qd[QF - 2], d2 = qd[QF - 1];
+      const T *U   = qd + 1 + dim * dim;
+      R        ugp = 0, gg = 0;
+#pragma unroll
+      for (int e = 0; e < dim; ++e)
+        {
+          ugp += U[e] * gp[e];
+          gg += gp[e] * gp[e];
+        }
+#pragma unroll
+      for (int c = 0; c < dim; ++c)
+        {
+          const R gdiag = MODE == MODE_NEWTON ? R(qd[1 + dim * dim + dim + c]) : R(0);
+          const R r1    = MODE == MODE_NEWTON ? R(qd[1 + dim * dim + 2 * dim + c]) : R(0);
+          const R adv   = th * ugp + phi * gdiag; // (U.grad) u + (u.grad) U, c-th entry
+          const R Vc    = w0 * phi + adv;
+          const R R0c   = d1 * ((a.td ? w0 * phi : R(0)) + adv);
+          // Gr_c . grad phi
+          const R grc = nu * th * (gg + gp[c] * gp[c]) + R0c * ugp + phi * r1 * gp[c] +
+                        d2 * th * gp[c] * gp[c];
+          acc[c] += JxW * (Vc * phi + grc);
+        }
+      acc[dim] += JxW * d1 * gg;
+    }
+  // distribute_local_to_global of the diagonal (constrained components skipped)
+  const uint32_t packed = a.nodes[cell * nq + p];
+  const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
+#pragma unroll
+  for (int c = 0; c < nc; ++c)
+    if (!((cm >> c) & 1))
+      unsafeAtomicAdd(da.diag + (size_t)node * nc + c, acc[c]);
+}
+
+// inverse of an FP64-assembled diagonal into the operator's precision
+template <typename T>
+__global__ void
+k_invert_diag64(T *__restrict__ out, const double *__restrict__ d, const uint32_t *__restrict__ cbits,
+                int64_t n_owned, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  double v = d[i];
+  if (i < n_owned && ((cbits[i >> 5] >> (i & 31)) & 1))
+    v = 1;
+  out[i] = (T)((fabs(v) > 1.0e-10) ? 1.0 / v : 1.0);
+}
+
 template <typename T>
 __global__ void
 k_invert_diag(T *__restrict__ d, const uint32_t *__restrict__ cbits, int64_t n_owned, int64_t n)

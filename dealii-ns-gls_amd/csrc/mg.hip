@@ -53,7 +53,8 @@ struct TransferArgs
 // through scratch: 28.7 us per r2 -> r1 restriction).
 template <int dim, int k, typename T>
 __global__ void __launch_bounds__(256)
-  k_prolongate(TransferArgs<T> a, T *__restrict__ dst_f, const T *__restrict__ src_c)
+  k_prolongate(TransferArgs<T> a, T *__restrict__ dst_f, const T *__restrict__ src_c,
+               const T *__restrict__ base = nullptr)
 {
   constexpr int n = k + 1, nq = ipow(n, dim), nc = dim + 1, L = 2 * k + 1;
   constexpr int nl = ipow(L, dim);
@@ -109,9 +110,12 @@ __global__ void __launch_bounds__(256)
                 }
               s += (dim == 3 ? pz[iz] : T(1)) * sy;
             }
-          const T w = a.weight[(size_t)fn * nc + comp];
-          if (w != T(0))
-            dst_f[(size_t)fn * nc + comp] += w * s;
+          const T      w = a.weight[(size_t)fn * nc + comp];
+          const size_t j = (size_t)fn * nc + comp;
+          if (base) // out of place: dst = base + w P src
+            dst_f[j] = base[j] + (w != T(0) ? w * s : T(0));
+          else if (w != T(0))
+            dst_f[j] += w * s;
         }
     }
 }
@@ -227,6 +231,25 @@ k_residual(T *__restrict__ t, const T *__restrict__ b, int64_t n)
     t[i] = b[i] - t[i];
 }
 
+// zero fill / copy as kernels: the captured V-cycle graph holds kernel
+// nodes only (graphs with captured memset / memcpy nodes were measured to
+// race on ROCm 7.2: scripts/graph_diag.py)
+__global__ void
+k_zero(uint32_t *__restrict__ x, int64_t n_words)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_words)
+    x[i] = 0u;
+}
+
+__global__ void
+k_copy(uint32_t *__restrict__ y, const uint32_t *__restrict__ x, int64_t n_words)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_words)
+    y[i] = x[i];
+}
+
 template <typename Tin, typename Tout>
 __global__ void
 k_convert(Tout *__restrict__ dst, const Tin *__restrict__ src, int64_t n)
@@ -271,6 +294,37 @@ __global__ void __launch_bounds__(256)
     {
       part[2 * blockIdx.x]     = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
       part[2 * blockIdx.x + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    }
+}
+
+// deal.II set_initial_guess + constraints.set_zero: x_i = i % 11 - mean,
+// zero on constrained components; per-block partial sums of x.x for the
+// normalisation (k_power_finish)
+template <typename T>
+__global__ void __launch_bounds__(256)
+  k_power_start(T *__restrict__ x, const uint8_t *__restrict__ cmask, int nc, double mean,
+                double *__restrict__ part, int64_t n)
+{
+  __shared__ double red[4];
+  const int64_t     i  = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double            xx = 0;
+  if (i < n)
+    {
+      const int64_t node = i / nc;
+      const int     c    = (int)(i - node * nc);
+      const double  v    = ((cmask[node] >> c) & 1) ? 0.0 : (double)(i % 11) - mean;
+      x[i]               = (T)v;
+      xx                 = v * v;
+    }
+  for (int off = 32; off > 0; off >>= 1)
+    xx += __shfl_down(xx, off);
+  if ((threadIdx.x & 63) == 0)
+    red[threadIdx.x >> 6] = xx;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    {
+      part[2 * blockIdx.x]     = 0.0;
+      part[2 * blockIdx.x + 1] = (red[0] + red[1]) + (red[2] + red[3]);
     }
 }
 
@@ -339,6 +393,17 @@ struct glsMG_
   double                  P[MAXP][MAXN]{};
   bool                    setup_done = false;
   gls::VecStage           stage; // caller layout of gls_mg_vcycle's vectors
+  // the V-cycle body (v_step on the finest level: ~80 launches between the
+  // copy_to_mg / copy_from_mg conversions, all on the multigrid's own
+  // buffers) captured once as a hipGraph and replayed on the caller's
+  // stream; re-captured after gls_mg_setup or when a level operator's state
+  // version moved (kernel arguments are captured by value).  GLS_MG_GRAPH=1
+  // enables it (off by default: measured slower, run_v_step).
+  hipGraph_t            graph      = nullptr;
+  hipGraphExec_t        graph_exec = nullptr;
+  hipStream_t           cap_stream = nullptr; // capture, then replay stream
+  hipEvent_t            ev_in = nullptr, ev_out = nullptr;
+  std::vector<uint64_t> graph_versions;
   // dense LU coarse solver (coarse_n_iterations < 0): the substitute for the
   // reference's Trilinos direct solver (multigrid.cc:448-455, 477-481)
   rocblas_handle blas   = nullptr;
@@ -371,17 +436,19 @@ targs(const glsMG_ *mg, int level)
   return a;
 }
 
-// kind: 0 prolongate_add, 1 restrict_add, 2 interpolate
+// kind: 0 prolongate_add, 1 restrict_add, 2 interpolate; base (prolongate
+// only): dst = base + P src instead of dst += P src
 template <int dim, int k, typename T>
 void
-transfer_t(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hipStream_t s)
+transfer_t(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hipStream_t s,
+           const void *base)
 {
   constexpr int nq = ipow(k + 1, dim);
   const auto    a  = targs<T>(mg, level);
   const dim3    grid((unsigned)a.n_cells_c);
   if (kind == 0)
     hipLaunchKernelGGL((k_prolongate<dim, k, T>), grid, dim3(256), 0, s, a, (T *)dst,
-                       (const T *)src);
+                       (const T *)src, (const T *)base);
   else if (kind == 1)
     hipLaunchKernelGGL((k_restrict<dim, k, T>), grid, dim3(256), 0, s, a, (T *)dst,
                        (const T *)src);
@@ -393,30 +460,32 @@ transfer_t(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hi
 
 template <typename T>
 void
-transfer_p(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hipStream_t s)
+transfer_p(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hipStream_t s,
+           const void *base)
 {
   const int d = mg->dim, k = mg->degree;
   if (d == 2 && k == 1)
-    transfer_t<2, 1, T>(mg, kind, level, dst, src, s);
+    transfer_t<2, 1, T>(mg, kind, level, dst, src, s, base);
   else if (d == 2 && k == 2)
-    transfer_t<2, 2, T>(mg, kind, level, dst, src, s);
+    transfer_t<2, 2, T>(mg, kind, level, dst, src, s, base);
   else if (d == 3 && k == 1)
-    transfer_t<3, 1, T>(mg, kind, level, dst, src, s);
+    transfer_t<3, 1, T>(mg, kind, level, dst, src, s, base);
   else if (d == 3 && k == 2)
-    transfer_t<3, 2, T>(mg, kind, level, dst, src, s);
+    transfer_t<3, 2, T>(mg, kind, level, dst, src, s, base);
   else
     throw std::runtime_error("multigrid transfer: degree must be 1 or 2");
 }
 
 void
-transfer(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hipStream_t s)
+transfer(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hipStream_t s,
+         const void *base = nullptr)
 {
   if (level < 1 || level >= (int)mg->ops.size())
     throw std::runtime_error("multigrid transfer: level out of range");
   if (mg->prec == GLS_F64)
-    transfer_p<double>(mg, kind, level, dst, src, s);
+    transfer_p<double>(mg, kind, level, dst, src, s, base);
   else
-    transfer_p<float>(mg, kind, level, dst, src, s);
+    transfer_p<float>(mg, kind, level, dst, src, s, base);
 }
 
 void
@@ -437,48 +506,67 @@ relax_t(const glsMG_ *mg, int level, void *x, const void *b, int first, hipStrea
   HIP_THROW(hipGetLastError());
 }
 
-// PreconditionRelaxation::vmult (zero start) / step, `iters` iterations
+// PreconditionRelaxation::vmult (zero start) / step, `iters` iterations;
+// the result in x.  x_in (step only): the starting iterate is in tmp[level]
+// instead of x (the multigrid's out-of-place prolongation put it there).
 void
 smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int iters,
-       hipStream_t s)
+       hipStream_t s, bool start_in_tmp = false)
 {
-  auto relax = mg->prec == GLS_F64 ? relax_t<double> : relax_t<float>;
-  int  it    = 0;
-  if (zero_start && iters > 0)
-    {
-      relax(mg, level, x, b, 1, s);
-      it = 1;
-    }
-  glsOp op = mg->ops[level];
+  auto  relax = mg->prec == GLS_F64 ? relax_t<double> : relax_t<float>;
+  glsOp op    = mg->ops[level];
+  void *tmp   = mg->tmp[level];
   if (!op->use_brick || op->n_owned_dofs != op->n_dofs)
     {
+      int it = 0;
+      if (start_in_tmp)
+        {
+          const int64_t w = (int64_t)((size_t)op->n_dofs * mg->ts() / 4);
+          hipLaunchKernelGGL(k_copy, g1(w), dim3(256), 0, s, (uint32_t *)x, (const uint32_t *)tmp,
+                             w);
+          HIP_THROW(hipGetLastError());
+        }
+      if (zero_start && iters > 0)
+        {
+          relax(mg, level, x, b, 1, s);
+          it = 1;
+        }
       for (; it < iters; ++it)
         {
-          gls::op_vmult_device(op, mg->tmp[level], x, s);
+          gls::op_vmult_device(op, tmp, x, s);
           relax(mg, level, x, b, 0, s);
         }
       return;
     }
   // brick operators: the step x + omega D^{-1} (b - A x) is fused into the
   // vmult's write-out (k_brick, k_shared_reduce_cls), ping-ponging between x
-  // and tmp; an odd count starts with one unfused step so the result lands
-  // in x without a copy
-  if ((iters - it) % 2 == 1)
+  // and tmp; the start buffer is chosen so that the last step lands in x
+  // (zero start: the first iterate omega D^{-1} b goes to tmp when the
+  // remaining count is odd), a final copy otherwise
+  int   it  = 0;
+  void *cur = start_in_tmp ? tmp : x;
+  if (zero_start && iters > 0)
     {
-      gls::op_vmult_device(op, mg->tmp[level], x, s);
-      relax(mg, level, x, b, 0, s);
-      ++it;
+      cur = ((iters - 1) % 2 == 1) ? tmp : x;
+      relax(mg, level, cur, b, 1, s);
+      it = 1;
     }
-  void          *cur = x, *oth = mg->tmp[level];
   gls::RelaxStep rx;
   rx.b     = b;
   rx.d     = mg->invdiag[level];
   rx.omega = mg->omega[level];
   for (; it < iters; ++it)
     {
+      void *oth = cur == x ? tmp : x;
       gls::brick_launch(op, gls::op_vmult_mode(op), oth, cur, 0, op->n_bricks,
                         gls::BRICK_RUN | gls::BRICK_REDUCE, s, &rx);
-      std::swap(cur, oth);
+      cur = oth;
+    }
+  if (cur != x)
+    {
+      const int64_t w = (int64_t)((size_t)op->n_dofs * mg->ts() / 4);
+      hipLaunchKernelGGL(k_copy, g1(w), dim3(256), 0, s, (uint32_t *)x, (const uint32_t *)cur, w);
+      HIP_THROW(hipGetLastError());
     }
 }
 
@@ -587,7 +675,12 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
             coarse_lu_solve_t<float>(mg, s);
         }
       else if (mg->desc.coarse_n_iterations == 0)
-        HIP_THROW(hipMemcpyAsync(mg->sol[0], mg->def[0], bytes, hipMemcpyDeviceToDevice, s));
+        {
+          const int64_t w = (int64_t)(bytes / 4);
+          hipLaunchKernelGGL(k_copy, g1(w), dim3(256), 0, s, (uint32_t *)mg->sol[0],
+                             (const uint32_t *)mg->def[0], w);
+          HIP_THROW(hipGetLastError());
+        }
       else
         smooth(mg, 0, mg->sol[0], mg->def[0], true, mg->desc.coarse_n_iterations, s);
       return;
@@ -595,17 +688,41 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
   const int nit = mg->desc.smoothing_n_iterations;
   // pre-smoothing from a zero initial guess (MGSmootherPrecondition::apply)
   smooth(mg, l, mg->sol[l], mg->def[l], true, nit, s);
-  // residual t = defect - A solution
-  gls::op_vmult_device(mg->ops[l], mg->tmp[l], mg->sol[l], s);
-  residual(mg, l, mg->tmp[l], mg->def[l], s);
+  // residual t = defect - A solution (fused into the brick vmult's write-out
+  // and shared-node reduction for brick operators)
+  if (mg->ops[l]->use_brick && mg->ops[l]->n_owned_dofs == mg->ops[l]->n_dofs)
+    {
+      gls::RelaxStep rs;
+      rs.b     = mg->def[l];
+      rs.omega = 1.0;
+      rs.keep  = false;
+      gls::brick_launch(mg->ops[l], gls::op_vmult_mode(mg->ops[l]), mg->tmp[l], mg->sol[l], 0,
+                        mg->ops[l]->n_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE, s, &rs);
+    }
+  else
+    {
+      gls::op_vmult_device(mg->ops[l], mg->tmp[l], mg->sol[l], s);
+      residual(mg, l, mg->tmp[l], mg->def[l], s);
+    }
   // restrict
-  HIP_THROW(hipMemsetAsync(mg->def[l - 1], 0, (size_t)mg->ops[l - 1]->n_dofs * mg->ts(), s));
+  {
+    const int64_t w = (int64_t)((size_t)mg->ops[l - 1]->n_dofs * mg->ts() / 4);
+    hipLaunchKernelGGL(k_zero, g1(w), dim3(256), 0, s, (uint32_t *)mg->def[l - 1], w);
+    HIP_THROW(hipGetLastError());
+  }
   transfer(mg, 1, l, mg->def[l - 1], mg->tmp[l], s);
   v_step(mg, l - 1, s);
-  // prolongate and add the coarse correction
-  transfer(mg, 0, l, mg->sol[l], mg->sol[l - 1], s);
+  // prolongate and add the coarse correction; with an odd number of fused
+  // smoothing steps to follow it goes out of place into tmp, so the
+  // ping-pong ends in sol without a copy
+  const bool odd = mg->ops[l]->use_brick && nit % 2 == 1 &&
+                   mg->ops[l]->n_owned_dofs == mg->ops[l]->n_dofs;
+  if (odd)
+    transfer(mg, 0, l, mg->tmp[l], mg->sol[l - 1], s, mg->sol[l]);
+  else
+    transfer(mg, 0, l, mg->sol[l], mg->sol[l - 1], s);
   // post-smoothing (MGSmootherPrecondition::smooth -> step)
-  smooth(mg, l, mg->sol[l], mg->def[l], false, nit, s);
+  smooth(mg, l, mg->sol[l], mg->def[l], false, nit, s, odd);
 }
 
 // Relaxation-factor estimate of PreconditionRelaxation with relaxation = 0
@@ -630,33 +747,20 @@ power_iteration_t(glsMG_ *mg, int l, hipStream_t s)
 {
   glsOp         op = mg->ops[l];
   const int64_t n  = op->n_dofs;
-  std::vector<double> h((size_t)n);
-  double              mean = 0;
-  for (int64_t i = 0; i < n; ++i)
-    {
-      h[i] = (double)(i % 11);
-      mean += h[i];
-    }
-  mean /= (double)std::max<int64_t>(1, n);
-  double nrm = 0;
-  for (int64_t i = 0; i < n; ++i)
-    {
-      const int64_t node = i / (op->dim + 1);
-      const int     comp = (int)(i % (op->dim + 1));
-      const bool    con  = (op->h_cmask[node] >> comp) & 1;
-      h[i]               = con ? 0.0 : h[i] - mean;
-      nrm += h[i] * h[i];
-    }
-  nrm = std::sqrt(nrm);
-  std::vector<T> hx((size_t)n);
-  for (int64_t i = 0; i < n; ++i)
-    hx[i] = (T)(nrm > 0 ? h[i] / nrm : 0.0);
-  void *x = mg->sol[l], *y = mg->tmp[l];
-  HIP_THROW(hipMemcpyAsync(x, hx.data(), n * sizeof(T), hipMemcpyHostToDevice, s));
+  void         *x = mg->sol[l], *y = mg->tmp[l];
   const int64_t nb   = (n + 255) / 256;
   double       *part = mg->d_acc, *scal = mg->d_acc + 2 * mg->acc_blocks;
   if (nb > mg->acc_blocks)
     throw std::runtime_error("power iteration: reduction buffer too small");
+  // start vector on the device: mean of i % 11 over [0, n) in closed form
+  const int64_t q11  = n / 11, r11 = n % 11;
+  const double  mean = n > 0 ? (double)(q11 * 55 + r11 * (r11 - 1) / 2) / (double)n : 0.0;
+  hipLaunchKernelGGL(k_power_start<T>, g1(n), dim3(256), 0, s, (T *)x, op->d_node_cmask,
+                     op->dim + 1, mean, part, n);
+  hipLaunchKernelGGL(k_power_finish, dim3(1), dim3(256), 0, s, (const double *)part, nb, scal);
+  hipLaunchKernelGGL(k_scale_dev<T>, g1(n), dim3(256), 0, s, (T *)x, (const T *)x,
+                     (const double *)scal, n);
+  HIP_THROW(hipGetLastError());
   HIP_THROW(hipMemsetAsync(scal, 0, 2 * sizeof(double), s));
   for (int it = 0; it < mg->desc.smoothing_eig_n_iterations; ++it)
     {
@@ -673,6 +777,79 @@ power_iteration_t(glsMG_ *mg, int l, hipStream_t s)
   HIP_THROW(hipMemcpyAsync(&lam, scal, sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_THROW(hipStreamSynchronize(s));
   return std::abs(lam);
+}
+
+// v_step(top) on stream s: replayed from a captured hipGraph when possible
+void
+run_v_step(glsMG_ *mg, int top, hipStream_t s)
+{
+  // measured (bench companion r2_vcycle_f32_coarse_relax10): the replay was
+  // slower than direct launches (0.67 vs 0.58 ms): the V-cycle is bound by
+  // the kernels' own duration, not by host launch overhead; off by default
+  const char *e   = getenv("GLS_MG_GRAPH");
+  const bool  use = (e && std::atoi(e) != 0) &&
+                   mg->desc.coarse_n_iterations >= 0; // rocSOLVER coarse LU: not captured
+  if (!use)
+    {
+      v_step(mg, top, s);
+      return;
+    }
+  std::vector<uint64_t> ver;
+  for (glsOp op : mg->ops)
+    ver.push_back(op->version);
+  if (!mg->graph_exec || ver != mg->graph_versions)
+    {
+      if (mg->graph_exec)
+        HIP_THROW(hipGraphExecDestroy(mg->graph_exec));
+      if (mg->graph)
+        HIP_THROW(hipGraphDestroy(mg->graph));
+      mg->graph_exec = nullptr;
+      mg->graph      = nullptr;
+      if (!mg->cap_stream)
+        HIP_THROW(hipStreamCreateWithFlags(&mg->cap_stream, hipStreamNonBlocking));
+      HIP_THROW(hipStreamBeginCapture(mg->cap_stream, hipStreamCaptureModeThreadLocal));
+      try
+        {
+          v_step(mg, top, mg->cap_stream);
+        }
+      catch (...)
+        {
+          hipGraph_t g = nullptr;
+          (void)hipStreamEndCapture(mg->cap_stream, &g);
+          if (g)
+            (void)hipGraphDestroy(g);
+          throw;
+        }
+      HIP_THROW(hipStreamEndCapture(mg->cap_stream, &mg->graph));
+      HIP_THROW(hipGraphInstantiate(&mg->graph_exec, mg->graph, nullptr, nullptr, 0));
+      mg->graph_versions = ver;
+    }
+  if (e && std::atoi(e) == 2) // debug: captured, but run kernel by kernel
+    {
+      v_step(mg, top, s);
+      return;
+    }
+  if (e && std::atoi(e) == 3) // debug: replay on the caller's stream, synchronised
+    {
+      HIP_THROW(hipStreamSynchronize(s));
+      HIP_THROW(hipGraphLaunch(mg->graph_exec, s));
+      HIP_THROW(hipStreamSynchronize(s));
+      return;
+    }
+  // replay on the multigrid's own stream, ordered after the caller's work
+  // (copy_to_mg) and before what follows (copy_from_mg) by events: a graph
+  // launched on the legacy NULL stream was measured NOT to wait for the
+  // preceding kernel (scripts/graph_diag.py)
+  if (!mg->ev_in)
+    {
+      HIP_THROW(hipEventCreateWithFlags(&mg->ev_in, hipEventDisableTiming));
+      HIP_THROW(hipEventCreateWithFlags(&mg->ev_out, hipEventDisableTiming));
+    }
+  HIP_THROW(hipEventRecord(mg->ev_in, s));
+  HIP_THROW(hipStreamWaitEvent(mg->cap_stream, mg->ev_in, 0));
+  HIP_THROW(hipGraphLaunch(mg->graph_exec, mg->cap_stream));
+  HIP_THROW(hipEventRecord(mg->ev_out, mg->cap_stream));
+  HIP_THROW(hipStreamWaitEvent(s, mg->ev_out, 0));
 }
 
 } // namespace
@@ -801,6 +978,16 @@ gls_mg_destroy(glsMG mg)
       (void)hipFree(p);
   if (mg->blas)
     rocblas_destroy_handle(mg->blas);
+  if (mg->graph_exec)
+    (void)hipGraphExecDestroy(mg->graph_exec);
+  if (mg->graph)
+    (void)hipGraphDestroy(mg->graph);
+  if (mg->cap_stream)
+    (void)hipStreamDestroy(mg->cap_stream);
+  if (mg->ev_in)
+    (void)hipEventDestroy(mg->ev_in);
+  if (mg->ev_out)
+    (void)hipEventDestroy(mg->ev_out);
   mg->stage.release();
   delete mg;
 }
@@ -855,6 +1042,7 @@ gls_mg_setup(glsMG mg, void *stream)
     }
   HIP_THROW(hipStreamSynchronize(s));
   mg->setup_done = true;
+  mg->graph_versions.clear(); // omega / diagonals changed: re-capture
   GLS_CATCH
 }
 
@@ -916,7 +1104,7 @@ mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s)
   else
     HIP_THROW(hipMemcpyAsync(mg->def[top], src, n * mg->ts(), hipMemcpyDeviceToDevice, s));
   HIP_THROW(hipGetLastError());
-  v_step(mg, top, s);
+  run_v_step(mg, top, s);
   // copy_from_mg
   if (cvt)
     hipLaunchKernelGGL((k_convert<float, double>), g1(n), dim3(256), 0, s, (double *)dst,

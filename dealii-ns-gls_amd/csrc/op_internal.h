@@ -58,6 +58,10 @@ struct glsOp_
 
   glsOpParams prm{};
   bool        have_lin = false, have_prev = false, have_old_grad = false;
+  // bumped by every call that changes what a launch captures by value
+  // (parameters, table producers): a captured V-cycle graph of the
+  // multigrid (csrc/mg.hip) is re-captured when a level's version moved
+  uint64_t    version = 0;
 
   // host copies the multigrid transfer setup needs
   std::vector<uint8_t>  h_cmask;      // [n_nodes]
@@ -125,8 +129,10 @@ namespace gls
 struct RelaxStep
 {
   const void *b     = nullptr;
-  const void *d     = nullptr;
+  const void *d     = nullptr; // null: 1
   double      omega = 0.0;
+  bool        keep  = true;    // false: omega d (b - A x) (with d null, omega 1: the
+                               // multigrid residual b - A x)
 };
 
 // the pieces of vmult that dist.hip / mg.hip orchestrate (gls_op.hip):
