@@ -538,6 +538,24 @@ gls_dist_update_ghost_values(glsDist d, void *vec, void *stream)
 }
 
 glsStatus
+gls_dist_compress_add(glsDist d, void *vec, void *stream)
+{
+  GLS_TRY
+  if (!d || !vec)
+    throw std::runtime_error("gls_dist_compress_add: null argument");
+  if (!d->comm)
+    throw std::runtime_error("gls_dist_compress_add: RCCL ranks only");
+  hipStream_t s = (hipStream_t)stream;
+  if (!d->peers.empty())
+    {
+      nccl_export(d, vec, s);
+      unpack(d, vec, s);
+    }
+  zero_ghosts(d, vec, s);
+  GLS_CATCH
+}
+
+glsStatus
 gls_dist_get_max_u(glsDist d, void *vec, double *u_max, void *stream)
 {
   GLS_TRY

@@ -1782,6 +1782,48 @@ gls_op_get_max_u(glsOp op, const void *vec, double *u_max, void *stream)
 }
 
 glsStatus
+gls_op_compute_diagonal(glsOp op, void *diag, void *stream)
+{
+  GLS_TRY
+  if (!op || !diag)
+    throw std::runtime_error("gls_op_compute_diagonal: null argument");
+  if (!op->have_lin)
+    throw std::runtime_error("compute_diagonal before set_linearization_point");
+  hipStream_t s   = (hipStream_t)stream;
+  double     *d64 = nullptr;
+  HIP_THROW(hipMallocAsync((void **)&d64, (size_t)op->n_dofs * sizeof(double), s));
+  HIP_THROW(hipMemsetAsync(d64, 0, (size_t)op->n_dofs * sizeof(double), s));
+  (op->prec == GLS_F64 ? select_diag_t<double>(op->dim, op->degree) :
+                         select_diag_t<float>(op->dim, op->degree))(op, vmult_mode(op), d64, s);
+  if (op->prec == GLS_F64)
+    hipLaunchKernelGGL(k_diag_out<double>, grid1d(op->n_dofs), dim3(256), 0, s, (double *)diag,
+                       (const double *)d64, op->d_cbits, op->n_owned_dofs, op->n_dofs);
+  else
+    hipLaunchKernelGGL(k_diag_out<float>, grid1d(op->n_dofs), dim3(256), 0, s, (float *)diag,
+                       (const double *)d64, op->d_cbits, op->n_owned_dofs, op->n_dofs);
+  HIP_THROW(hipGetLastError());
+  HIP_THROW(hipFreeAsync(d64, s));
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_invert_diagonal(glsOp op, void *diag, void *stream)
+{
+  GLS_TRY
+  if (!op || !diag)
+    throw std::runtime_error("gls_op_invert_diagonal: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  if (op->prec == GLS_F64)
+    hipLaunchKernelGGL(k_invert_diag<double>, grid1d(op->n_dofs), dim3(256), 0, s,
+                       (double *)diag, op->d_cbits, op->n_owned_dofs, op->n_dofs);
+  else
+    hipLaunchKernelGGL(k_invert_diag<float>, grid1d(op->n_dofs), dim3(256), 0, s, (float *)diag,
+                       op->d_cbits, op->n_owned_dofs, op->n_dofs);
+  HIP_THROW(hipGetLastError());
+  GLS_CATCH
+}
+
+glsStatus
 gls_op_compute_inverse_diagonal(glsOp op, void *diag_, void *stream)
 {
   GLS_TRY

@@ -1253,6 +1253,23 @@ __global__ void __launch_bounds__(BLOCK)
       unsafeAtomicAdd(da.diag + (size_t)node * nc + c, acc[c]);
 }
 
+// the assembled (not inverted) diagonal in the operator's precision, the
+// identity rows' 1 on constrained owned components (partitioned operators:
+// the ghost partials are added to their owners before the inversion)
+template <typename T>
+__global__ void
+k_diag_out(T *__restrict__ out, const double *__restrict__ d, const uint32_t *__restrict__ cbits,
+           int64_t n_owned, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  double v = d[i];
+  if (i < n_owned && ((cbits[i >> 5] >> (i & 31)) & 1))
+    v = 1;
+  out[i] = (T)v;
+}
+
 // inverse of an FP64-assembled diagonal into the operator's precision
 template <typename T>
 __global__ void

@@ -392,6 +392,7 @@ struct glsMG_
   int64_t                 acc_blocks = 0;
   double                  P[MAXP][MAXN]{};
   bool                    setup_done = false;
+  bool                    partitioned = false; // rank-local level operators
   gls::VecStage           stage; // caller layout of gls_mg_vcycle's vectors
   // the V-cycle body (v_step on the finest level: ~80 launches between the
   // copy_to_mg / copy_from_mg conversions, all on the multigrid's own
@@ -876,9 +877,11 @@ gls_mg_create(const glsMGDesc *desc, const glsOp *levels, const uint32_t *const 
       if (!op || op->prec != mg->prec || op->dim != mg->dim || op->degree != mg->degree)
         throw std::runtime_error("gls_mg_create: level operators must share dim, degree and "
                                  "precision");
-      if (op->n_owned_nodes != op->n_nodes)
-        throw std::runtime_error("gls_mg_create: distributed level operators are not "
-                                 "supported yet");
+      // partitioned (rank-local) level operators: the transfers
+      // (prolongate_add / restrict_add / interpolate) and the relaxation
+      // step serve the host-driven distributed multigrid (glsdist.py);
+      // setup / V-cycle / smooth are single-domain and refuse them
+      mg->partitioned = mg->partitioned || op->n_owned_nodes != op->n_nodes;
       mg->ops.push_back(op);
     }
   if (nl_levels > 1 && (!child || mg->degree > 2))
@@ -909,12 +912,19 @@ gls_mg_create(const glsMGDesc *desc, const glsOp *levels, const uint32_t *const 
       const int64_t nch = cop->n_cells * nl;
       std::vector<uint32_t> ch(child[l], child[l] + nch);
       std::vector<uint8_t>  seen((size_t)fop->n_nodes, 0);
+      // ownership of the fine nodes: the first coarse cell touching a node
+      // owns it; a lattice that already carries NOT_OWNER bits (bit 31,
+      // e.g. the global-first owners of a partitioned hierarchy) is taken as
+      // given
+      bool flagged = false;
+      for (uint32_t fn : ch)
+        flagged = flagged || (fn & NOT_OWNER);
       for (uint32_t &fn : ch)
         {
-          if ((int64_t)fn >= fop->n_nodes || fn >= NOT_OWNER)
+          if ((int64_t)(fn & ~NOT_OWNER) >= fop->n_nodes)
             throw std::runtime_error("gls_mg_create: child lattice node out of range");
-          if (seen[fn])
-            fn |= NOT_OWNER; // the first coarse cell touching a fine node owns it
+          if (!flagged && seen[fn])
+            fn |= NOT_OWNER;
           seen[fn & ~NOT_OWNER] = 1;
         }
       std::vector<double> w((size_t)fop->n_dofs, 0.0);
@@ -998,6 +1008,9 @@ gls_mg_setup(glsMG mg, void *stream)
   GLS_TRY
   if (!mg)
     throw std::runtime_error("gls_mg_setup: null handle");
+  if (mg->partitioned)
+    throw std::runtime_error("gls_mg_setup: partitioned levels are set up by the host-driven "
+                             "distributed multigrid (glsdist.py)");
   hipStream_t s = (hipStream_t)stream;
   for (size_t l = 0; l < mg->ops.size(); ++l)
     {
@@ -1071,6 +1084,28 @@ gls_mg_vcycle(glsMG mg, void *dst, const void *src, void *stream)
   gls::mg_vcycle_device(mg, y, x, s);
   mg->stage.finish_out(dst, s);
   mg->stage.done(s);
+  GLS_CATCH
+}
+
+glsStatus
+gls_mg_relax(glsMG mg, int level, void *x, const void *b, const void *ax, const void *inv_diag,
+             double omega, int zero_start, void *stream)
+{
+  GLS_TRY
+  if (!mg || level < 0 || level >= (int)mg->ops.size() || !x || !b || !inv_diag ||
+      (!zero_start && !ax))
+    throw std::runtime_error("gls_mg_relax: bad arguments");
+  const int64_t n = mg->ops[level]->n_dofs;
+  hipStream_t   s = (hipStream_t)stream;
+  if (mg->prec == GLS_F64)
+    hipLaunchKernelGGL(k_relax<double>, g1(n), dim3(256), 0, s, (double *)x, (const double *)b,
+                       (const double *)ax, (const double *)inv_diag, omega, zero_start ? 1 : 0,
+                       n);
+  else
+    hipLaunchKernelGGL(k_relax<float>, g1(n), dim3(256), 0, s, (float *)x, (const float *)b,
+                       (const float *)ax, (const float *)inv_diag, (float)omega,
+                       zero_start ? 1 : 0, n);
+  HIP_THROW(hipGetLastError());
   GLS_CATCH
 }
 

@@ -34,7 +34,8 @@ EXPORTS = [
     "gls_dist_unique_id", "gls_dist_create", "gls_dist_destroy", "gls_dist_vmult",
     "gls_dist_vmult_group", "gls_dist_interior_bricks", "gls_op_set_vector_layout",
     "gls_op_get_max_u", "gls_mg_set_vector_layout", "gls_dist_update_ghost_values",
-    "gls_dist_get_max_u",
+    "gls_dist_get_max_u", "gls_op_compute_diagonal", "gls_op_invert_diagonal", "gls_mg_relax",
+    "gls_dist_compress_add",
 ]
 
 GLS_MEM_DEVICE, GLS_MEM_HOST = 0, 1
@@ -135,6 +136,10 @@ def lib():
         L.gls_mg_set_vector_layout.argtypes = [vp, C.c_int, vp]
         L.gls_dist_update_ghost_values.argtypes = [vp, vp, vp]
         L.gls_dist_get_max_u.argtypes = [vp, vp, C.POINTER(C.c_double), vp]
+        L.gls_op_compute_diagonal.argtypes = [vp, vp, vp]
+        L.gls_op_invert_diagonal.argtypes = [vp, vp, vp]
+        L.gls_mg_relax.argtypes = [vp, C.c_int, vp, vp, vp, vp, C.c_double, C.c_int, vp]
+        L.gls_dist_compress_add.argtypes = [vp, vp, vp]
         L.gls_last_error.restype = C.c_char_p
         _lib = L
     return _lib
@@ -299,6 +304,16 @@ class NavierStokesOperator:
         _check(lib().gls_op_compute_inverse_diagonal(self.h, _vptr(diag), _stream()))
         return diag
 
+    def compute_diagonal(self, diag):
+        """Assembled (not inverted) diagonal: the rank-local half of a
+        partitioned compute_inverse_diagonal."""
+        _check(lib().gls_op_compute_diagonal(self.h, _ptr(diag), _stream()))
+        return diag
+
+    def invert_diagonal(self, diag):
+        _check(lib().gls_op_invert_diagonal(self.h, _ptr(diag), _stream()))
+        return diag
+
     def get_max_u(self, vec):
         """OperatorBase::get_max_u (operator_ns.cc:530-568): max |u(x_q)|."""
         out = C.c_double()
@@ -392,6 +407,9 @@ class PartitionedOperator:
     def update_ghost_values(self, vec):
         _check(lib().gls_dist_update_ghost_values(self.h, _ptr(vec), _stream()))
 
+    def compress_add(self, vec):
+        _check(lib().gls_dist_compress_add(self.h, _ptr(vec), _stream()))
+
     def get_max_u(self, vec):
         """get_max_u of the partitioned operator: ghost import, local max,
         RCCL all-reduce max (operator_ns.cc:540-567)."""
@@ -476,6 +494,13 @@ class Multigrid:
     def interpolate(self, level, dst_coarse, src_fine):
         _check(lib().gls_mg_interpolate(self.h, level, _ptr(dst_coarse), _ptr(src_fine),
                                         _stream()))
+
+    def relax(self, level, x, b, ax, inv_diag, omega, zero_start):
+        """x = omega d b (zero_start) or x += omega d (b - ax): one damped
+        Jacobi update (the distributed smoother's elementwise half)."""
+        _check(lib().gls_mg_relax(self.h, level, _ptr(x), _ptr(b),
+                                  None if ax is None else _ptr(ax), _ptr(inv_diag),
+                                  float(omega), int(zero_start), _stream()))
 
     def smooth(self, level, x, b, zero_initial_guess=True):
         _check(lib().gls_mg_smooth(self.h, level, _ptr(x), _ptr(b), int(zero_initial_guess),

@@ -64,16 +64,29 @@ def _brick_cells(mesh):
     return n
 
 
-def build_partitions(mesh, world):
-    """Split the cell list into `world` contiguous brick ranges and derive the
-    ownership / ghost / exchange plan for every rank."""
-    nbc = _brick_cells(mesh)
-    if mesh.n_cells % nbc:
-        raise ValueError("cell count is not a multiple of the brick size")
-    nb = mesh.n_cells // nbc
-    if world > nb:
-        raise ValueError(f"{world} ranks for {nb} bricks")
-    bounds = [(r * nb // world) * nbc for r in range(world + 1)]
+def coarse_bounds(n_coarse_cells, world):
+    """Contiguous ranges of coarse (level 0) cells per rank: every level of a
+    hierarchy is partitioned by the same coarse cells (the children of a
+    rank's coarse cells are its fine cells), as p4est's partition of the
+    coarse forest keeps the levels aligned (main.cc:398-400)."""
+    if world > n_coarse_cells:
+        raise ValueError(f"{world} ranks for {n_coarse_cells} coarse cells")
+    return [r * n_coarse_cells // world for r in range(world + 1)]
+
+
+def build_partitions(mesh, world, bounds=None):
+    """Split the cell list into `world` contiguous brick ranges (or the given
+    cell `bounds`) and derive the ownership / ghost / exchange plan for every
+    rank."""
+    if bounds is None:
+        nbc = _brick_cells(mesh)
+        if mesh.n_cells % nbc:
+            raise ValueError("cell count is not a multiple of the brick size")
+        nb = mesh.n_cells // nbc
+        if world > nb:
+            raise ValueError(f"{world} ranks for {nb} bricks")
+        bounds = [(r * nb // world) * nbc for r in range(world + 1)]
+    bounds = [int(b) for b in bounds]
     touched = [np.unique(mesh.cell_nodes[bounds[r]:bounds[r + 1]].ravel())
                for r in range(world)]
     owner = np.full(mesh.n_nodes, world, dtype=np.int64)
@@ -175,6 +188,12 @@ class GpuEngine:
     def identity_rows(self, dst, src):
         self.op.apply_identity_rows(dst, src)
 
+    def diagonal_raw(self, d):
+        self.op.compute_diagonal(d)
+
+    def invert_diagonal(self, d):
+        self.op.invert_diagonal(d)
+
     def partitioned(self, part, nccl_id=None, group=None):
         import glsamd
         peers = sorted(set(part.recv_nodes) | set(part.send_nodes))
@@ -203,6 +222,9 @@ class RankOperator:
         self.dtype, self.device = self.eng.dtype, self.eng.device
         self.n_dofs = part.n_nodes * self.nc
         self.n_owned_dofs = part.n_owned * self.nc
+        cmo = np.asarray(lcmask[:part.n_owned], dtype=np.int64)
+        self.con_owned = torch.from_numpy(
+            (((cmo[:, None] >> np.arange(self.nc)[None, :]) & 1) != 0).ravel()).to(self.device)
         self.global_dofs = torch.from_numpy(_dofs(part.local_nodes, self.nc)).to(self.device)
         dev = lambda a: torch.from_numpy(_dofs(a, self.nc)).to(self.device)  # noqa: E731
         self.recv_idx = {q: dev(v) for q, v in part.recv_nodes.items()}
@@ -263,9 +285,10 @@ class DistributedOperator:
     distributed operator (set_linearization_point, set_previous_solution,
     vmult), on rank-local [owned | ghost] vectors."""
 
-    def __init__(self, mesh, cmask, precision, dist, rank, world, engine="gpu", native=None):
+    def __init__(self, mesh, cmask, precision, dist, rank, world, engine="gpu", native=None,
+                 bounds=None):
         self.dist, self.rank, self.world = dist, rank, world
-        self.parts = build_partitions(mesh, world)
+        self.parts = build_partitions(mesh, world, bounds)
         self.r = RankOperator(mesh, cmask, self.parts[rank], precision, engine)
         self.n_local_cells = self.r.part.n_cells
         self.n_global_dofs = mesh.n_dofs
@@ -305,11 +328,15 @@ class DistributedOperator:
                 w.wait()
 
     def update_ghost_values(self, v):
+        if self.native is not None:
+            return self.native.update_ghost_values(v)
         sends, recvs = self.r.pack_import(v)
         self._exchange(sends, recvs)
         self.r.unpack_import(v)
 
     def compress_add(self, v):
+        if self.native is not None:
+            return self.native.compress_add(v)
         sends, recvs = self.r.pack_export(v)
         self._exchange(sends, recvs)
         self.r.unpack_export(v)
@@ -422,3 +449,313 @@ class LocalGroup:
             n = r.n_owned_dofs
             g.index_copy_(0, r.global_dofs[:n], v[:n])
         return g
+
+
+# ------------------------------------------------------------ multigrid
+def global_first_owners(child):
+    """NOT_OWNER flags (bit 31) of a global child lattice [coarse cell][nl]:
+    the first coarse cell (global order) touching a fine node owns it — the
+    owner-only transfers of csrc/mg.hip, and with ranks holding contiguous
+    coarse-cell ranges the owner cell of every fine node lies on the rank that
+    owns the node (the lowest rank touching it)."""
+    flat = np.asarray(child, dtype=np.int64).ravel()
+    _, first = np.unique(flat, return_index=True)
+    owner = np.zeros(flat.shape, dtype=bool)
+    owner[first] = True
+    return owner.reshape(np.shape(child))
+
+
+class DistributedMultigrid:
+    """PreconditionerGMG (multigrid.h:61-141) over a partitioned level
+    hierarchy, one process per GPU: every level is a DistributedOperator on
+    the same coarse-cell partition (main.cc:398-400), the transfers run the
+    owner-only lattice kernels on the rank-local cells with halo exchanges
+    around them (MGTransferGlobalCoarsening's ghosted level vectors,
+    main.cc:540-563):
+        prolongate: update_ghost_values(coarse), local prolongate_add
+                    (every owned fine node is written by its owner rank);
+        restrict:   local restrict_add (owned fine nodes feed the coarse
+                    nodes of their owner cell), compress(add) on the coarse
+                    vector;
+        interpolate_to_mg: update_ghost_values(fine), local injection.
+    Smoother: PreconditionRelaxation (damped Jacobi, power-iteration omega
+    with deal.II's start vector on the GLOBAL dof index and all-reduced
+    dots, multigrid.cc:281-369); inverse diagonals from the rank-local
+    assembled diagonals after compress(add).  Coarse solve: relaxation
+    sweeps (the substitute for the direct solver) or
+    identity.  engine: "gpu" (libglsamd.so kernels, RCCL exchange) or a test
+    engine (tests/dist_engines.py) with the same interface."""
+
+    def __init__(self, meshes, cmasks, precision, dist, rank, world, engine="gpu",
+                 transfers=None, n_smooth=5, n_eig=20, smoothing_range=20.0,
+                 coarse_n_iterations=10, compute_evs_n_levels=0, native=None):
+        self.dist, self.rank, self.world = dist, rank, world
+        self.n_smooth, self.n_eig, self.range = n_smooth, n_eig, smoothing_range
+        self.coarse_iters, self.evs_levels = coarse_n_iterations, compute_evs_n_levels
+        n0 = meshes[0].n_cells
+        cb = coarse_bounds(n0, world)
+        self.levels = []
+        for m, cm in zip(meshes, cmasks):
+            if m.n_cells % n0:
+                raise ValueError("level meshes must refine the coarse cells uniformly")
+            ratio = m.n_cells // n0
+            self.levels.append(DistributedOperator(m, cm, precision, dist, rank, world,
+                                                   engine=engine, native=native,
+                                                   bounds=[b * ratio for b in cb]))
+        # rank-local child lattices (local fine node ids) with global-first
+        # owner flags
+        self.child = [None]
+        for l in range(1, len(meshes)):
+            G = np.asarray(meshes[l - 1].child_lattice(meshes[l]), dtype=np.int64)
+            own = global_first_owners(G)
+            pc = self.levels[l - 1].r.part
+            pf = self.levels[l].r.part
+            g2l = np.full(meshes[l].n_nodes, -1, dtype=np.int64)
+            g2l[pf.local_nodes] = np.arange(pf.n_nodes)
+            rows = G[pc.cell_begin:pc.cell_end]
+            loc = g2l[rows]
+            if (loc < 0).any():
+                raise ValueError("a child lattice node is not local to the fine partition")
+            ch = loc.astype(np.uint32)
+            ch[~own[pc.cell_begin:pc.cell_end]] |= np.uint32(0x80000000)
+            self.child.append(ch)
+        if transfers is None:
+            import glsamd
+            transfers = glsamd.Multigrid([D.op for D in self.levels], self.child[1:],
+                                         coarse_n_iterations=coarse_n_iterations,
+                                         outer_precision=precision)
+        elif callable(transfers) and not hasattr(transfers, "prolongate_add"):
+            transfers = transfers(self)  # a factory (tests: numpy transfers)
+        self.tr = transfers
+        self.omega = [1.0] * len(self.levels)
+        self.lam = [0.0] * len(self.levels)
+        self.invdiag = [None] * len(self.levels)
+        import torch
+        self._global_dof = []
+        for D in self.levels:
+            gd = torch.from_numpy(_dofs(D.r.part.local_nodes[:D.r.part.n_owned], D.r.nc))
+            self._global_dof.append(gd.to(D.r.device))
+
+    # ---- vectors and reductions
+    def new_vector(self, l):
+        return self.levels[l].new_vector()
+
+    def _owned(self, l, v):
+        return v[:self.levels[l].r.n_owned_dofs]
+
+    def _allreduce(self, t):
+        self.dist.all_reduce(t)
+        return t
+
+    def dot(self, l, a, b):
+        import torch
+        s = torch.dot(self._owned(l, a).double(), self._owned(l, b).double()).reshape(1)
+        return float(self._allreduce(s)[0])
+
+    # ---- setup (PreconditionerGMG::initialize, main.cc:815-839)
+    def interpolate(self, l, dst_coarse, src_fine):
+        """interpolate_to_mg level l -> l-1 on owned + ghost coarse nodes."""
+        self.levels[l].update_ghost_values(src_fine)
+        self.tr.interpolate(l, dst_coarse, src_fine)
+        self.levels[l - 1].update_ghost_values(dst_coarse)
+
+    def set_linearization_point(self, params, u_fine, hist_fine=None, weights=None):
+        """u_fine / hist_fine: finest-level local vectors in the level precision."""
+        L = len(self.levels)
+        us = [None] * L
+        hs = [None] * L
+        us[-1] = u_fine
+        hs[-1] = hist_fine
+        for l in range(L - 1, 0, -1):
+            us[l - 1] = self.new_vector(l - 1)
+            self.interpolate(l, us[l - 1], us[l])
+            if hs[l] is not None:
+                hs[l - 1] = []
+                for h in hs[l]:
+                    t = self.new_vector(l - 1)
+                    self.interpolate(l, t, h)
+                    hs[l - 1].append(t)
+        for l, D in enumerate(self.levels):
+            D.update_ghost_values(us[l])
+            D.r.eng.set_parameters(**params)
+            D.r.eng.set_linearization_point(us[l])
+            if hs[l] is not None and params.get("order", 0) > 0:
+                for h in hs[l]:
+                    D.update_ghost_values(h)
+                D.r.eng.set_previous_solution(hs[l], weights)
+
+    def setup(self):
+        for l, D in enumerate(self.levels):
+            d = D.new_vector()
+            D.r.eng.diagonal_raw(d)
+            D.compress_add(d)
+            D.r.eng.invert_diagonal(d)
+            self.invdiag[l] = d
+            if l == 0 and len(self.levels) > 1 and self.coarse_iters <= 0 and self.evs_levels <= 0:
+                self.lam[l], self.omega[l] = 0.0, 1.0
+                continue
+            ev = 1.2 * self.power_iteration(l)
+            self.lam[l] = ev
+            alpha = ev / self.range if self.range > 1 else 0.9 * ev
+            self.omega[l] = 2.0 / (alpha + ev) if ev > 0 else 1.0
+
+    def power_iteration(self, l):
+        """deal.II power_iteration with set_initial_guess on the global dof
+        index (x_i = i % 11 - mean, constrained 0), dots all-reduced."""
+        import torch
+        D = self.levels[l]
+        n_glob = D.n_global_dofs
+        mean = (n_glob // 11 * 55 + (n_glob % 11) * (n_glob % 11 - 1) // 2) / n_glob
+        x = D.new_vector()
+        xo = (self._global_dof[l] % 11).to(torch.float64) - mean
+        con = D.r.con_owned
+        xo[con] = 0.0
+        x[:D.r.n_owned_dofs] = xo.to(x.dtype)
+        nx = self.dot(l, x, x) ** 0.5
+        x *= 1.0 / nx
+        y = D.new_vector()
+        lam = 0.0
+        d = self.invdiag[l]
+        for _ in range(self.n_eig):
+            D.vmult(y, x)
+            y *= d
+            lam = self.dot(l, x, y)
+            ny = self.dot(l, y, y) ** 0.5
+            x.copy_(y * (1.0 / ny if ny > 0 else 0.0))
+        return abs(lam)
+
+    # ---- V-cycle (Multigrid::level_v_step)
+    def relax(self, l, x, b, ax, zero):
+        relax = getattr(self.tr, "relax", None)
+        if relax is not None:
+            return relax(l, x, b, ax, self.invdiag[l], self.omega[l], zero)
+        w, d = self.omega[l], self.invdiag[l]
+        if zero:
+            x.copy_(w * d * b)
+        else:
+            x.add_(w * d * (b - ax))
+
+    def smooth(self, l, x, b, zero, iters):
+        D = self.levels[l]
+        t = D.new_vector()
+        it = 0
+        if zero and iters > 0:
+            self.relax(l, x, b, None, True)
+            it = 1
+        for _ in range(it, iters):
+            D.vmult(t, x)
+            self.relax(l, x, b, t, False)
+
+    def v_step(self, l, x, b):
+        if l == 0:
+            if self.coarse_iters > 0:
+                self.smooth(0, x, b, True, self.coarse_iters)
+            else:
+                x.copy_(b)
+            return
+        D, Dc = self.levels[l], self.levels[l - 1]
+        self.smooth(l, x, b, True, self.n_smooth)
+        t = D.new_vector()
+        D.vmult(t, x)
+        t.neg_().add_(b)
+        bc = Dc.new_vector()
+        self.tr.restrict_add(l, bc, t)
+        Dc.compress_add(bc)
+        xc = Dc.new_vector()
+        self.v_step(l - 1, xc, bc)
+        Dc.update_ghost_values(xc)
+        self.tr.prolongate_add(l, x, xc)
+        self.smooth(l, x, b, False, self.n_smooth)
+
+    def vmult(self, dst, src):
+        """PreconditionMG::vmult on finest-level local vectors (copy_to_mg /
+        copy_from_mg convert to the level precision)."""
+        L = len(self.levels) - 1
+        D = self.levels[L]
+        b = src.to(D.r.dtype)
+        x = D.new_vector()
+        self.v_step(L, x, b)
+        dst.copy_(x.to(dst.dtype))
+        return dst
+
+
+def gmres_solve(apply_A, apply_P, b, x, n_owned, allreduce, max_n_tmp_vectors=30,
+                max_iterations=10000, relative_tolerance=1e-8, absolute_tolerance=1e-12):
+    """LinearSolverGMRES::solve (solver_l.cc:45-74) on rank-local vectors of a
+    partitioned operator: right-preconditioned restarted GMRES(m = 28) with
+    classical Gram-Schmidt + one re-orthogonalisation, the basis V in HBM,
+    dots over the owned entries all-reduced (MPI_Allreduce in deal.II;
+    RCCL / gloo here).  x = 0 on entry; returns (iterations, residual);
+    raises RuntimeError on no convergence (SolverControl::NoConvergence)."""
+    import torch
+    m = max_n_tmp_vectors - 2
+    n = b.numel()
+    dev, dt = b.device, torch.float64
+
+    def ared(t):
+        allreduce(t)
+        return t
+
+    def nrm(v):
+        return float(ared((v[:n_owned].double() ** 2).sum().reshape(1))[0]) ** 0.5
+
+    bnorm = nrm(b)
+    tol = max(relative_tolerance * bnorm, absolute_tolerance)
+    x.zero_()
+    V = torch.zeros(m + 1, n, dtype=b.dtype, device=dev)
+    z = torch.zeros_like(b)
+    w = torch.zeros_like(b)
+    it, res = 0, bnorm
+    V[0].copy_(b)
+    while res > tol and it < max_iterations:
+        beta = res
+        V[0] *= 1.0 / beta
+        H = np.zeros((m + 1, m))
+        g = np.zeros(m + 1)
+        g[0] = beta
+        cs, sn = np.zeros(m), np.zeros(m)
+        jd = 0
+        for j in range(m):
+            if it >= max_iterations:
+                break
+            apply_P(z, V[j])
+            apply_A(w, z)
+            hj = torch.zeros(j + 1, dtype=dt, device=dev)
+            for _ in range(2):
+                h = ared(V[:j + 1, :n_owned].double() @ w[:n_owned].double())
+                w.sub_((h.to(w.dtype) @ V[:j + 1]))
+                hj += h
+            hn = nrm(w)
+            H[:j + 1, j] = hj.cpu().numpy()
+            H[j + 1, j] = hn
+            if hn > 0:
+                V[j + 1].copy_(w * (1.0 / hn))
+            for i in range(j):
+                tmp = cs[i] * H[i, j] + sn[i] * H[i + 1, j]
+                H[i + 1, j] = -sn[i] * H[i, j] + cs[i] * H[i + 1, j]
+                H[i, j] = tmp
+            rr = np.hypot(H[j, j], H[j + 1, j])
+            cs[j] = H[j, j] / rr if rr > 0 else 1.0
+            sn[j] = H[j + 1, j] / rr if rr > 0 else 0.0
+            H[j, j], H[j + 1, j] = rr, 0.0
+            g[j + 1] = -sn[j] * g[j]
+            g[j] = cs[j] * g[j]
+            it += 1
+            jd += 1
+            res = abs(g[j + 1])
+            if res <= tol or hn == 0:
+                break
+        y = np.zeros(jd)
+        for i in range(jd - 1, -1, -1):
+            y[i] = (g[i] - H[i, i + 1:jd] @ y[i + 1:jd]) / H[i, i]
+        w.copy_(torch.from_numpy(y).to(device=dev, dtype=b.dtype) @ V[:jd])
+        apply_P(z, w)
+        x.add_(z)
+        if res <= tol or it >= max_iterations:
+            break
+        apply_A(V[0], x)
+        V[0].neg_().add_(b)
+        res = nrm(V[0])
+    if res > tol:
+        raise RuntimeError(f"GMRES: no convergence in {it} iterations ({res} > {tol})")
+    return it, res

@@ -195,6 +195,12 @@ glsStatus gls_op_compute_inverse_diagonal(glsOp op, void *inv_diag,
  * (main.cc:913-920).  Partitioned operators: gls_dist_get_max_u adds the
  * MPI max. */
 glsStatus gls_op_get_max_u(glsOp op, const void *vec, double *u_max, void *stream);
+/* the pieces of compute_inverse_diagonal for a partitioned operator: the
+ * rank-local assembled diagonal (constrained owned components 1), then —
+ * after the caller's compress(add) of the ghost partials (gls_dist_compress_
+ * add) — d <- |d| > 1e-10 ? 1/d : 1 (operator_ns.cc:220-224) */
+glsStatus gls_op_compute_diagonal(glsOp op, void *diag, void *stream);
+glsStatus gls_op_invert_diagonal(glsOp op, void *diag, void *stream);
 
 /* canonical host layout [cell][q][field] (fields: delta1, delta2, U(dim),
  * gradU(dim*dim), gradP(dim), Ut_old(dim)) + cellwise [cell][2] */
@@ -254,6 +260,11 @@ glsStatus gls_mg_interpolate(glsMG mg, int level, void *dst_coarse,
 /* PreconditionRelaxation::vmult (zero start) / step on one level */
 glsStatus gls_mg_smooth(glsMG mg, int level, void *x, const void *b,
                         int zero_initial_guess, void *stream);
+/* one damped-Jacobi update on level `level`'s vectors (the host-driven
+ * distributed smoother, glsdist.py): zero_start: x = omega d b, else
+ * x += omega d (b - ax), ax = A x from a partitioned vmult */
+glsStatus gls_mg_relax(glsMG mg, int level, void *x, const void *b, const void *ax,
+                       const void *inv_diag, double omega, int zero_start, void *stream);
 
 /* ---- partitioned operator: one rank per GPU, ghost exchange over RCCL
  * (deal.II update_ghost_values / compress(add) inside
@@ -295,6 +306,10 @@ glsStatus gls_dist_interior_bricks(glsDist d, int64_t *n_interior,
 /* update_ghost_values of a rank-local [owned | ghost] vector (the import
  * half of gls_dist_vmult), RCCL ranks only */
 glsStatus gls_dist_update_ghost_values(glsDist d, void *vec, void *stream);
+/* compress(VectorOperation::add): the ghost block's partial sums added to
+ * their owners (constrained components skipped), ghost block zeroed (the
+ * export half of gls_dist_vmult), RCCL ranks only */
+glsStatus gls_dist_compress_add(glsDist d, void *vec, void *stream);
 /* get_max_u of the partitioned operator (operator_ns.cc:530-568): ghost
  * import, local max (gls_op_get_max_u), RCCL all-reduce max */
 glsStatus gls_dist_get_max_u(glsDist d, void *vec, double *u_max, void *stream);

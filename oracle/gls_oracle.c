@@ -695,6 +695,34 @@ orc_cell_matrix(const orc_op *op, int64_t c, double *mat)
     }
 }
 
+/* the assembled diagonal before the inversion (constrained components: 1 on
+ * the owned range [0, n_owned_nodes), 0 elsewhere): the rank-local half of a
+ * partitioned compute_inverse_diagonal (the caller adds the ghost partials
+ * to their owners, then inverts) */
+void
+orc_compute_diagonal(const orc_op *op, int64_t n_owned_nodes, double *diag)
+{
+  const int     nq = op->nq, nc = op->m.dim + 1, nd = nq * nc;
+  const int64_t n  = op->m.n_nodes * nc;
+  memset(diag, 0, sizeof(double) * (size_t)n);
+  for (int64_t c = 0; c < op->m.n_cells; ++c)
+    for (int j = 0; j < nd; ++j)
+      {
+        const uint32_t node = op->m.cell_nodes[c * nq + j / nc];
+        const int      comp = j % nc;
+        if ((op->m.cmask[node] >> comp) & 1)
+          continue;
+        double uloc[4][MAXNQ] = {{0}}, out[4][MAXNQ];
+        uloc[comp][j / nc]    = 1.0;
+        cell_apply(op, c, (const double(*)[MAXNQ])uloc, out, 0);
+        diag[(size_t)node * nc + comp] += out[comp][j / nc];
+      }
+  for (int64_t node = 0; node < n_owned_nodes; ++node)
+    for (int comp = 0; comp < nc; ++comp)
+      if ((op->m.cmask[node] >> comp) & 1)
+        diag[node * nc + comp] = 1.0;
+}
+
 void
 orc_compute_inverse_diagonal(const orc_op *op, double *diag)
 {

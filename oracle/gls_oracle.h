@@ -78,6 +78,7 @@ void orc_vmult(const orc_op *op, double *dst, const double *src);
 void orc_evaluate_residual(const orc_op *op, double *dst, const double *src);
 /* operator_ns.cc:195-225 */
 void orc_compute_inverse_diagonal(const orc_op *op, double *inv_diag);
+void orc_compute_diagonal(const orc_op *op, int64_t n_owned_nodes, double *diag);
 /* get_max_u, operator_ns.cc:530-568 */
 double orc_get_max_u(const orc_op *op, const double *vec);
 /* element matrix of one cell, column j = cell operator applied to unit

@@ -46,6 +46,7 @@ def lib():
         L.orc_vmult.argtypes = [vp, vp, vp]
         L.orc_evaluate_residual.argtypes = [vp, vp, vp]
         L.orc_compute_inverse_diagonal.argtypes = [vp, vp]
+        L.orc_compute_diagonal.argtypes = [vp, C.c_int64, vp]
         L.orc_get_max_u.argtypes = [vp, vp]
         L.orc_get_max_u.restype = C.c_double
         L.orc_cell_matrix.argtypes = [vp, C.c_int64, vp]
@@ -135,6 +136,13 @@ class Oracle:
     def get_max_u(self, vec):
         vec = np.ascontiguousarray(vec, dtype=np.float64)
         return float(lib().orc_get_max_u(self.h, _p(vec)))
+
+    def diagonal(self, n_owned_nodes=None):
+        """Assembled diagonal before inversion (partitioned operators)."""
+        d = np.empty(self.m.n_dofs)
+        lib().orc_compute_diagonal(self.h, self.m.n_nodes if n_owned_nodes is None
+                                   else int(n_owned_nodes), _p(d))
+        return d
 
     def inverse_diagonal(self):
         d = np.empty(self.m.n_dofs)

@@ -1,0 +1,195 @@
+"""Multi-GPU on the preconditioner side: the
+partitioned multigrid (per-level partitions on the same coarse cells,
+main.cc:398-400; halo exchanges around the transfers, main.cc:540-563) and
+GMRES with all-reduced dots (solver_l.cc:45-74), glsdist.DistributedMultigrid
+/ gmres_solve, against the single-domain restatement on the same inputs.
+
+CPU: world_size-2 gloo process group, the oracle as every rank's local
+operator (tests/dist_engines.py); FP64 throughout, so the partitioned V-cycle
+and GMRES solution agree with the single-domain ones to 1e-10 (summation
+order only).  GPU: the product path (libglsamd.so kernels, RCCL exchange) at
+world 1 against the single-domain GPU multigrid."""
+import os
+
+import numpy as np
+import pytest
+
+import glsdist
+from helpers import deck, rel_err
+
+CASE = ("input_hoffmann_3D_Re3900.json", 1)
+# a short solve (GMRES(28), a few dozen iterations) keeps the CPU test brief
+GMRES_TOL = 1e-3
+GMRES_M = 30
+
+
+def _hierarchy(name, n_ref):
+    import glsinputs as gi
+    d = deck(name)
+    meshes = [d.mesh(r) for r in range(n_ref + 1)]
+    vel, p, slip = d.boundary_descriptor()
+    cm = [m.constraint_mask(vel, p, slip) for m in meshes]
+    params, w = d.operator_parameters(2.5e-4)
+    u = gi.linearization_point(meshes[-1].n_nodes, meshes[-1].dim, d.u_max)
+    hist = gi.history(u, params["order"])
+    b = gi.rnd(11, meshes[-1].n_dofs)
+    return meshes, cm, params, w, u, hist, b
+
+
+def _single_domain(name, n_ref, coarse):
+    """OracleGMG V-cycle and GMRES(OracleGMG) with the oracle operator."""
+    import torch
+    import oracle as orc
+    from mg_ref import OracleGMG
+    meshes, cm, params, w, u, hist, b = _hierarchy(name, n_ref)
+    ref = OracleGMG(meshes, cm, params, u, hist, w, coarse_iters=coarse)
+    ref.setup_omega()
+    o = orc.Oracle(orc.OracleMesh(meshes[-1], cm[-1]), **params)
+    o.set_linearization_point(u)
+    o.set_previous_solution(hist, w)
+    vc = ref.vcycle(b)
+    if coarse == 0:
+        return ref.omega, vc, None, 0
+    x = torch.zeros(len(b), dtype=torch.float64)
+    bt = torch.from_numpy(b)
+    it, res = glsdist.gmres_solve(
+        lambda dst, src: dst.copy_(torch.from_numpy(o.vmult(src.numpy()))),
+        lambda dst, src: dst.copy_(torch.from_numpy(ref.vcycle(src.numpy()))),
+        bt, x, len(b), lambda t: t, relative_tolerance=GMRES_TOL,
+        max_n_tmp_vectors=GMRES_M)
+    return ref.omega, vc, x.numpy(), it
+
+
+def _worker(rank, world, port, name, n_ref, coarse, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "dealii-ns-gls_amd", "python"), os.path.join(root, "oracle"),
+              os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    import glsdist as gd
+    from dist_engines import OracleEngine, OracleTransfers
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        meshes, cm, params, w, u, hist, b = _hierarchy(name, n_ref)
+        dmg = gd.DistributedMultigrid(meshes, cm, "f64", dist, rank, world, engine=OracleEngine,
+                                      transfers=lambda m: OracleTransfers(m, meshes),
+                                      coarse_n_iterations=coarse)
+        top = dmg.levels[-1]
+        dmg.set_linearization_point(params, top.scatter_global(u),
+                                    [top.scatter_global(h) for h in hist], w)
+        dmg.setup()
+        bl = top.scatter_global(b)
+        xl = top.new_vector()
+        dmg.vmult(xl, bl)
+        vc = top.gather_global(xl).numpy()
+        if coarse == 0:  # V-cycle only
+            if rank == 0:
+                q.put((list(dmg.omega), vc, None, 0))
+            return
+        # the fine FP64 operator on the finest level's partition
+        A = gd.DistributedOperator(meshes[-1], cm[-1], "f64", dist, rank, world,
+                                   engine=OracleEngine,
+                                   bounds=[bb * (meshes[-1].n_cells // meshes[0].n_cells)
+                                           for bb in gd.coarse_bounds(meshes[0].n_cells, world)])
+        A.setup(params, u, hist, w)
+        x = A.new_vector()
+        it, res = gd.gmres_solve(lambda dst, src: A.vmult(dst, src),
+                                 lambda dst, src: dmg.vmult(dst, src),
+                                 A.scatter_global(b), x, A.r.n_owned_dofs,
+                                 lambda t: dist.all_reduce(t), relative_tolerance=GMRES_TOL,
+        max_n_tmp_vectors=GMRES_M)
+        xs = A.gather_global(x).numpy()
+        if rank == 0:
+            q.put((list(dmg.omega), vc, xs, it))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("coarse", [10, 0])
+def test_gloo_world2_vcycle_gmres(coarse):
+    import socket
+    import torch.multiprocessing as mp
+    name, n_ref = CASE
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, n_ref, coarse, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    omega, vc, xs, it = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    omega_ref, vc_ref, xs_ref, it_ref = _single_domain(name, n_ref, coarse)
+    for l, (a, r) in enumerate(zip(omega, omega_ref)):
+        if l == 0 and coarse <= 0:
+            continue
+        assert abs(a - r) < 1e-10 * r, (l, a, r)
+    assert rel_err(vc, vc_ref) < 1e-10
+    if xs is not None:
+        assert abs(it - it_ref) <= 1
+        assert rel_err(xs, xs_ref) < 1e-7
+
+
+@pytest.mark.gpu
+def test_rccl_world1_multigrid_gmres():
+    """The product path of the partitioned multigrid at world 1 (RCCL
+    communicator, libglsamd.so transfers / diagonals / relaxation kernels)
+    against the single-domain GPU multigrid and GMRES."""
+    import torch
+    import torch.distributed as dist
+    import glsamd
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        name, n_ref = CASE
+        meshes, cm, params, w, u, hist, b = _hierarchy(name, n_ref)
+        dmg = glsdist.DistributedMultigrid(meshes, cm, "f32", dist, 0, 1, coarse_n_iterations=10)
+        top = dmg.levels[-1]
+        dmg.set_linearization_point(params, top.scatter_global(u),
+                                    [top.scatter_global(h) for h in hist], w)
+        dmg.setup()
+        mg, ops = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f32",
+                                   coarse_n_iterations=10)
+        for l in range(len(meshes)):
+            wd, lam = mg.relaxation(l)
+            assert abs(dmg.omega[l] - wd) < 1e-4 * wd, (l, dmg.omega[l], wd)
+        bd = torch.from_numpy(b).cuda()
+        x1 = torch.zeros_like(bd)
+        dmg.vmult(x1, top.scatter_global(b).double())
+        x2 = torch.zeros_like(bd)
+        mg.vcycle(x2, bd)
+        torch.cuda.synchronize()
+        g1 = top.gather_global(x1).cpu().numpy()
+        assert rel_err(g1, x2.cpu().numpy()) < 1e-3  # FP32 levels, different omega rounding
+        A = glsdist.DistributedOperator(meshes[-1], cm[-1], "f64", dist, 0, 1)
+        A.setup(params, u, hist, w)
+        x = A.new_vector()
+        it, res = glsdist.gmres_solve(lambda dst, src: A.vmult(dst, src),
+                                      lambda dst, src: dmg.vmult(dst, src),
+                                      A.scatter_global(b), x, A.r.n_owned_dofs,
+                                      lambda t: dist.all_reduce(t), relative_tolerance=1e-6)
+        Ad = glsamd.NavierStokesOperator(meshes[-1], cm[-1], "f64")
+        Ad.set_parameters(**params)
+        Ad.set_linearization_point(u)
+        Ad.set_previous_solution(hist, w)
+        lin = glsamd.LinearSolverGMRES(Ad, mg, relative_tolerance=1e-6)
+        xd = Ad.initialize_dof_vector()
+        lin.solve(xd, bd)
+        torch.cuda.synchronize()
+        assert abs(it - lin.last["n_iterations"]) <= 2, (it, lin.last)
+        assert rel_err(A.gather_global(x).cpu().numpy(), xd.cpu().numpy()) < 1e-4
+    finally:
+        dist.destroy_process_group()
