@@ -253,6 +253,68 @@ def mg_companions(d, params, weights, n_ref, reps=20):
                                                   "Hessenberg step, wall clock"}}
 
 
+def dist_gmres_companion(d, params, weights, n_ref, dist, rank, world, reps=10):
+    """The whole GMRES iteration on N GPUs: the partitioned
+    multigrid (glsdist.DistributedMultigrid: FP32 levels on the same
+    coarse-cell partition, halo exchanges around the transfers, all-reduced
+    power-iteration dots; coarse solve 10 relaxation sweeps) preconditioning
+    right GMRES on the FP64 distributed operator with all-reduced CGS2 dots.
+    Wall times, barrier-bracketed, max over ranks: setup, one V-cycle, one
+    GMRES iteration (28 iterations = one restart cycle, tolerance 0)."""
+    import torch
+    import glsdist
+    meshes = [d.mesh(r) for r in range(n_ref + 1)]
+    vel, p, slip = d.boundary_descriptor()
+    cm = [m.constraint_mask(vel, p, slip) for m in meshes]
+    u = gi.linearization_point(meshes[-1].n_nodes, meshes[-1].dim, d.u_max)
+    hist = gi.history(u, params["order"])
+    dmg = glsdist.DistributedMultigrid(meshes, cm, "f32", dist, rank, world,
+                                       coarse_n_iterations=10)
+    top = dmg.levels[-1]
+    dmg.set_linearization_point(params, top.scatter_global(u),
+                                [top.scatter_global(h) for h in hist], weights)
+    A = dmg.fine_operator("f64")
+    A.setup(params, u, hist, weights)
+    b = A.scatter_global(gi.src_vector(meshes[-1].n_dofs))
+    x = A.new_vector()
+
+    def wall(fn, n):
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    dmg.setup()
+    t_setup = wall(dmg.setup, 3)
+    dmg.vmult(x, b)
+    t_vc = wall(lambda: dmg.vmult(x, b), reps)
+
+    def gmres():
+        try:
+            glsdist.gmres_solve(lambda dst, src: A.vmult(dst, src),
+                                lambda dst, src: dmg.vmult(dst, src), b, x,
+                                A.r.n_owned_dofs, lambda t: dist.all_reduce(t),
+                                max_iterations=28, relative_tolerance=0.0,
+                                absolute_tolerance=0.0)
+        except RuntimeError:
+            pass  # tolerance 0: exactly 28 iterations
+
+    its = 2 * 28
+    t_gm = wall(gmres, 2)
+    return {f"r{n_ref}_dist_mg_setup_f32": {"ms": t_setup / 3 * 1e3, "levels": n_ref + 1},
+            f"r{n_ref}_dist_vcycle_f32_coarse_relax10": {"ms": t_vc / reps * 1e3},
+            f"r{n_ref}_dist_gmres_iteration": {
+                "ms": t_gm / its * 1e3, "n_gpus": world,
+                "note": "glsdist.DistributedMultigrid V-cycle + FP64 distributed vmult + "
+                        "all-reduced CGS2, host-driven, wall clock max over ranks"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -268,10 +330,18 @@ def main():
                     help="cells per brick 'bx,by,bz' (a sub-brick of the mesh order)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle check of the headline result (profiling runs)")
+    ap.add_argument("--gmres-iteration", action="store_true",
+                    help="multi-GPU (or GLS_BENCH_DIST=1): also time the partitioned "
+                         "multigrid + GMRES iteration (reported beside the headline)")
     ap.add_argument("--allow-p2p-fallback", action="store_true",
                     help="multi-GPU: on a native/P2P mismatch time the torch P2P path "
                          "instead of failing")
     args = ap.parse_args()
+    # stdout carries exactly one JSON line: everything else the process or
+    # its libraries write to fd 1 (RCCL's version banner, ...) goes to stderr
+    out_fd = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -284,6 +354,13 @@ def main():
     use_dist = world > 1 or os.environ.get("GLS_BENCH_DIST") == "1"
     if use_dist:
         import torch.distributed as dist
+        if "RANK" not in os.environ:  # GLS_BENCH_DIST=1 without a launcher
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(port))
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     import glsamd
@@ -326,7 +403,8 @@ def main():
             if not args.allow_p2p_fallback:
                 if rank == 0:
                     print(json.dumps({"error": "native RCCL partitioned vmult disagrees with "
-                                               "the torch P2P path", "rel_l2": rel}), flush=True)
+                                               "the torch P2P path", "rel_l2": rel}),
+                          file=out_fd, flush=True)
                 dist.barrier()
                 dist.destroy_process_group()
                 sys.exit(4)
@@ -394,6 +472,10 @@ def main():
         torch.cuda.synchronize()
         kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
 
+    dist_comp = None
+    if use_dist and args.gmres_iteration:
+        dist_comp = dist_gmres_companion(d, params, weights, n_ref, dist, rank, world)
+        log(f"[bench] distributed GMRES iteration: {dist_comp}")
     bytes_per_vmult = op.vmult_bytes()
     n_gen, n_cart = op.geometry_counts()
     # parity of the timed result: the headline dst (FP64) against the oracle
@@ -482,9 +564,9 @@ def main():
                          "kernel_ms": kernel_ms, "algorithmic_bytes": bytes_per_vmult},
             "cpu_baseline": cpu,
             "parity": parity,
-            "companions": comp,
+            "companions": comp if dist_comp is None else dict(comp or {}, **dist_comp),
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=out_fd, flush=True)
     ok = parity is None or parity["ok"]
     if dist is not None:
         t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device="cuda")

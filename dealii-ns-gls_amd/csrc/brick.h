@@ -281,6 +281,25 @@ field_read(int f)
          (MODE == MODE_RESIDUAL && ut);
 }
 
+// a 16-byte group whose only Newton fields are U_t (read when the time
+// derivative is considered): loaded only when the runtime flag td says so
+template <int dim, int MODE>
+__host__ __device__ constexpr bool
+group_ut_only(int g, int W)
+{
+  using F  = Fields<dim>;
+  bool any = false, other = false;
+  for (int w = 0; w < W; ++w)
+    {
+      const int f = g * W + w;
+      if (!field_read<dim, MODE>(f))
+        continue;
+      any = true;
+      other = other || !(f >= F::UT && f < F::UT + dim);
+    }
+  return MODE == MODE_NEWTON && any && !other;
+}
+
 // everything one lane needs from HBM for one (cell, q point)
 template <int dim, typename T, int MODE>
 struct LaneData
@@ -357,8 +376,9 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
     }
   // per-q tables (operator_ns.h:120-132): the round's CPW cells form one
   // chunk, each 16-byte field group of it one contiguous wave load; the
-  // groups a mode reads are fixed at compile time (fields a runtime flag
-  // switches off are loaded and ignored)
+  // groups a mode reads are fixed at compile time, except that a group of
+  // U_t values only is skipped (uniform branch) without the time derivative
+  // (other fields a runtime flag switches off are loaded and ignored)
   constexpr int GS = CPW * nq; // group stride in packs
   const V *tv = a.tab_v + (chunk0 + lcell / CPW) * (NG * GS) + (lcell % CPW) * nq + p;
   T        tf[NG * W];
@@ -370,7 +390,7 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
       for (int w = 0; w < W; ++w)
         any = any || field_read<dim, MODE>(g * W + w);
       V v = {};
-      if (any)
+      if (any && (!group_ut_only<dim, MODE>(g, W) || a.td))
         v = tv[g * GS];
 #pragma unroll
       for (int w = 0; w < W; ++w)

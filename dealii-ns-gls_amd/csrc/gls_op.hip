@@ -2005,10 +2005,11 @@ gls_op_vmult_bytes(glsOp op)
     return 0;
   // B = s 2N + s C nq n_tab + s [n_gen nq (dim^2+1) +
   //                 n_cart (dim+1)] + 4 C nq,
-  // with n_tab the table values per q this build streams: the brick kernel's
-  // Newton vmult reads U, grad U, T1 and h (16 in 3D; delta_1/2 recomputed,
-  // kernels.h Fields), in whole 16-byte groups; the per-cell path the
-  // reference's 20 (operator_ns.h:120-132)
+  // with n_tab the table values per q this build streams, in whole 16-byte
+  // groups (brick.h field_read): the reference's 20 in 3D (operator_ns.h:
+  // 120-132) with the time derivative, the U_t-only group skipped without it
+  // (18 in FP64); 16 with GLS_NEWTON_T1; the per-cell path the reference's
+  // set
   const double s   = (double)op->tsize();
   const int    dim = op->dim;
   const bool   td  = (op->prm.flags & GLS_CONSIDER_TIME_DERIVATIVE) && op->prm.order > 0;
@@ -2027,7 +2028,9 @@ gls_op_vmult_bytes(glsOp op)
               any = any || (dim == 3 ? (nt ? field_read<3, MODE_NEWTON>(f) : field_read<3, MODE_FIXED>(f))
                                      : (nt ? field_read<2, MODE_NEWTON>(f) : field_read<2, MODE_FIXED>(f)));
             }
-          n_tab += any ? W : 0;
+          const bool ut_only = nt && (dim == 3 ? group_ut_only<3, MODE_NEWTON>(g, W)
+                                               : group_ut_only<2, MODE_NEWTON>(g, W));
+          n_tab += any && (!ut_only || td) ? W : 0;
         }
     }
   else if (nt)

@@ -494,6 +494,8 @@ class DistributedMultigrid:
         self.coarse_iters, self.evs_levels = coarse_n_iterations, compute_evs_n_levels
         n0 = meshes[0].n_cells
         cb = coarse_bounds(n0, world)
+        self.fine_bounds = [b * (meshes[-1].n_cells // n0) for b in cb]
+        self._fine = (meshes[-1], cmasks[-1], engine, native)
         self.levels = []
         for m, cm in zip(meshes, cmasks):
             if m.n_cells % n0:
@@ -535,6 +537,13 @@ class DistributedMultigrid:
         for D in self.levels:
             gd = torch.from_numpy(_dofs(D.r.part.local_nodes[:D.r.part.n_owned], D.r.nc))
             self._global_dof.append(gd.to(D.r.device))
+
+    def fine_operator(self, precision="f64"):
+        """The outer (system) operator on the finest level's partition: its
+        rank-local vectors are the ones vmult() takes (the GMRES operand)."""
+        m, cm, engine, native = self._fine
+        return DistributedOperator(m, cm, precision, self.dist, self.rank, self.world,
+                                   engine=engine, native=native, bounds=self.fine_bounds)
 
     # ---- vectors and reductions
     def new_vector(self, l):

@@ -90,10 +90,7 @@ def _worker(rank, world, port, name, n_ref, coarse, q):
                 q.put((list(dmg.omega), vc, None, 0))
             return
         # the fine FP64 operator on the finest level's partition
-        A = gd.DistributedOperator(meshes[-1], cm[-1], "f64", dist, rank, world,
-                                   engine=OracleEngine,
-                                   bounds=[bb * (meshes[-1].n_cells // meshes[0].n_cells)
-                                           for bb in gd.coarse_bounds(meshes[0].n_cells, world)])
+        A = dmg.fine_operator("f64")
         A.setup(params, u, hist, w)
         x = A.new_vector()
         it, res = gd.gmres_solve(lambda dst, src: A.vmult(dst, src),
@@ -174,7 +171,7 @@ def test_rccl_world1_multigrid_gmres():
         torch.cuda.synchronize()
         g1 = top.gather_global(x1).cpu().numpy()
         assert rel_err(g1, x2.cpu().numpy()) < 1e-3  # FP32 levels, different omega rounding
-        A = glsdist.DistributedOperator(meshes[-1], cm[-1], "f64", dist, 0, 1)
+        A = dmg.fine_operator("f64")
         A.setup(params, u, hist, w)
         x = A.new_vector()
         it, res = glsdist.gmres_solve(lambda dst, src: A.vmult(dst, src),
