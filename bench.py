@@ -170,6 +170,25 @@ def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src,
     out[f"sphere_r{ds.n_refinements}_f64_warm"] = line(ops_, dsts, srcs)
     out[f"sphere_r{ds.n_refinements}_f64_warm"]["cells"] = ms.n_cells
     del ops_, dsts, srcs
+    # a deal.II cell order: the headline mesh with its
+    # cells shuffled and nodes renumbered by first touch, bricks discovered
+    # by gls_op_create (brick = {-1,-1,-1}), beside the per-cell kernel
+    # (brick = {0,0,0}) on the same shuffled mesh; parity checked in
+    # tests/test_brick_discovery.py
+    sm = gm.ShuffledMesh(mesh, seed=1)
+    smask = sm.constraint_mask(vel, p, slip)
+    for tag, brick in (("auto_bricks", None), ("per_cell", (0, 0, 0))):
+        u_s = gi.linearization_point(sm.n_nodes, sm.dim, d.u_max)
+        op_s = glsamd.NavierStokesOperator(sm, smask, "f64", brick=brick)
+        op_s.set_parameters(**params)
+        op_s.set_linearization_point(u_s)
+        if params["order"] > 0:
+            op_s.set_previous_solution(gi.history(u_s, params["order"]), weights)
+        src_s = op_s._dev(gi.src_vector(sm.n_dofs))
+        key = f"r{n_ref}_f64_shuffled_{tag}"
+        out[key] = line(op_s, op_s.initialize_dof_vector(), src_s)
+        out[key]["brick_shape"] = list(op_s.brick_shape)
+        del op_s, src_s
     out.update(mg_companions(d, params, weights, n_ref))
     del scratch
     torch.cuda.empty_cache()

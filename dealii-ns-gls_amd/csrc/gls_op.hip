@@ -1214,7 +1214,49 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
     throw std::runtime_error("gls_op_create: invalid descriptor");
   if (d->n_nodes >= (int64_t)NODE_MASK)
     throw std::runtime_error("gls_op_create: too many local nodes for 28-bit node indices");
+  // an arbitrary cell order (brick[0] < 0, e.g. deal.II's MatrixFree cell
+  // order): discover the bricks from the connectivity and run the cells in
+  // brick order (brick_discovery.cc); every cell-indexed input is permuted
+  // here, vectors are node-indexed and unaffected
+  const glsOpDesc      *caller = d;
+  glsOpDesc             dd     = *d;
+  gls::BrickPlan        plan;
+  std::vector<uint32_t> p_nodes;
+  std::vector<double>   p_meas, p_hmin;
+  if (d->brick[0] < 0)
+    {
+      dd.brick[0] = dd.brick[1] = dd.brick[2] = 0;
+      for (int64_t i = 0; i < d->n_cells * (int64_t)(d->dim == 3 ? (d->degree + 1) * (d->degree + 1) * (d->degree + 1)
+                                                                   : (d->degree + 1) * (d->degree + 1));
+           ++i)
+        if ((int64_t)d->cell_nodes[i] >= d->n_nodes)
+          throw std::runtime_error("gls_op_create: node index out of range");
+      if (gls::discover_bricks(d->dim, d->degree, d->n_cells, d->cell_nodes, plan))
+        {
+          const int nqc = d->dim == 3 ? (d->degree + 1) * (d->degree + 1) * (d->degree + 1)
+                                      : (d->degree + 1) * (d->degree + 1);
+          p_nodes.resize((size_t)d->n_cells * nqc);
+          p_meas.resize((size_t)d->n_cells);
+          p_hmin.resize((size_t)d->n_cells);
+          for (int64_t c = 0; c < d->n_cells; ++c)
+            {
+              const int64_t e = plan.perm[(size_t)c];
+              std::copy(d->cell_nodes + e * nqc, d->cell_nodes + (e + 1) * nqc,
+                        p_nodes.begin() + c * nqc);
+              p_meas[c] = d->cell_measure[e];
+              p_hmin[c] = d->cell_hmin[e];
+            }
+          dd.cell_nodes   = p_nodes.data();
+          dd.cell_measure = p_meas.data();
+          dd.cell_hmin    = p_hmin.data();
+          for (int a = 0; a < 3; ++a)
+            dd.brick[a] = plan.shape[a];
+        }
+    }
+  d = &dd;
   auto *op          = new glsOp_();
+  if (!p_nodes.empty())
+    op->cell_perm = std::move(plan.perm);
   op->dim           = d->dim;
   op->degree        = d->degree;
   op->prec          = d->precision;
@@ -1243,7 +1285,7 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
     }
   upload((void **)&op->d_nodes, nodes);
   op->h_cmask.assign(d->node_cmask, d->node_cmask + d->n_nodes);
-  op->h_cell_nodes.assign(d->cell_nodes, d->cell_nodes + (size_t)d->n_cells * nq);
+  op->h_cell_nodes.assign(caller->cell_nodes, caller->cell_nodes + (size_t)d->n_cells * nq);
 
   // constrained dof bitmask on the owned range (identity rows)
   std::vector<uint32_t> cbits((size_t)(op->n_owned_dofs + 31) / 32 + 1, 0u);
@@ -1900,13 +1942,13 @@ gls_op_upload_tables(glsOp op, const double *tables, const double *cellwise)
     for (int q = 0; q < op->nq; ++q)
       for (int f = 0; f < op->nf; ++f)
         soa[host_tab_index(op, c, q, storage_field(op, f))] =
-          tables[((size_t)c * op->nq + q) * op->nf + f];
+          tables[((size_t)ext_cell(op, c) * op->nq + q) * op->nf + f];
   std::vector<double> cw((size_t)2 * op->n_cells, 0.0);
   if (cellwise)
     for (int64_t c = 0; c < op->n_cells; ++c)
       {
-        cw[c]               = cellwise[2 * c];
-        cw[op->n_cells + c] = cellwise[2 * c + 1];
+        cw[c]               = cellwise[2 * ext_cell(op, c)];
+        cw[op->n_cells + c] = cellwise[2 * ext_cell(op, c) + 1];
       }
   if (op->prec == GLS_F64)
     {
@@ -1974,14 +2016,60 @@ gls_op_download_tables(glsOp op, double *tables, double *cellwise)
     for (int64_t c = 0; c < op->n_cells; ++c)
       for (int q = 0; q < op->nq; ++q)
         for (int f = 0; f < op->nf; ++f)
-          tables[((size_t)c * op->nq + q) * op->nf + f] =
+          tables[((size_t)ext_cell(op, c) * op->nq + q) * op->nf + f] =
             soa[host_tab_index(op, c, q, storage_field(op, f))];
   if (cellwise)
     for (int64_t c = 0; c < op->n_cells; ++c)
       {
-        cellwise[2 * c]     = cw[c];
-        cellwise[2 * c + 1] = cw[op->n_cells + c];
+        cellwise[2 * ext_cell(op, c)]     = cw[c];
+        cellwise[2 * ext_cell(op, c) + 1] = cw[op->n_cells + c];
       }
+  GLS_CATCH
+}
+
+glsStatus
+gls_discover_bricks(int dim, int degree, int64_t n_cells, const uint32_t *cell_nodes,
+                    int *shape, int64_t *perm)
+{
+  GLS_TRY
+  if (!cell_nodes || !shape || !perm || (dim != 2 && dim != 3) || degree < 1 || n_cells < 0)
+    throw std::runtime_error("gls_discover_bricks: invalid argument");
+  gls::BrickPlan plan;
+  if (!gls::discover_bricks(dim, degree, n_cells, cell_nodes, plan))
+    {
+      shape[0] = shape[1] = shape[2] = 0;
+      for (int64_t c = 0; c < n_cells; ++c)
+        perm[c] = c;
+    }
+  else
+    {
+      for (int a = 0; a < 3; ++a)
+        shape[a] = plan.shape[a];
+      std::copy(plan.perm.begin(), plan.perm.end(), perm);
+    }
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_brick_shape(glsOp op, int *dims)
+{
+  GLS_TRY
+  if (!op || !dims)
+    throw std::runtime_error("gls_op_brick_shape: null argument");
+  dims[0] = op->use_brick ? op->bx : 0;
+  dims[1] = op->use_brick ? op->by : 0;
+  dims[2] = op->use_brick ? op->bz : 0;
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_cell_permutation(glsOp op, int64_t *perm)
+{
+  GLS_TRY
+  if (!op || !perm)
+    throw std::runtime_error("gls_op_cell_permutation: null argument");
+  for (int64_t c = 0; c < op->n_cells; ++c)
+    perm[c] = ext_cell(op, c);
   GLS_CATCH
 }
 

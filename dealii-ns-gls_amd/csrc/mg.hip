@@ -927,6 +927,16 @@ gls_mg_create(const glsMGDesc *desc, const glsOp *levels, const uint32_t *const 
             fn |= NOT_OWNER;
           seen[fn & ~NOT_OWNER] = 1;
         }
+      // the transfer kernels walk the coarse operator's cells in its own
+      // (possibly brick-discovered) order: rows follow it
+      if (!cop->cell_perm.empty())
+        {
+          std::vector<uint32_t> pc(ch.size());
+          for (int64_t c = 0; c < cop->n_cells; ++c)
+            std::copy(ch.begin() + gls::ext_cell(cop, c) * nl,
+                      ch.begin() + (gls::ext_cell(cop, c) + 1) * nl, pc.begin() + c * nl);
+          ch.swap(pc);
+        }
       std::vector<double> w((size_t)fop->n_dofs, 0.0);
       for (int64_t nd = 0; nd < fop->n_nodes; ++nd)
         for (int c = 0; c < mg->nc; ++c)

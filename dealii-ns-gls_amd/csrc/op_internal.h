@@ -65,7 +65,10 @@ struct glsOp_
 
   // host copies the multigrid transfer setup needs
   std::vector<uint8_t>  h_cmask;      // [n_nodes]
-  std::vector<uint32_t> h_cell_nodes; // [n_cells][nq]
+  std::vector<uint32_t> h_cell_nodes; // [n_cells][nq], caller cell order
+  // discovered bricks (glsOpDesc::brick[0] < 0): the operator runs its cells
+  // in brick order, cell_perm[internal cell] = caller cell (empty: identity)
+  std::vector<int64_t>  cell_perm;
 
   int64_t n_gen = 0, n_cart = 0;
   // device buffers
@@ -122,6 +125,22 @@ struct glsOp_
 
 namespace gls
 {
+// brick discovery for an arbitrary cell order (brick_discovery.cc)
+struct BrickPlan
+{
+  int                  shape[3] = {0, 0, 0};
+  std::vector<int64_t> perm; // internal (brick-ordered) cell -> caller cell
+};
+bool discover_bricks(int dim, int degree, int64_t n_cells, const uint32_t *cell_nodes,
+                     BrickPlan &plan);
+
+// caller cell of internal cell c
+inline int64_t
+ext_cell(const glsOp_ *op, int64_t c)
+{
+  return op->cell_perm.empty() ? c : op->cell_perm[(size_t)c];
+}
+
 // fused damped-Jacobi step of the multigrid smoother (csrc/mg.hip): with it a
 // brick vmult writes x + omega * d . (b - A x) instead of A x.  Passed per
 // launch, never stored on the handle (a concurrent plain vmult on the same

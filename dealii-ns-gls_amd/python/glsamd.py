@@ -35,7 +35,8 @@ EXPORTS = [
     "gls_dist_vmult_group", "gls_dist_interior_bricks", "gls_op_set_vector_layout",
     "gls_op_get_max_u", "gls_mg_set_vector_layout", "gls_dist_update_ghost_values",
     "gls_dist_get_max_u", "gls_op_compute_diagonal", "gls_op_invert_diagonal", "gls_mg_relax",
-    "gls_dist_compress_add",
+    "gls_dist_compress_add", "gls_op_brick_shape", "gls_op_cell_permutation",
+    "gls_discover_bricks",
 ]
 
 GLS_MEM_DEVICE, GLS_MEM_HOST = 0, 1
@@ -140,6 +141,9 @@ def lib():
         L.gls_op_invert_diagonal.argtypes = [vp, vp, vp]
         L.gls_mg_relax.argtypes = [vp, C.c_int, vp, vp, vp, vp, C.c_double, C.c_int, vp]
         L.gls_dist_compress_add.argtypes = [vp, vp, vp]
+        L.gls_op_brick_shape.argtypes = [vp, vp]
+        L.gls_op_cell_permutation.argtypes = [vp, vp]
+        L.gls_discover_bricks.argtypes = [C.c_int, C.c_int, i64, vp, vp, vp]
         L.gls_last_error.restype = C.c_char_p
         _lib = L
     return _lib
@@ -171,6 +175,21 @@ def _vptr(v):
     return _ptr(v)
 
 
+def discover_bricks(mesh_or_cells, dim=None, degree=None):
+    """gls_discover_bricks: (shape, perm) for a cell list in any order (host
+    only).  Accepts a mesh (cell_nodes, dim, degree) or a cell_nodes array."""
+    if dim is None:
+        cn, dim, degree = mesh_or_cells.cell_nodes, mesh_or_cells.dim, mesh_or_cells.degree
+    else:
+        cn = mesh_or_cells
+    cn = np.ascontiguousarray(cn, dtype=np.uint32)
+    shape = (C.c_int * 3)()
+    perm = np.empty(cn.shape[0], dtype=np.int64)
+    _check(lib().gls_discover_bricks(int(dim), int(degree), cn.shape[0], cn.ctypes.data, shape,
+                                     perm.ctypes.data))
+    return tuple(shape), perm
+
+
 class NavierStokesOperator:
     """Mirror of NavierStokesOperator<dim, Number> (operator_ns.h:17-189) over
     the HIP C-ABI.  precision: "f64" (fine level, Number=double) or "f32"
@@ -198,6 +217,8 @@ class NavierStokesOperator:
         self.n_cells = k[0].shape[0]
         if brick is None:
             brick = mesh.brick() if cells is None else (0, 0, 0)
+        elif brick == "auto":  # any cell order: bricks discovered by the library
+            brick = (-1, -1, -1)
         self.brick = tuple(brick)
         d = OpDesc(self.dim, self.degree, self.prec, self.n_cells, mesh.n_nodes,
                    mesh.n_nodes if n_owned_nodes is None else n_owned_nodes,
@@ -207,6 +228,16 @@ class NavierStokesOperator:
         _check(lib().gls_op_create(C.byref(d), C.byref(h)))
         self.h = h
         self.n_dofs = lib().gls_op_m(h)
+        dims = (C.c_int * 3)()
+        _check(lib().gls_op_brick_shape(h, dims))
+        self.brick_shape = tuple(dims)  # what runs: (0, 0, 0) = per-cell kernel
+
+    def cell_permutation(self):
+        """perm[internal cell] = caller cell (identity unless bricks were
+        discovered)."""
+        p = np.empty(self.n_cells, dtype=np.int64)
+        _check(lib().gls_op_cell_permutation(self.h, p.ctypes.data))
+        return p
 
     def __del__(self):
         try:

@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes as C
 import json
 import os
+import itertools
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -408,3 +409,83 @@ def read_deck(path):
     d.u_max = float(raw.get("simulation u max", 1.0))
     d.t_init = float(raw.get("simulation t init", 0.0))
     return d
+
+
+# ------------------------------------------------------------ arbitrary order
+def _rotations(dim):
+    """Proper rotations of the reference cell: (axis permutation, flips)."""
+    out = []
+    for perm in itertools.permutations(range(dim)):
+        sign = np.linalg.det(np.eye(dim)[list(perm)])
+        for flips in itertools.product((1, -1), repeat=dim):
+            if sign * np.prod(flips) > 0:
+                out.append((perm, flips))
+    return out
+
+
+class ShuffledMesh:
+    """A generated mesh in an arbitrary cell order, the way a deal.II
+    DoFHandler / MatrixFree hands it over (operator_ns.cc:806-830 loops over
+    MatrixFree's cell batches, whatever their order): cells shuffled, nodes
+    renumbered by first touch in the new cell order (DoFHandler's
+    enumeration), optionally every cell re-oriented by a random proper
+    rotation of its local lexicographic numbering.  Duck-types Mesh for
+    NavierStokesOperator and the multigrid; brick() asks the library to
+    discover the bricks (glsOpDesc::brick = {-1,-1,-1})."""
+
+    def __init__(self, mesh, seed=0, rotate=False):
+        rng = np.random.default_rng(seed)
+        self.base = mesh
+        self.dim, self.degree = mesh.dim, mesh.degree
+        self.n_cells, self.n_nodes = mesh.n_cells, mesh.n_nodes
+        n = self.degree + 1
+        self.cell_order = rng.permutation(mesh.n_cells)  # new cell -> old cell
+        cn = np.asarray(mesh.cell_nodes, dtype=np.int64)[self.cell_order]
+        if rotate:
+            rots = _rotations(self.dim)
+            pick = rng.integers(0, len(rots), mesh.n_cells)
+            shp = (n,) * self.dim
+            for r, (perm, flips) in enumerate(rots):
+                sel = pick == r
+                if not sel.any():
+                    continue
+                # local arrays indexed [z][y][x] (x fastest): axis a of the
+                # cell is array axis dim-1-a
+                a = cn[sel].reshape((-1,) + shp)
+                axes = [0] + [1 + (self.dim - 1 - perm[self.dim - 1 - q]) for q in range(self.dim)]
+                a = a.transpose(axes)
+                for q in range(self.dim):
+                    if flips[q] < 0:
+                        a = np.flip(a, axis=1 + (self.dim - 1 - q))
+                cn[sel] = a.reshape(a.shape[0], -1)
+        # first-touch node numbering in the new cell order
+        flat = cn.ravel()
+        _, first = np.unique(flat, return_index=True)
+        order_old = flat[np.sort(first)]               # old nodes in first-touch order
+        self.node_old = order_old                      # new node -> old node
+        new_of_old = np.empty(mesh.n_nodes, dtype=np.int64)
+        new_of_old[order_old] = np.arange(len(order_old))
+        self.new_of_old = new_of_old
+        self.cell_nodes = new_of_old[cn].astype(np.uint32)
+        self.coords = np.asarray(mesh.coords)[order_old]
+        self._cached = None
+
+    @property
+    def n_dofs(self):
+        return self.n_nodes * (self.dim + 1)
+
+    def brick(self):
+        return (-1, -1, -1)
+
+    def cell_measure(self):
+        meas, hmin = self.base.cell_measure()
+        return meas[self.cell_order], hmin[self.cell_order]
+
+    def constraint_mask(self, *a, **k):
+        return np.asarray(self.base.constraint_mask(*a, **k))[self.node_old]
+
+    def child_lattice(self, fine):
+        """Child lattices of this (coarse) level's cells into `fine` (both
+        shuffled views of consecutive generator levels)."""
+        ch = np.asarray(self.base.child_lattice(fine.base), dtype=np.int64)
+        return fine.new_of_old[ch[self.cell_order]].astype(np.uint32)

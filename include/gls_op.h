@@ -108,8 +108,12 @@ typedef struct
                                  of bricks of brick[0]*brick[1]*brick[2]
                                  cells, lexicographic inside a brick, sharing
                                  nodes like a structured block (as produced by
-                                 gls_mesh_brick).  {0,0,0}: no structure —
-                                 every cell is its own brick.               */
+                                 gls_mesh_brick).  {-1,-1,-1}: any cell order
+                                 (deal.II's MatrixFree order) — the bricks are
+                                 discovered from the connectivity and the
+                                 cells run in brick order internally
+                                 (gls_op_cell_permutation).  {0,0,0}: no
+                                 structure, per-cell kernel.                */
 } glsOpDesc;
 
 typedef struct
@@ -123,6 +127,17 @@ typedef struct
 } glsOpParams;
 
 glsStatus gls_op_create(const glsOpDesc *desc, glsOp *out);
+/* The brick shape the operator runs ({0,0,0}: per-cell kernel) and its
+ * internal cell order: perm[internal cell] = caller cell, n_cells entries.
+ * Only gls_op_vmult_cells ranges refer to the internal order; table
+ * upload/download and every vector use the caller's numbering. */
+glsStatus gls_op_brick_shape(glsOp op, int *dims);
+/* The discovery gls_op_create runs for brick = {-1,-1,-1}, on its own (host
+ * only, no device call): shape = the brick shape found ({0,0,0}: none),
+ * perm[internal cell] = caller cell. */
+glsStatus gls_discover_bricks(int dim, int degree, int64_t n_cells, const uint32_t *cell_nodes,
+                              int *shape, int64_t *perm);
+glsStatus gls_op_cell_permutation(glsOp op, int64_t *perm);
 void      gls_op_destroy(glsOp op);
 glsStatus gls_op_set_parameters(glsOp op, const glsOpParams *prm);
 int64_t   gls_op_m(glsOp op); /* number of local dofs */
