@@ -412,6 +412,11 @@ struct glsMG_
   rocblas_int   *d_ipiv = nullptr;
   rocblas_int   *d_info = nullptr;
   double        *d_rhs  = nullptr; // [n0]
+  // coarse GMRES (coarse_iterate): FP64 Krylov workspace, two level-
+  // precision operand buffers, statistics of the last solve
+  double *cg_ws    = nullptr;
+  void   *cg_lvl   = nullptr;
+  int     cg_iters = 0, cg_conv = 0;
 
   size_t
   ts() const
@@ -659,31 +664,202 @@ coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
   HIP_THROW(hipGetLastError());
 }
 
+void v_step(glsMG_ *mg, int l, hipStream_t s);
+
+// the coarse "preconditioner" once: sol[0] from def[0] (multigrid.cc:465-489):
+// dense LU (< 0), identity (0) or relaxation sweeps (> 0)
+void
+coarse_apply(glsMG_ *mg, hipStream_t s)
+{
+  const size_t bytes = (size_t)mg->ops[0]->n_dofs * mg->ts();
+  if (mg->desc.coarse_n_iterations < 0)
+    {
+      if (mg->prec == GLS_F64)
+        coarse_lu_solve_t<double>(mg, s);
+      else
+        coarse_lu_solve_t<float>(mg, s);
+    }
+  else if (mg->desc.coarse_n_iterations == 0)
+    {
+      const int64_t w = (int64_t)(bytes / 4);
+      hipLaunchKernelGGL(k_copy, g1(w), dim3(256), 0, s, (uint32_t *)mg->sol[0],
+                         (const uint32_t *)mg->def[0], w);
+      HIP_THROW(hipGetLastError());
+    }
+  else
+    smooth(mg, 0, mg->sol[0], mg->def[0], true, mg->desc.coarse_n_iterations, s);
+}
+
+// r = b - r (the coarse GMRES restart residual)
+__global__ void
+k_sub(double *__restrict__ r, const double *__restrict__ b, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    r[i] = b[i] - r[i];
+}
+
+// coarse_grid_iterate (multigrid.cc:491-530, MGCoarseGridIterativeSolver):
+// SolverGMRES<VectorType<double>> with deal.II's defaults (left
+// preconditioning, max_n_tmp_vectors 30 -> restart after 28) under
+// ReductionControl(maxiter, 1e-20, reltol) on the coarse level operator,
+// preconditioned by coarse_apply (the substitute for Trilinos AMG / ILU:
+// relaxation sweeps or the dense LU).  FP64 Krylov vectors, the level
+// operator and preconditioner in the level precision (the reference solves
+// with the FP64 system matrix assembled from the MGNumber operator).  Every
+// vector stays on the device; per iteration the Hessenberg column crosses.
+template <typename T>
+void
+coarse_gmres_t(glsMG_ *mg, hipStream_t s)
+{
+  glsOp         op = mg->ops[0];
+  const int64_t n  = op->n_dofs;
+  const int     m  = 28;
+  if (n > (int64_t)0x7fffffff)
+    throw std::runtime_error("coarse GMRES: level too large for 32-bit rocBLAS sizes");
+  if (!mg->blas)
+    check_blas(rocblas_create_handle(&mg->blas), "rocblas_create_handle");
+  check_blas(rocblas_set_stream(mg->blas, s), "rocblas_set_stream");
+  check_blas(rocblas_set_pointer_mode(mg->blas, rocblas_pointer_mode_host), "pointer mode");
+  rocblas_handle h = mg->blas;
+  if (!mg->cg_ws)
+    {
+      HIP_THROW(hipMalloc((void **)&mg->cg_ws, ((size_t)(m + 4) * n + 2 * (m + 1)) * 8));
+      HIP_THROW(hipMalloc(&mg->cg_lvl, (size_t)2 * n * sizeof(T)));
+    }
+  double *V = mg->cg_ws, *w = V + (size_t)(m + 1) * n, *x = w + n, *b = x + n,
+         *dh = b + n;
+  T *la = (T *)mg->cg_lvl, *lb = la + n;
+  auto cvt_in = [&](T *dst, const double *src) {
+    hipLaunchKernelGGL((k_convert<double, T>), g1(n), dim3(256), 0, s, dst, src, n);
+  };
+  auto cvt_out = [&](double *dst, const T *src) {
+    hipLaunchKernelGGL((k_convert<T, double>), g1(n), dim3(256), 0, s, dst, src, n);
+  };
+  // dst = P^{-1} src (through def[0] -> sol[0])
+  auto prec = [&](double *dst, const double *src) {
+    cvt_in((T *)mg->def[0], src);
+    coarse_apply(mg, s);
+    cvt_out(dst, (const T *)mg->sol[0]);
+  };
+  auto apply_A = [&](double *dst, const double *src) {
+    cvt_in(la, src);
+    gls::op_vmult_device(op, lb, la, s);
+    cvt_out(dst, lb);
+  };
+  auto nrm2 = [&](const double *v) {
+    double r = 0;
+    check_blas(rocblas_dnrm2(h, (rocblas_int)n, v, 1, &r), "rocblas_dnrm2");
+    return r;
+  };
+  auto vc = [&](int j) { return V + (size_t)j * n; };
+  cvt_out(b, (const T *)mg->def[0]);
+  HIP_THROW(hipMemsetAsync(x, 0, n * 8, s));
+  // r0 = P^{-1} (b - A 0)
+  prec(vc(0), b);
+  double       res = nrm2(vc(0));
+  const double tol = std::max(mg->desc.coarse_reltol * res, 1e-20);
+  int          it  = 0;
+  std::vector<double> H((size_t)(m + 1) * m), g(m + 1), cs(m), sn(m), hc(2 * (m + 1)), y(m);
+  while (res > tol && it < mg->desc.coarse_maxiter)
+    {
+      const double sc = 1.0 / res;
+      check_blas(rocblas_dscal(h, (rocblas_int)n, &sc, vc(0), 1), "rocblas_dscal");
+      std::fill(g.begin(), g.end(), 0.0);
+      g[0]   = res;
+      int jd = 0;
+      for (int j = 0; j < m && it < mg->desc.coarse_maxiter; ++j)
+        {
+          apply_A(w, vc(j));   // w = A v_j
+          prec(vc(j + 1), w); // v_{j+1} = P^{-1} A v_j
+          double *wv = vc(j + 1);
+          const double one = 1.0, zero = 0.0, mone = -1.0;
+          for (int pass = 0; pass < 2; ++pass)
+            {
+              double *hp = dh + pass * (m + 1);
+              check_blas(rocblas_dgemv(h, rocblas_operation_transpose, (rocblas_int)n, j + 1,
+                                       &one, V, (rocblas_int)n, wv, 1, &zero, hp, 1),
+                         "rocblas_dgemv");
+              check_blas(rocblas_dgemv(h, rocblas_operation_none, (rocblas_int)n, j + 1, &mone, V,
+                                       (rocblas_int)n, hp, 1, &one, wv, 1),
+                         "rocblas_dgemv");
+            }
+          HIP_THROW(hipMemcpyAsync(hc.data(), dh, 2 * (m + 1) * 8, hipMemcpyDeviceToHost, s));
+          const double hn = nrm2(wv);
+          HIP_THROW(hipStreamSynchronize(s));
+          double *Hj = &H[(size_t)j * (m + 1)];
+          for (int i = 0; i <= j; ++i)
+            Hj[i] = hc[i] + hc[(m + 1) + i];
+          Hj[j + 1] = hn;
+          if (hn > 0)
+            {
+              const double sc2 = 1.0 / hn;
+              check_blas(rocblas_dscal(h, (rocblas_int)n, &sc2, wv, 1), "rocblas_dscal");
+            }
+          for (int i = 0; i < j; ++i)
+            {
+              const double t = cs[i] * Hj[i] + sn[i] * Hj[i + 1];
+              Hj[i + 1]      = -sn[i] * Hj[i] + cs[i] * Hj[i + 1];
+              Hj[i]          = t;
+            }
+          const double rr = std::hypot(Hj[j], Hj[j + 1]);
+          cs[j]           = rr > 0 ? Hj[j] / rr : 1.0;
+          sn[j]           = rr > 0 ? Hj[j + 1] / rr : 0.0;
+          Hj[j]           = rr;
+          Hj[j + 1]       = 0;
+          g[j + 1]        = -sn[j] * g[j];
+          g[j]            = cs[j] * g[j];
+          ++it;
+          ++jd;
+          res = std::fabs(g[j + 1]);
+          if (res <= tol || hn == 0)
+            break;
+        }
+      // x += V y (left preconditioning: the update is in the Krylov space)
+      for (int i = jd - 1; i >= 0; --i)
+        {
+          double t = g[i];
+          for (int c = i + 1; c < jd; ++c)
+            t -= H[(size_t)c * (m + 1) + i] * y[c];
+          y[i] = t / H[(size_t)i * (m + 1) + i];
+        }
+      HIP_THROW(hipMemcpyAsync(dh, y.data(), jd * 8, hipMemcpyHostToDevice, s));
+      {
+        const double one = 1.0;
+        check_blas(rocblas_dgemv(h, rocblas_operation_none, (rocblas_int)n, jd, &one, V,
+                                 (rocblas_int)n, dh, 1, &one, x, 1),
+                   "rocblas_dgemv");
+      }
+      HIP_THROW(hipStreamSynchronize(s)); // y is a host buffer reused below
+      if (res <= tol || it >= mg->desc.coarse_maxiter)
+        break;
+      // restart: r = P^{-1} (b - A x)
+      apply_A(w, x);
+      hipLaunchKernelGGL(k_sub, g1(n), dim3(256), 0, s, w, b, n);
+      prec(vc(0), w);
+      res = nrm2(vc(0));
+    }
+  mg->cg_iters = it;
+  mg->cg_conv  = res <= tol;
+  cvt_in((T *)mg->sol[0], x);
+  HIP_THROW(hipGetLastError());
+}
+
 // Multigrid::level_v_step (deal.II default V-cycle): solution[l] from defect[l]
 void
 v_step(glsMG_ *mg, int l, hipStream_t s)
 {
-  const size_t bytes = (size_t)mg->ops[l]->n_dofs * mg->ts();
+  if (l == 0 && mg->desc.coarse_iterate)
+    {
+      if (mg->prec == GLS_F64)
+        coarse_gmres_t<double>(mg, s);
+      else
+        coarse_gmres_t<float>(mg, s);
+      return;
+    }
   if (l == 0)
     {
-      // coarse solve (multigrid.cc:465-489): dense LU (< 0), identity (0)
-      // or relaxation sweeps (> 0)
-      if (mg->desc.coarse_n_iterations < 0)
-        {
-          if (mg->prec == GLS_F64)
-            coarse_lu_solve_t<double>(mg, s);
-          else
-            coarse_lu_solve_t<float>(mg, s);
-        }
-      else if (mg->desc.coarse_n_iterations == 0)
-        {
-          const int64_t w = (int64_t)(bytes / 4);
-          hipLaunchKernelGGL(k_copy, g1(w), dim3(256), 0, s, (uint32_t *)mg->sol[0],
-                             (const uint32_t *)mg->def[0], w);
-          HIP_THROW(hipGetLastError());
-        }
-      else
-        smooth(mg, 0, mg->sol[0], mg->def[0], true, mg->desc.coarse_n_iterations, s);
+      coarse_apply(mg, s);
       return;
     }
   const int nit = mg->desc.smoothing_n_iterations;
@@ -789,7 +965,8 @@ run_v_step(glsMG_ *mg, int top, hipStream_t s)
   // the kernels' own duration, not by host launch overhead; off by default
   const char *e   = getenv("GLS_MG_GRAPH");
   const bool  use = (e && std::atoi(e) != 0) &&
-                   mg->desc.coarse_n_iterations >= 0; // rocSOLVER coarse LU: not captured
+                   mg->desc.coarse_n_iterations >= 0 && // rocSOLVER coarse LU: not captured
+                   !mg->desc.coarse_iterate;            // coarse GMRES syncs the host
   if (!use)
     {
       v_step(mg, top, s);
@@ -993,7 +1170,8 @@ gls_mg_destroy(glsMG mg)
         (void)hipFree(p);
   if (mg->d_acc)
     (void)hipFree(mg->d_acc);
-  for (void *p : {(void *)mg->d_lu, (void *)mg->d_ipiv, (void *)mg->d_info, (void *)mg->d_rhs})
+  for (void *p : {(void *)mg->d_lu, (void *)mg->d_ipiv, (void *)mg->d_info, (void *)mg->d_rhs,
+                  (void *)mg->cg_ws, mg->cg_lvl})
     if (p)
       (void)hipFree(p);
   if (mg->blas)
@@ -1161,6 +1339,17 @@ mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s)
 } // namespace gls
 
 extern "C" {
+
+glsStatus
+gls_mg_coarse_statistics(glsMG mg, int *n_iterations, int *converged)
+{
+  GLS_TRY
+  if (!mg || !n_iterations || !converged)
+    throw std::runtime_error("gls_mg_coarse_statistics: null argument");
+  *n_iterations = mg->cg_iters;
+  *converged    = mg->cg_conv;
+  GLS_CATCH
+}
 
 glsStatus
 gls_mg_prolongate_add(glsMG mg, int level, void *dst_fine, const void *src_coarse,

@@ -36,7 +36,7 @@ EXPORTS = [
     "gls_op_get_max_u", "gls_mg_set_vector_layout", "gls_dist_update_ghost_values",
     "gls_dist_get_max_u", "gls_op_compute_diagonal", "gls_op_invert_diagonal", "gls_mg_relax",
     "gls_dist_compress_add", "gls_op_brick_shape", "gls_op_cell_permutation",
-    "gls_discover_bricks",
+    "gls_discover_bricks", "gls_mg_coarse_statistics",
 ]
 
 GLS_MEM_DEVICE, GLS_MEM_HOST = 0, 1
@@ -60,7 +60,8 @@ class MGDesc(C.Structure):
     _fields_ = [("n_levels", C.c_int), ("smoothing_n_iterations", C.c_int),
                 ("smoothing_eig_n_iterations", C.c_int), ("smoothing_range", C.c_double),
                 ("coarse_n_iterations", C.c_int), ("outer_precision", C.c_int),
-                ("compute_evs_n_levels", C.c_int)]
+                ("compute_evs_n_levels", C.c_int), ("coarse_iterate", C.c_int),
+                ("coarse_reltol", C.c_double), ("coarse_maxiter", C.c_int)]
 
 
 class DistDesc(C.Structure):
@@ -143,6 +144,7 @@ def lib():
         L.gls_dist_compress_add.argtypes = [vp, vp, vp]
         L.gls_op_brick_shape.argtypes = [vp, vp]
         L.gls_op_cell_permutation.argtypes = [vp, vp]
+        L.gls_mg_coarse_statistics.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.gls_discover_bricks.argtypes = [C.c_int, C.c_int, i64, vp, vp, vp]
         L.gls_last_error.restype = C.c_char_p
         _lib = L
@@ -471,7 +473,8 @@ class Multigrid:
 
     def __init__(self, level_ops, child_lattices, smoothing_n_iterations=5,
                  smoothing_eig_n_iterations=20, smoothing_range=20.0, coarse_n_iterations=20,
-                 outer_precision="f64", compute_evs_n_levels=0):
+                 outer_precision="f64", compute_evs_n_levels=0, coarse_iterate=False,
+                 coarse_reltol=1e-4, coarse_maxiter=10000):
         self.ops = list(level_ops)
         self._child = [None] + [np.ascontiguousarray(c, dtype=np.uint32)
                                 for c in child_lattices]
@@ -480,7 +483,8 @@ class Multigrid:
         ch = (C.c_void_p * n)(*[0 if c is None else c.ctypes.data for c in self._child])
         outer = GLS_F64 if outer_precision in ("f64", GLS_F64) else GLS_F32
         self.desc = MGDesc(n, smoothing_n_iterations, smoothing_eig_n_iterations,
-                           smoothing_range, coarse_n_iterations, outer, compute_evs_n_levels)
+                           smoothing_range, coarse_n_iterations, outer, compute_evs_n_levels,
+                           int(bool(coarse_iterate)), coarse_reltol, coarse_maxiter)
         self.outer_dtype = None
         h = C.c_void_p()
         _check(lib().gls_mg_create(C.byref(self.desc), C.cast(arr, C.c_void_p),
@@ -497,6 +501,13 @@ class Multigrid:
 
     def setup(self):
         _check(lib().gls_mg_setup(self.h, _stream()))
+
+    def coarse_statistics(self):
+        """(GMRES iterations, converged) of the last coarse solve
+        (coarse_iterate=True)."""
+        it, cv = C.c_int(), C.c_int()
+        _check(lib().gls_mg_coarse_statistics(self.h, C.byref(it), C.byref(cv)))
+        return it.value, bool(cv.value)
 
     def relaxation(self, level):
         w, lam = C.c_double(), C.c_double()

@@ -246,6 +246,14 @@ typedef struct
   int    compute_evs_n_levels; /* "gmg compute evs n levels" (multigrid.cc:
                                   307, 355-358): > 0 also estimates the
                                   relaxation factor on the coarsest level    */
+  int    coarse_iterate;       /* "gmg coarse grid iterate" (multigrid.cc:
+                                  491-530): 1 = GMRES on the coarse level
+                                  (FP64 vectors, left preconditioning, 30
+                                  temporary vectors, deal.II SolverGMRES
+                                  defaults) preconditioned by the coarse
+                                  solver above; 0 = apply it once            */
+  double coarse_reltol;        /* 1e-4  multigrid.h:41 (ReductionControl)    */
+  int    coarse_maxiter;       /* 10000 multigrid.h:39                       */
 } glsMGDesc;
 
 /* levels[l] are level operators (same precision); child[l] for l >= 1 is the
@@ -259,6 +267,9 @@ void      gls_mg_destroy(glsMG mg);
 glsStatus gls_mg_setup(glsMG mg, void *stream);
 glsStatus gls_mg_get_relaxation(glsMG mg, int level, double *omega,
                                 double *lambda_max);
+/* GMRES iterations of the last coarse solve (coarse_iterate = 1), and
+ * whether it reached the tolerance */
+glsStatus gls_mg_coarse_statistics(glsMG mg, int *n_iterations, int *converged);
 /* one V-cycle on the finest level: dst = V(src) (PreconditionMG::vmult) */
 glsStatus gls_mg_vcycle(glsMG mg, void *dst, const void *src, void *stream);
 /* caller vector layout of gls_mg_vcycle's dst / src (as gls_op_set_vector_

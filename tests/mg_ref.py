@@ -10,7 +10,10 @@ reference binary):
   Multigrid::level_v_step V-cycle with MGSmootherPrecondition pre/post
     smoothing, MGTwoLevelTransfer restrict/prolongate (multigrid.cc:534-548)
   coarse solve: relaxation sweeps from zero (substitution for the
-    Trilinos direct / AMG coarse solvers, multigrid.cc:448-489)
+    Trilinos direct / AMG coarse solvers, multigrid.cc:448-489); with
+    coarse_gmres_reltol, coarse_grid_iterate (multigrid.cc:491-530): deal.II
+    SolverGMRES defaults (left preconditioning, restart after 28) under
+    ReductionControl(10000, 1e-20, reltol), preconditioned by those sweeps
 """
 import numpy as np
 
@@ -33,7 +36,8 @@ def power_start_vector(n_dofs, cmask, dim):
 
 class OracleGMG:
     def __init__(self, meshes, cmasks, params, u_star, hist=None, weights=None,
-                 n_smooth=5, n_eig=20, smoothing_range=20.0, coarse_iters=20):
+                 n_smooth=5, n_eig=20, smoothing_range=20.0, coarse_iters=20,
+                 coarse_gmres_reltol=None):
         self.meshes = meshes
         self.om = [orc.OracleMesh(m, c) for m, c in zip(meshes, cmasks)]
         self.omz = [orc.OracleMesh(m, np.zeros(m.n_nodes, np.uint8)) for m in meshes]
@@ -41,6 +45,8 @@ class OracleGMG:
                                for l in range(1, len(meshes))]
         self.n_smooth, self.n_eig = n_smooth, n_eig
         self.range, self.coarse_iters = smoothing_range, coarse_iters
+        self.coarse_gmres_reltol = coarse_gmres_reltol
+        self.coarse_gmres_iterations = 0
         L = len(meshes)
         u = [None] * L
         h = [None] * L
@@ -118,7 +124,66 @@ class OracleGMG:
             self._A0 = A
         return self._A0
 
+    def coarse_precondition(self, b):
+        if self.coarse_iters < 0:
+            return np.linalg.solve(self.coarse_matrix(), b)
+        if self.coarse_iters == 0:
+            return b.copy()
+        return self.smooth(0, None, b, True, self.coarse_iters)
+
+    def coarse_gmres(self, b, m=28, maxiter=10000):
+        A, P = self.ops[0].vmult, self.coarse_precondition
+        x = np.zeros_like(b)
+        r = P(b)
+        res = np.linalg.norm(r)
+        tol = max(self.coarse_gmres_reltol * res, 1e-20)
+        it = 0
+        while res > tol and it < maxiter:
+            V = [r / res]
+            H = np.zeros((m + 1, m))
+            g = np.zeros(m + 1)
+            g[0] = res
+            cs, sn = np.zeros(m), np.zeros(m)
+            jd = 0
+            for j in range(m):
+                w = P(A(V[j]))
+                h = np.zeros(j + 1)
+                for _ in range(2):  # CGS2
+                    hp = np.array([v @ w for v in V])
+                    w = w - sum(c * v for c, v in zip(hp, V))
+                    h += hp
+                hn = np.linalg.norm(w)
+                H[:j + 1, j] = h
+                H[j + 1, j] = hn
+                V.append(w / hn if hn > 0 else w)
+                for i in range(j):
+                    t = cs[i] * H[i, j] + sn[i] * H[i + 1, j]
+                    H[i + 1, j] = -sn[i] * H[i, j] + cs[i] * H[i + 1, j]
+                    H[i, j] = t
+                rr = np.hypot(H[j, j], H[j + 1, j])
+                cs[j], sn[j] = (H[j, j] / rr, H[j + 1, j] / rr) if rr > 0 else (1.0, 0.0)
+                H[j, j], H[j + 1, j] = rr, 0.0
+                g[j + 1] = -sn[j] * g[j]
+                g[j] = cs[j] * g[j]
+                it += 1
+                jd += 1
+                res = abs(g[j + 1])
+                if res <= tol or hn == 0:
+                    break
+            y = np.zeros(jd)
+            for i in range(jd - 1, -1, -1):
+                y[i] = (g[i] - H[i, i + 1:jd] @ y[i + 1:jd]) / H[i, i]
+            x = x + sum(c * v for c, v in zip(y, V[:jd]))
+            if res <= tol:
+                break
+            r = P(b - A(x))
+            res = np.linalg.norm(r)
+        self.coarse_gmres_iterations = it
+        return x
+
     def v_step(self, l, b):
+        if l == 0 and self.coarse_gmres_reltol is not None:
+            return self.coarse_gmres(b)
         if l == 0:
             if self.coarse_iters < 0:
                 return np.linalg.solve(self.coarse_matrix(), b)

@@ -187,3 +187,38 @@ def test_vcycle_preconditions_gmres():
     # measured: 6.2e-3 after 20 iterations with a two-level FP32 V-cycle
     assert prec[-1] < 1e-2, prec
     assert prec[-1] < 0.25 * plain[-1], (prec[-1], plain[-1])
+
+
+@pytest.mark.parametrize("name,n_ref,coarse", [("input_turek_2D_Re20_stat.json", 2, -1),
+                                               ("input_sphere_amg.json", 1, 10)])
+def test_coarse_gmres_vcycle(name, n_ref, coarse):
+    """The AMG decks' "gmg coarse grid iterate" (multigrid.cc:491-530): GMRES
+    to 1e-4 on the coarse level inside the V-cycle, preconditioned by the
+    substitute for Trilinos AMG: the dense LU on the
+    stationary saddle-point deck (Jacobi sweeps diverge there), 10 relaxation
+    sweeps on the sphere; against the oracle multigrid's restatement on the
+    GPU's own omegas/diagonals."""
+    import torch
+    import glsamd
+    meshes, cmasks, params, w, u, hist = _hierarchy(name, n_ref)
+    mg, ops = glsamd.build_gmg(meshes, cmasks, params, u, hist, w, precision="f32",
+                               coarse_n_iterations=coarse, coarse_iterate=True,
+                               coarse_reltol=1e-4, coarse_maxiter=500)
+    ref = OracleGMG(meshes, cmasks, params, u, hist, w, coarse_iters=coarse,
+                    coarse_gmres_reltol=1e-4)
+    ref.set_omega([mg.relaxation(l)[0] for l in range(len(meshes))])
+    for l in range(len(meshes)):
+        dl = ops[l].initialize_dof_vector()
+        ops[l].compute_inverse_diagonal(dl)
+        ref.invdiag[l] = _np(dl)
+    L = len(meshes) - 1
+    b = gi.rnd(11, meshes[L].n_dofs)
+    src = torch.from_numpy(b).cuda()
+    dst = torch.zeros_like(src)
+    mg.vcycle(dst, src)
+    torch.cuda.synchronize()
+    it, conv = mg.coarse_statistics()
+    xr = ref.vcycle(b)
+    assert conv and it > 0
+    assert abs(it - ref.coarse_gmres_iterations) <= 3, (it, ref.coarse_gmres_iterations)
+    assert rel_err(_np(dst), xr) < 2e-3
