@@ -15,8 +15,11 @@ out = {}
 for (k, c), v in sorted(agg.items()):
     out.setdefault(k, {})[c] = sum(v) / len(v)
 traffic = 0.0
+prec_t = "double" if (sys.argv[3] if len(sys.argv) > 3 else "f64") == "f64" else "float"
 for k, d in out.items():
-    if "k_brick" in k or "k_shared_reduce" in k:
+    # the headline precision only (bench's parity check also runs the FP32
+    # level operator under the same passes)
+    if ("k_brick" in k or "k_shared_reduce" in k) and prec_t in k:
         traffic += 1024 * (2 * d.get("FETCH_SIZE", 0) + d.get("WRITE_SIZE", 0))
 for k, d in out.items():
     print(k)
