@@ -388,8 +388,12 @@ struct glsMG_
   std::vector<void *>     d_weight; // level l >= 1: [n_dofs(l)]
   std::vector<void *>     invdiag, sol, def, tmp;
   std::vector<double>     omega, lambda;
-  double                 *d_acc = nullptr; // power iteration: block partials | 2 scalars
-  int64_t                 acc_blocks = 0;
+  // power iteration: per level, block partials | 2 scalars (the levels'
+  // estimates run concurrently, gls_mg_setup)
+  double                 *d_acc = nullptr;
+  std::vector<int64_t>    acc_off; // level l's partials start at d_acc + acc_off[l]
+  std::vector<hipStream_t> side;   // setup: one stream per level, joined by events
+  std::vector<hipEvent_t>  side_ev;
   double                  P[MAXP][MAXN]{};
   bool                    setup_done = false;
   bool                    partitioned = false; // rank-local level operators
@@ -919,16 +923,16 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
 // different numbering (deviation).  All reductions stay on the
 // device; the host reads lambda once after the last iteration.
 template <typename T>
-double
+void
 power_iteration_t(glsMG_ *mg, int l, hipStream_t s)
 {
+  // enqueues the estimate on s; the Rayleigh quotient x.y of the last step
+  // ends in d_acc[acc_off[l] + 2 nb] (gls_mg_setup collects it)
   glsOp         op = mg->ops[l];
   const int64_t n  = op->n_dofs;
   void         *x = mg->sol[l], *y = mg->tmp[l];
   const int64_t nb   = (n + 255) / 256;
-  double       *part = mg->d_acc, *scal = mg->d_acc + 2 * mg->acc_blocks;
-  if (nb > mg->acc_blocks)
-    throw std::runtime_error("power iteration: reduction buffer too small");
+  double       *part = mg->d_acc + mg->acc_off[l], *scal = part + 2 * nb;
   // start vector on the device: mean of i % 11 over [0, n) in closed form
   const int64_t q11  = n / 11, r11 = n % 11;
   const double  mean = n > 0 ? (double)(q11 * 55 + r11 * (r11 - 1) / 2) / (double)n : 0.0;
@@ -950,10 +954,6 @@ power_iteration_t(glsMG_ *mg, int l, hipStream_t s)
                          (const double *)scal, n);
       HIP_THROW(hipGetLastError());
     }
-  double lam = 0;
-  HIP_THROW(hipMemcpyAsync(&lam, scal, sizeof(double), hipMemcpyDeviceToHost, s));
-  HIP_THROW(hipStreamSynchronize(s));
-  return std::abs(lam);
 }
 
 // v_step(top) on stream s: replayed from a captured hipGraph when possible
@@ -1146,9 +1146,13 @@ gls_mg_create(const glsMGDesc *desc, const glsOp *levels, const uint32_t *const 
     }
   mg->omega.assign(nl_levels, 1.0);
   mg->lambda.assign(nl_levels, 0.0);
+  int64_t acc_total = 0;
   for (int l = 0; l < nl_levels; ++l)
-    mg->acc_blocks = std::max<int64_t>(mg->acc_blocks, (mg->ops[l]->n_dofs + 255) / 256);
-  HIP_THROW(hipMalloc((void **)&mg->d_acc, (2 * mg->acc_blocks + 2) * sizeof(double)));
+    {
+      mg->acc_off.push_back(acc_total);
+      acc_total += 2 * ((mg->ops[l]->n_dofs + 255) / 256) + 2;
+    }
+  HIP_THROW(hipMalloc((void **)&mg->d_acc, std::max<int64_t>(acc_total, 1) * sizeof(double)));
   *out = mg;
   GLS_CATCH
 }
@@ -1170,6 +1174,10 @@ gls_mg_destroy(glsMG mg)
         (void)hipFree(p);
   if (mg->d_acc)
     (void)hipFree(mg->d_acc);
+  for (hipStream_t st : mg->side)
+    (void)hipStreamDestroy(st);
+  for (hipEvent_t ev : mg->side_ev)
+    (void)hipEventDestroy(ev);
   for (void *p : {(void *)mg->d_lu, (void *)mg->d_ipiv, (void *)mg->d_info, (void *)mg->d_rhs,
                   (void *)mg->cg_ws, mg->cg_lvl})
     if (p)
@@ -1199,11 +1207,32 @@ gls_mg_setup(glsMG mg, void *stream)
   if (mg->partitioned)
     throw std::runtime_error("gls_mg_setup: partitioned levels are set up by the host-driven "
                              "distributed multigrid (glsdist.py)");
-  hipStream_t s = (hipStream_t)stream;
-  for (size_t l = 0; l < mg->ops.size(); ++l)
+  hipStream_t  s  = (hipStream_t)stream;
+  const size_t nl = mg->ops.size();
+  // the levels are independent here: each level's diagonal and power
+  // iteration run on a stream of its own (forked from and joined back into
+  // s by events), so the small levels' launch-bound steps overlap the fine
+  // level's instead of queueing behind them
+  if (mg->side.empty())
+    for (size_t l = 0; l < nl; ++l)
+      {
+        hipStream_t st;
+        hipEvent_t  ev;
+        HIP_THROW(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIP_THROW(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        mg->side.push_back(st);
+        mg->side_ev.push_back(ev);
+      }
+  hipEvent_t fork;
+  HIP_THROW(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+  HIP_THROW(hipEventRecord(fork, s));
+  std::vector<char> estimate(nl, 0);
+  for (size_t l = 0; l < nl; ++l)
     {
+      hipStream_t ls = mg->side[l];
+      HIP_THROW(hipStreamWaitEvent(ls, fork, 0));
       // compute_inverse_diagonal (multigrid.cc:290-293)
-      gls::op_inverse_diagonal_device(mg->ops[l], mg->invdiag[l], s);
+      gls::op_inverse_diagonal_device(mg->ops[l], mg->invdiag[l], ls);
       // relaxation = 0: omega from the power-iteration estimate of
       // lambda_max(D^-1 A) (power_iteration_t), estimated on the levels
       // above the coarsest one (multigrid.cc:355-358 with
@@ -1218,22 +1247,42 @@ gls_mg_setup(glsMG mg, void *stream)
         }
       else
         {
-          const double lam = mg->prec == GLS_F64 ? power_iteration_t<double>(mg, (int)l, s) :
-                                                   power_iteration_t<float>(mg, (int)l, s);
-          const double ev_max = 1.2 * lam; // estimate_eigenvalues' safety factor
-          mg->lambda[l]       = ev_max;
-          if (ev_max > 0)
-            {
-              const double alpha = mg->desc.smoothing_range > 1.0 ?
-                                     ev_max / mg->desc.smoothing_range :
-                                     0.9 * ev_max;
-              mg->omega[l] = 2.0 / (alpha + ev_max);
-            }
+          if (mg->prec == GLS_F64)
+            power_iteration_t<double>(mg, (int)l, ls);
           else
-            mg->omega[l] = 1.0;
+            power_iteration_t<float>(mg, (int)l, ls);
+          estimate[l] = 1;
         }
-      HIP_THROW(hipMemsetAsync(mg->sol[l], 0, (size_t)mg->ops[l]->n_dofs * mg->ts(), s));
+      HIP_THROW(hipMemsetAsync(mg->sol[l], 0, (size_t)mg->ops[l]->n_dofs * mg->ts(), ls));
+      HIP_THROW(hipEventRecord(mg->side_ev[l], ls));
+      HIP_THROW(hipStreamWaitEvent(s, mg->side_ev[l], 0));
     }
+  HIP_THROW(hipEventDestroy(fork));
+  // collect the Rayleigh quotients (one host sync for all levels)
+  std::vector<double> lam(nl, 0.0);
+  for (size_t l = 0; l < nl; ++l)
+    if (estimate[l])
+      {
+        const int64_t nb = (mg->ops[l]->n_dofs + 255) / 256;
+        HIP_THROW(hipMemcpyAsync(&lam[l], mg->d_acc + mg->acc_off[l] + 2 * nb, sizeof(double),
+                                 hipMemcpyDeviceToHost, s));
+      }
+  HIP_THROW(hipStreamSynchronize(s));
+  for (size_t l = 0; l < nl; ++l)
+    if (estimate[l])
+      {
+        const double ev_max = 1.2 * std::abs(lam[l]); // estimate_eigenvalues' safety factor
+        mg->lambda[l]       = ev_max;
+        if (ev_max > 0)
+          {
+            const double alpha = mg->desc.smoothing_range > 1.0 ?
+                                   ev_max / mg->desc.smoothing_range :
+                                   0.9 * ev_max;
+            mg->omega[l] = 2.0 / (alpha + ev_max);
+          }
+        else
+          mg->omega[l] = 1.0;
+      }
   if (mg->desc.coarse_n_iterations < 0)
     {
       if (mg->prec == GLS_F64)
