@@ -246,6 +246,34 @@ def mg_companions(d, params, weights, n_ref, reps=20):
     os.environ["GLS_MG_GRAPH"] = "1"
     vc_graph = vcycles()
     os.environ.pop("GLS_MG_GRAPH")
+    # the deck's own coarse solver ("gmg coarse grid solver": "direct",
+    # multigrid.cc:448-455): a dense LU of the assembled r0 operator
+    # (rocSOLVER getrf once in the setup, getrs per V-cycle)
+    lu = {}
+    try:
+        mg_lu, _ = glsamd.build_gmg(meshes, cm, params, u, hist, weights, precision="f32",
+                                    coarse_n_iterations=-1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        mg_lu.setup()
+        torch.cuda.synchronize()
+        lu["setup_ms"] = (time.perf_counter() - t0) * 1e3
+        for _ in range(3):
+            mg_lu.vcycle(x, b)
+        torch.cuda.synchronize()
+        t = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            mg_lu.vcycle(x, b)
+            e1.record()
+            torch.cuda.synchronize()
+            t.append(e0.elapsed_time(e1))
+        lu["ms"] = float(np.median(t))
+        lu["coarse_dofs"] = meshes[0].n_dofs
+        del mg_lu
+    except Exception as e:  # reported, never fatal
+        lu = {"error": str(e)}
     # GMRES: fixed 28 iterations (one restart cycle), wall time per iteration
     solver = glsamd.LinearSolverGMRES(A, mg, n_max_iterations=28, relative_tolerance=1e-30,
                                       absolute_tolerance=0.0)
@@ -267,6 +295,7 @@ def mg_companions(d, params, weights, n_ref, reps=20):
                                                     "levels": n_ref + 1,
                                                     "finest_dofs": meshes[-1].n_dofs,
                                                     "vcycles_per_s": 1e3 / vc},
+            f"r{n_ref}_vcycle_f32_coarse_direct_lu": lu,
             f"r{n_ref}_gmres_iteration": {"ms": float(np.median(times)) * 1e3,
                                           "note": "V-cycle + FP64 vmult + CGS2 + host "
                                                   "Hessenberg step, wall clock"}}
