@@ -649,7 +649,9 @@ struct Impl
         a.Ly            = op->Ly;
         // padded LDS lattice: 3D Q2 bricks of 4x4 cells in x, y use strides
         // 11, 12 (ds_read_b128 conflict-free x sweep, exhaustive search)
-        const bool pad  = dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9;
+        static const bool pad32 = !getenv("GLS_PAD32") || std::atoi(getenv("GLS_PAD32")) != 0;
+        const bool pad  = dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9 &&
+                         (sizeof(T) == 8 || pad32);
         a.PLx           = pad ? 11 : op->Lx;
         a.PLy           = pad ? 12 : op->Ly;
         a.LP            = a.PLx * a.PLy * (op->L / (op->Lx * op->Ly));
