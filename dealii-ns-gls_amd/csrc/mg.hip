@@ -394,7 +394,7 @@ struct glsMG_
   std::vector<int64_t>    acc_off; // level l's partials start at d_acc + acc_off[l]
   std::vector<hipStream_t> side;   // setup: one stream per level, joined by events
   std::vector<hipEvent_t>  side_ev;
-  double                  P[MAXP][MAXN]{};
+  double                  P[3][MAXP][MAXN]{}; // 1D prolongation per coarse degree (1, 2)
   bool                    setup_done = false;
   bool                    partitioned = false; // rank-local level operators
   gls::VecStage           stage; // caller layout of gls_mg_vcycle's vectors
@@ -440,9 +440,10 @@ targs(const glsMG_ *mg, int level)
   a.child        = mg->d_child[level];
   a.weight       = (const T *)mg->d_weight[level];
   a.n_cells_c    = mg->ops[level - 1]->n_cells;
+  const int kc   = mg->ops[level - 1]->degree;
   for (int i = 0; i < MAXP; ++i)
     for (int j = 0; j < MAXN; ++j)
-      a.P[i][j] = (T)mg->P[i][j];
+      a.P[i][j] = (T)mg->P[kc][i][j];
   return a;
 }
 
@@ -473,7 +474,9 @@ void
 transfer_p(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hipStream_t s,
            const void *base)
 {
-  const int d = mg->dim, k = mg->degree;
+  // the coarse level's degree: a FE_Q_iso_Q1 coarsest level is Q1 on the
+  // sub-cells under Q_k levels (main.cc:436-446)
+  const int d = mg->dim, k = mg->ops[level - 1]->degree;
   if (d == 2 && k == 1)
     transfer_t<2, 1, T>(mg, kind, level, dst, src, s, base);
   else if (d == 2 && k == 2)
@@ -1098,15 +1101,18 @@ gls_mg_create(const glsMGDesc *desc, const glsOp *levels, const uint32_t *const 
   mg->desc   = *desc;
   mg->prec   = levels[0]->prec;
   mg->dim    = levels[0]->dim;
-  mg->degree = levels[0]->degree;
+  mg->degree = levels[desc->n_levels - 1]->degree;
   mg->nc     = mg->dim + 1;
   const int nl_levels = desc->n_levels;
   for (int l = 0; l < nl_levels; ++l)
     {
       glsOp op = levels[l];
-      if (!op || op->prec != mg->prec || op->dim != mg->dim || op->degree != mg->degree)
+      // every level shares dim, precision and degree, except that the
+      // coarsest may be of lower degree (FE_Q_iso_Q1: Q1 on the sub-cells)
+      if (!op || op->prec != mg->prec || op->dim != mg->dim ||
+          (l > 0 && op->degree != mg->degree) || op->degree > mg->degree)
         throw std::runtime_error("gls_mg_create: level operators must share dim, degree and "
-                                 "precision");
+                                 "precision (the coarsest may be of lower degree)");
       // partitioned (rank-local) level operators: the transfers
       // (prolongate_add / restrict_add / interpolate) and the relaxation
       // step serve the host-driven distributed multigrid (glsdist.py);
@@ -1116,29 +1122,32 @@ gls_mg_create(const glsMGDesc *desc, const glsOp *levels, const uint32_t *const 
     }
   if (nl_levels > 1 && (!child || mg->degree > 2))
     throw std::runtime_error("gls_mg_create: child lattices required (degree <= 2)");
-  // 1D prolongation: parent GLL basis at the child lattice points
-  const int k = mg->degree;
-  Basis1D   b(k);
-  for (int I = 0; I <= 2 * k; ++I)
+  // 1D prolongation per coarse degree: parent GLL basis at the child
+  // lattice points (for a Q1 coarse level under Q_k: the iso-Q1 embedding)
+  for (int k = 1; k <= 2; ++k)
     {
-      const int    c = I / k > 1 ? 1 : I / k;
-      const double x = 0.5 * (c + b.nodes[I - c * k]);
-      for (int j = 0; j <= k; ++j)
+      Basis1D b(k);
+      for (int I = 0; I <= 2 * k; ++I)
         {
-          double v = 1;
-          for (int m = 0; m <= k; ++m)
-            if (m != j)
-              v *= (x - b.nodes[m]) / (b.nodes[j] - b.nodes[m]);
-          mg->P[I][j] = v;
+          const int    c = I / k > 1 ? 1 : I / k;
+          const double x = 0.5 * (c + b.nodes[I - c * k]);
+          for (int j = 0; j <= k; ++j)
+            {
+              double v = 1;
+              for (int m = 0; m <= k; ++m)
+                if (m != j)
+                  v *= (x - b.nodes[m]) / (b.nodes[j] - b.nodes[m]);
+              mg->P[k][I][j] = v;
+            }
         }
     }
-  const int L  = 2 * k + 1;
-  const int nl = mg->dim == 3 ? L * L * L : L * L;
   mg->d_child.assign(nl_levels, nullptr);
   mg->d_weight.assign(nl_levels, nullptr);
   for (int l = 1; l < nl_levels; ++l)
     {
       glsOp         cop = mg->ops[l - 1], fop = mg->ops[l];
+      const int     L   = 2 * cop->degree + 1;
+      const int     nl  = mg->dim == 3 ? L * L * L : L * L;
       const int64_t nch = cop->n_cells * nl;
       std::vector<uint32_t> ch(child[l], child[l] + nch);
       std::vector<uint8_t>  seen((size_t)fop->n_nodes, 0);

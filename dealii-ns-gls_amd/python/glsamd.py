@@ -550,11 +550,16 @@ class Multigrid:
 
 
 def build_gmg(meshes, cmasks, params, u_star_fine, history_fine=None, weights=None,
-              precision="f32", **mg_kwargs):
+              precision="f32", coarse_iso_q1=False, **mg_kwargs):
     """Level operators + transfers for a mesh hierarchy (coarse -> fine), the
     linearization point / history interpolated down level by level
-    (interpolate_to_mg, main.cc:772-803, 815-832).  Returns (mg, level_ops)."""
+    (interpolate_to_mg, main.cc:772-803, 815-832).  coarse_iso_q1: the
+    coarsest level with FE_Q_iso_Q1 (glsmesh.IsoQ1Mesh, main.cc:436-446).
+    Returns (mg, level_ops)."""
     import torch
+    if coarse_iso_q1:
+        import glsmesh
+        meshes = [glsmesh.IsoQ1Mesh(meshes[0])] + list(meshes[1:])
     ops = []
     for m, cm in zip(meshes, cmasks):
         op = NavierStokesOperator(m, cm, precision)

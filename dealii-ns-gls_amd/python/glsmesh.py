@@ -287,6 +287,11 @@ class Deck:
         # main.cc:331
         return self.nonlinear_solver == "Newton"
 
+    @property
+    def use_fe_q_iso_q1(self):
+        # "gmg coarse grid use fe q iso q1" (main.cc:136, 436-446)
+        return bool(self.raw.get("gmg coarse grid use fe q iso q1", False))
+
     def boundary_descriptor(self):
         """(vel_ids, p_ids, slip_ids) of constraints_homogeneous
         (simulation.cc:378-431 + main.cc:259-291)."""
@@ -489,3 +494,88 @@ class ShuffledMesh:
         shuffled views of consecutive generator levels)."""
         ch = np.asarray(self.base.child_lattice(fine.base), dtype=np.int64)
         return fine.new_of_old[ch[self.cell_order]].astype(np.uint32)
+
+
+# ------------------------------------------------------------ FE_Q_iso_Q1
+class IsoQ1Mesh:
+    """The multigrid's coarsest level with FE_Q_iso_Q1 (main.cc:436-446,
+    "gmg coarse grid use fe q iso q1"): the same support points as FE_Q(k)
+    on the coarse cells, the basis piecewise linear on the k^dim sub-cells of
+    every cell, quadrature QIterated(QGauss(2), k) — which is the Q1 operator
+    on the sub-cells with QGauss(2), on the unchanged node numbering.  So the
+    level is a degree-1 NavierStokesOperator over the sub-cells (k^dim per
+    coarse cell, lexicographic, a k x k (x k) brick each); the penalty
+    parameters keep the coarse cell's (operator_ns.cc:399-407: measure /
+    fe_degree with fe_degree = k — here the sub-cell measure |K| / k^dim at
+    degree 1 — and the cell's minimum vertex distance).  The transfer to the
+    next level is the Q1 one: every sub-cell is one child of the next level,
+    whose Q_k nodes sit at the sub-cell's 3^dim refined lattice points
+    (child_lattice), and the linear embedding is the iso-Q1 prolongation.
+    Geometry: the sub-cells are mapped multilinearly through their corner
+    support points — exact for multilinear coarse cells (the sphere mesh);
+    on MappingQ_k-curved cells this differs from the parent mapping at the
+    iterated points."""
+
+    def __init__(self, mesh):
+        k, dim = mesh.degree, mesh.dim
+        if k < 2:
+            raise ValueError("FE_Q_iso_Q1 needs a coarse element of degree >= 2")
+        self.base, self.k = mesh, k
+        self.dim, self.degree = dim, 1
+        self.n_nodes = mesh.n_nodes
+        self.coords = mesh.coords
+        n = k + 1
+        cn = np.asarray(mesh.cell_nodes, dtype=np.int64).reshape((-1,) + (n,) * dim)  # [c][z][y][x]
+        subs = []
+        rng = range(k)
+        if dim == 3:
+            for a in rng:            # sub-cell z
+                for b in rng:        # y
+                    for c in rng:    # x
+                        corners = [cn[:, a + l, b + j, c + i] for l in (0, 1) for j in (0, 1)
+                                   for i in (0, 1)]
+                        subs.append(np.stack(corners, axis=1))
+        else:
+            for b in rng:
+                for c in rng:
+                    corners = [cn[:, b + j, c + i] for j in (0, 1) for i in (0, 1)]
+                    subs.append(np.stack(corners, axis=1))
+        # [coarse cell][sub-cell lexicographic][2^dim]
+        self.cell_nodes = np.ascontiguousarray(np.stack(subs, axis=1).reshape(-1, 2 ** dim),
+                                               dtype=np.uint32)
+        self.n_cells = self.cell_nodes.shape[0]
+        self.n_sub = k ** dim
+
+    @property
+    def n_dofs(self):
+        return self.n_nodes * (self.dim + 1)
+
+    def brick(self):
+        return (self.k, self.k, self.k if self.dim == 3 else 1)
+
+    def cell_measure(self):
+        meas, hmin = self.base.cell_measure()
+        return (np.repeat(np.asarray(meas) / self.n_sub, self.n_sub),
+                np.repeat(np.asarray(hmin), self.n_sub))
+
+    def constraint_mask(self, *a, **kw):
+        return self.base.constraint_mask(*a, **kw)
+
+    def child_lattice(self, fine):
+        """Per sub-cell, the 3^dim next-level nodes of its child (the
+        sub-block of the coarse cell's (2k+1)^dim child lattice)."""
+        k, dim = self.k, self.dim
+        L = 2 * k + 1
+        ch = np.asarray(self.base.child_lattice(fine), dtype=np.int64).reshape((-1,) + (L,) * dim)
+        out = []
+        if dim == 3:
+            for a in range(k):
+                for b in range(k):
+                    for c in range(k):
+                        out.append(ch[:, 2 * a:2 * a + 3, 2 * b:2 * b + 3, 2 * c:2 * c + 3]
+                                   .reshape(ch.shape[0], -1))
+        else:
+            for b in range(k):
+                for c in range(k):
+                    out.append(ch[:, 2 * b:2 * b + 3, 2 * c:2 * c + 3].reshape(ch.shape[0], -1))
+        return np.ascontiguousarray(np.stack(out, axis=1).reshape(-1, 3 ** dim), dtype=np.uint32)

@@ -860,7 +860,7 @@ lattice_prolongation_1d(int k, double P[2 * MAXK + 1][MAXN])
 static double *
 fine_weights(const orc_mesh *coarse, const orc_mesh *fine, const uint32_t *child)
 {
-  const int dim = fine->dim, k = fine->degree, nc = dim + 1;
+  const int dim = fine->dim, k = coarse->degree, nc = dim + 1;
   const int L = 2 * k + 1, nl = dim == 3 ? L * L * L : L * L;
   double   *val = (double *)calloc((size_t)fine->n_nodes, sizeof(double));
   for (int64_t c = 0; c < coarse->n_cells; ++c)
@@ -878,7 +878,9 @@ void
 orc_prolongate_add(const orc_mesh *coarse, const orc_mesh *fine,
                    const uint32_t *child, double *dst_f, const double *src_c)
 {
-  const int dim = fine->dim, k = fine->degree, nc = dim + 1, n = k + 1;
+  /* the coarse level's degree (FE_Q_iso_Q1 coarse levels are Q1 on the
+     sub-cells below a Q_k level, main.cc:436-446) */
+  const int dim = fine->dim, k = coarse->degree, nc = dim + 1, n = k + 1;
   const int L = 2 * k + 1, nl = dim == 3 ? L * L * L : L * L;
   const int nloc = dim == 3 ? n * n * n : n * n;
   double    P[2 * MAXK + 1][MAXN];
@@ -913,7 +915,9 @@ void
 orc_restrict_add(const orc_mesh *coarse, const orc_mesh *fine,
                  const uint32_t *child, double *dst_c, const double *src_f)
 {
-  const int dim = fine->dim, k = fine->degree, nc = dim + 1, n = k + 1;
+  /* the coarse level's degree (FE_Q_iso_Q1 coarse levels are Q1 on the
+     sub-cells below a Q_k level, main.cc:436-446) */
+  const int dim = fine->dim, k = coarse->degree, nc = dim + 1, n = k + 1;
   const int L = 2 * k + 1, nl = dim == 3 ? L * L * L : L * L;
   const int nloc = dim == 3 ? n * n * n : n * n;
   double    P[2 * MAXK + 1][MAXN];
@@ -950,7 +954,9 @@ void
 orc_interpolate(const orc_mesh *coarse, const orc_mesh *fine,
                 const uint32_t *child, double *dst_c, const double *src_f)
 {
-  const int dim = fine->dim, k = fine->degree, nc = dim + 1, n = k + 1;
+  /* the coarse level's degree (FE_Q_iso_Q1 coarse levels are Q1 on the
+     sub-cells below a Q_k level, main.cc:436-446) */
+  const int dim = fine->dim, k = coarse->degree, nc = dim + 1, n = k + 1;
   const int L = 2 * k + 1, nl = dim == 3 ? L * L * L : L * L;
   const int nloc = dim == 3 ? n * n * n : n * n;
   (void)nl;

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 mkdir -p dealii-ns-gls_amd/lib/var
 rm -f dealii-ns-gls_amd/lib/var/*.so
 HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -Wno-unused-parameter -Wno-unused-function"
-SRC="$(ls dealii-ns-gls_amd/csrc/*.hip)"
+SRC="$(ls dealii-ns-gls_amd/csrc/*.hip dealii-ns-gls_amd/csrc/*.cc)"
 LIBS="-L/opt/rocm/lib -lrocsolver -lrocblas -lrccl -Wl,-rpath,/opt/rocm/lib"
 while read -r name flags; do
   [ -z "$name" ] && continue
