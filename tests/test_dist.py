@@ -91,7 +91,7 @@ def _gloo_worker(rank, world, port, name, n_ref, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,n_ref", CASES)
+@pytest.mark.parametrize("name,n_ref", CASES + [("input_sphere_amg.json", 1)])
 def test_gloo_world2(name, n_ref):
     import socket
     import torch.multiprocessing as mp
@@ -176,3 +176,20 @@ def test_rccl_world1_native():
         assert rel_err(dst.cpu().numpy(), _oracle_ref(c)) < 1e-12
     finally:
         dist.destroy_process_group()
+
+
+def test_sphere_r3_partition_balance():
+    """BASELINE's sphere configuration (input_sphere_amg.json r3, 524,288
+    unstructured cells, "load balance at 8 GPUs"): the 8-rank partition gives
+    every rank the same cells, owned nodes within 5 % of the mean, ghosts
+    below 10 % of the owned nodes and at most two peers per rank."""
+    from helpers import deck
+    m = deck("input_sphere_amg.json").mesh(3)
+    parts = glsdist.build_partitions(m, 8)
+    cells = [p.cell_end - p.cell_begin for p in parts]
+    owned = np.array([p.n_owned for p in parts])
+    ghost = np.array([p.n_nodes - p.n_owned for p in parts])
+    assert len(set(cells)) == 1 and sum(cells) == m.n_cells
+    assert np.abs(owned / owned.mean() - 1).max() < 0.05
+    assert (ghost < 0.10 * owned).all()
+    assert max(len(p.recv_nodes) for p in parts) <= 2
