@@ -301,6 +301,45 @@ def mg_companions(d, params, weights, n_ref, reps=20):
                                                   "Hessenberg step, wall clock"}}
 
 
+def dist_size_companion(d, params, weights, n_ref, dist, rank, world, reps=30):
+    """Multi-GPU beside the strong-scaled headline: the same deck one
+    refinement finer (r{n_ref+1}, 8x the cells: the HBM-bound size where the
+    halo exchange no longer dominates), partitioned the same
+    way, FP64 vmult over RCCL; barrier-bracketed wall time per vmult, max
+    over ranks.  B_tab per vmult over the aggregate HBM peak of the ranks."""
+    import torch
+    import glsdist
+    m = d.mesh(n_ref + 1)
+    vel, p, slip = d.boundary_descriptor()
+    cm = m.constraint_mask(vel, p, slip)
+    u = gi.linearization_point(m.n_nodes, m.dim, d.u_max)
+    hist = gi.history(u, params["order"])
+    A = glsdist.DistributedOperator(m, cm, "f64", dist, rank, world)
+    A.setup(params, u, hist, weights)
+    src = A.scatter_global(gi.src_vector(m.n_dofs))
+    dst = A.new_vector()
+    for _ in range(3):
+        A.vmult(dst, src)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        A.vmult(dst, src)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = float(t.item()) / reps * 1e3
+    b = torch.tensor([A.op.vmult_bytes()], dtype=torch.float64, device="cuda")
+    dist.all_reduce(b)  # the ranks' local algorithmic bytes (ghost cells counted once each)
+    return {f"r{n_ref + 1}_f64_dist": {
+        "ms": ms, "dofs": m.n_dofs, "cells": m.n_cells, "dofs_per_s": m.n_dofs / (ms * 1e-3),
+        "n_gpus": world, "algorithmic_bytes_all_ranks": float(b.item()),
+        "roofline_frac_aggregate": float(b.item()) / (ms * 1e-3) / (HBM_PEAK * world),
+        "note": "DistributedOperator (native RCCL halo import overlapped with interior bricks, "
+                "export-add), wall clock max over ranks"}}
+
+
 def dist_gmres_companion(d, params, weights, n_ref, dist, rank, world, reps=10):
     """The whole GMRES iteration on N GPUs: the partitioned
     multigrid (glsdist.DistributedMultigrid: FP32 levels on the same
@@ -521,9 +560,13 @@ def main():
         kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
 
     dist_comp = None
+    if use_dist and not args.no_companions:
+        dist_comp = dist_size_companion(d, params, weights, n_ref, dist, rank, world)
+        log(f"[bench] distributed r{n_ref + 1}: {dist_comp}")
     if use_dist and args.gmres_iteration:
-        dist_comp = dist_gmres_companion(d, params, weights, n_ref, dist, rank, world)
-        log(f"[bench] distributed GMRES iteration: {dist_comp}")
+        g = dist_gmres_companion(d, params, weights, n_ref, dist, rank, world)
+        dist_comp = dict(dist_comp or {}, **g)
+        log(f"[bench] distributed GMRES iteration: {g}")
     bytes_per_vmult = op.vmult_bytes()
     n_gen, n_cart = op.geometry_counts()
     # parity of the timed result: the headline dst (FP64) against the oracle
