@@ -620,18 +620,25 @@ class DistributedMultigrid:
         con = D.r.con_owned
         xo[con] = 0.0
         x[:D.r.n_owned_dofs] = xo.to(x.dtype)
-        nx = self.dot(l, x, x) ** 0.5
-        x *= 1.0 / nx
+
+        # dots all-reduced on the device: no host round trip inside the
+        # iteration, the estimate is read once at the end
+        def ddot(a, b):
+            t = torch.dot(self._owned(l, a).double(), self._owned(l, b).double()).reshape(1)
+            return self._allreduce(t)
+
+        x *= (1.0 / ddot(x, x).sqrt()).to(x.dtype)
         y = D.new_vector()
-        lam = 0.0
+        lam = torch.zeros(1, dtype=torch.float64, device=x.device)
         d = self.invdiag[l]
         for _ in range(self.n_eig):
             D.vmult(y, x)
             y *= d
-            lam = self.dot(l, x, y)
-            ny = self.dot(l, y, y) ** 0.5
-            x.copy_(y * (1.0 / ny if ny > 0 else 0.0))
-        return abs(lam)
+            lam = ddot(x, y)
+            ny = ddot(y, y).sqrt()
+            inv = torch.where(ny > 0, 1.0 / ny, torch.zeros_like(ny))
+            x.copy_(y * inv.to(y.dtype))
+        return abs(float(lam[0]))
 
     # ---- V-cycle (Multigrid::level_v_step)
     def relax(self, l, x, b, ax, zero):
@@ -734,8 +741,11 @@ def gmres_solve(apply_A, apply_P, b, x, n_owned, allreduce, max_n_tmp_vectors=30
                 h = ared(V[:j + 1, :n_owned].double() @ w[:n_owned].double())
                 w.sub_((h.to(w.dtype) @ V[:j + 1]))
                 hj += h
-            hn = nrm(w)
-            H[:j + 1, j] = hj.cpu().numpy()
+            # the Hessenberg column and the new norm cross to the host together
+            hn2 = ared((w[:n_owned].double() ** 2).sum().reshape(1))
+            col = torch.cat([hj, hn2]).cpu().numpy()
+            hn = float(col[j + 1]) ** 0.5
+            H[:j + 1, j] = col[:j + 1]
             H[j + 1, j] = hn
             if hn > 0:
                 V[j + 1].copy_(w * (1.0 / hn))
