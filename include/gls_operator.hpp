@@ -235,7 +235,41 @@ public:
     check(gls_mg_interpolate(h, level, dst_coarse, src_fine, stream), "gls_mg_interpolate");
   }
 
+  glsMG handle() const { return h; }
+
 private:
   glsMG h = nullptr;
+};
+
+// LinearSolverGMRES (solver_l.h:60-82, solver_l.cc:26-74): right-
+// preconditioned restarted GMRES on the device (gls_gmres_solve), the
+// preconditioner a Multigrid (PreconditionerGMG::vmult, one V-cycle) or none;
+// vectors in the operator's layout.  solve() throws gls::Error on no
+// convergence (SolverControl::NoConvergence); last() holds the statistics.
+class LinearSolverGMRES
+{
+public:
+  LinearSolverGMRES(const Operator &op, const Multigrid *preconditioner = nullptr,
+                    int n_max_iterations = 10000, double absolute_tolerance = 1e-12,
+                    double relative_tolerance = 1e-8, int max_n_tmp_vectors = 30)
+    : op(op), mg(preconditioner),
+      desc{max_n_tmp_vectors, n_max_iterations, absolute_tolerance, relative_tolerance}
+  {}
+
+  void
+  solve(void *dst, const void *src, void *stream = nullptr)
+  {
+    check(gls_gmres_solve(op.handle(), mg ? mg->handle() : nullptr, &desc, dst, src, &res,
+                          stream),
+          "gls_gmres_solve");
+  }
+
+  const glsGMRESResult &last() const { return res; }
+
+private:
+  const Operator   &op;
+  const Multigrid  *mg;
+  glsGMRESDesc      desc;
+  glsGMRESResult    res{};
 };
 } // namespace gls
