@@ -488,8 +488,18 @@ class DistributedMultigrid:
 
     def __init__(self, meshes, cmasks, precision, dist, rank, world, engine="gpu",
                  transfers=None, n_smooth=5, n_eig=20, smoothing_range=20.0,
-                 coarse_n_iterations=10, compute_evs_n_levels=0, native=None):
+                 coarse_n_iterations=10, compute_evs_n_levels=0, native=None,
+                 coarse_solver=None):
         self.dist, self.rank, self.world = dist, rank, world
+        # coarse_n_iterations < 0: the deck's direct coarse solver, redundant
+        # on every rank (the coarse right-hand side all-gathered, SURVEY
+        # §8e "the coarse level is gathered for the direct solve"):
+        # coarse_solver (a factory taking the level-0 mesh, cmask, precision)
+        # or RedundantCoarseLU
+        self._coarse_direct = coarse_n_iterations < 0
+        if self._coarse_direct:
+            make = coarse_solver or RedundantCoarseLU
+            self.coarse = make(meshes[0], cmasks[0], precision)
         self.n_smooth, self.n_eig, self.range = n_smooth, n_eig, smoothing_range
         self.coarse_iters, self.evs_levels = coarse_n_iterations, compute_evs_n_levels
         n0 = meshes[0].n_cells
@@ -584,6 +594,7 @@ class DistributedMultigrid:
                     t = self.new_vector(l - 1)
                     self.interpolate(l, t, h)
                     hs[l - 1].append(t)
+        self._lin0 = (params, us[0], hs[0], weights)
         for l, D in enumerate(self.levels):
             D.update_ghost_values(us[l])
             D.r.eng.set_parameters(**params)
@@ -607,6 +618,11 @@ class DistributedMultigrid:
             self.lam[l] = ev
             alpha = ev / self.range if self.range > 1 else 0.9 * ev
             self.omega[l] = 2.0 / (alpha + ev) if ev > 0 else 1.0
+        if self._coarse_direct:
+            params, u0, h0, w = self._lin0
+            D0 = self.levels[0]
+            g = lambda v: D0.gather_global(v.to(D0.r.dtype))  # noqa: E731
+            self.coarse.setup(params, g(u0), None if h0 is None else [g(h) for h in h0], w)
 
     def power_iteration(self, l):
         """deal.II power_iteration with set_initial_guess on the global dof
@@ -664,7 +680,11 @@ class DistributedMultigrid:
 
     def v_step(self, l, x, b):
         if l == 0:
-            if self.coarse_iters > 0:
+            if self._coarse_direct:
+                D0 = self.levels[0]
+                xg = self.coarse.solve(D0.gather_global(b))
+                x.copy_(D0.scatter_global(xg).to(x.dtype))
+            elif self.coarse_iters > 0:
                 self.smooth(0, x, b, True, self.coarse_iters)
             else:
                 x.copy_(b)
@@ -693,6 +713,39 @@ class DistributedMultigrid:
         self.v_step(L, x, b)
         dst.copy_(x.to(dst.dtype))
         return dst
+
+
+class RedundantCoarseLU:
+    """The deck's direct coarse solver for a partitioned hierarchy
+    (multigrid.cc:448-455, 477-481): every rank holds the whole coarse level
+    (400 cells at Re3900) as a single-domain operator and its dense LU
+    (gls_mg with coarse_n_iterations = -1: rocSOLVER getrf + the inverse
+    GEMV); the coarse right-hand side arrives all-gathered, the solution is
+    sliced back to the rank's [owned | ghost] entries by the caller."""
+
+    def __init__(self, mesh, cmask, precision):
+        import glsamd
+        self.op = glsamd.NavierStokesOperator(mesh, cmask, precision)
+        self.mg = None
+        self.precision = precision
+
+    def setup(self, params, u, hist, weights):
+        import glsamd
+        import torch
+        self.op.set_parameters(**params)
+        self.op.set_linearization_point(u.to(self.op.dtype))
+        if hist is not None and params.get("order", 0) > 0:
+            self.op.set_previous_solution([h.to(self.op.dtype) for h in hist], weights)
+        self.mg = glsamd.Multigrid([self.op], [], coarse_n_iterations=-1,
+                                   outer_precision=self.precision)
+        self.mg.setup()
+        torch.cuda.synchronize()
+
+    def solve(self, b):
+        import torch
+        x = torch.zeros_like(b)
+        self.mg.vcycle(x, b)
+        return x
 
 
 def gmres_solve(apply_A, apply_P, b, x, n_owned, allreduce, max_n_tmp_vectors=30,

@@ -129,3 +129,32 @@ class OracleTransfers:
         for comp in range(nc):
             out[cn * nc + comp] = src[f * nc + comp]
 
+
+
+class OracleCoarseDirect:
+    """Test twin of glsdist.RedundantCoarseLU: the whole coarse level on the
+    oracle, its matrix assembled from unit vectors, dense solve (numpy)."""
+
+    def __init__(self, mesh, cmask, precision):
+        import oracle as orc
+        self.om = orc.OracleMesh(mesh, cmask)
+        self.A = None
+
+    def setup(self, params, u, hist, weights):
+        import oracle as orc
+        o = orc.Oracle(self.om, **params)
+        o.set_linearization_point(u.double().numpy())
+        if hist is not None and params.get("order", 0) > 0:
+            o.set_previous_solution([h.double().numpy() for h in hist], weights)
+        n = self.om.n_dofs
+        A = np.empty((n, n))
+        e = np.zeros(n)
+        for j in range(n):
+            e[j] = 1.0
+            A[:, j] = o.vmult(e)
+            e[j] = 0.0
+        self.A = A
+
+    def solve(self, b):
+        import torch
+        return torch.from_numpy(np.linalg.solve(self.A, b.double().numpy())).to(b.dtype)

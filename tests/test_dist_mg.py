@@ -191,3 +191,98 @@ def test_rccl_world1_multigrid_gmres():
         assert rel_err(A.gather_global(x).cpu().numpy(), xd.cpu().numpy()) < 1e-4
     finally:
         dist.destroy_process_group()
+
+
+def _worker_direct(rank, world, port, name, n_ref, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "dealii-ns-gls_amd", "python"), os.path.join(root, "oracle"),
+              os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    import glsdist as gd
+    from dist_engines import OracleCoarseDirect, OracleEngine, OracleTransfers
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        meshes, cm, params, w, u, hist, b = _hierarchy(name, n_ref)
+        dmg = gd.DistributedMultigrid(meshes, cm, "f64", dist, rank, world, engine=OracleEngine,
+                                      transfers=lambda m: OracleTransfers(m, meshes),
+                                      coarse_n_iterations=-1, coarse_solver=OracleCoarseDirect)
+        top = dmg.levels[-1]
+        dmg.set_linearization_point(params, top.scatter_global(u),
+                                    [top.scatter_global(h) for h in hist], w)
+        dmg.setup()
+        xl = top.new_vector()
+        dmg.vmult(xl, top.scatter_global(b))
+        vc = top.gather_global(xl).numpy()
+        if rank == 0:
+            q.put((list(dmg.omega), vc))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_vcycle_direct_coarse():
+    """The deck's direct coarse solver on a partitioned hierarchy: the coarse
+    right-hand side all-gathered, solved redundantly on every rank
+    (glsdist.RedundantCoarseLU on the GPU; the oracle's dense solve here)."""
+    import socket
+    import torch.multiprocessing as mp
+    from mg_ref import OracleGMG
+    name, n_ref = "input_turek_2D_Re100.json", 1
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_direct, args=(r, 2, port, name, n_ref, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    meshes, cm, params, w, u, hist, b = _hierarchy(name, n_ref)
+    ref = OracleGMG(meshes, cm, params, u, hist, w, coarse_iters=-1)
+    ref.setup_omega()
+    vc_ref = ref.vcycle(b)
+    omega, vc = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert abs(omega[1] - ref.omega[1]) < 1e-10 * ref.omega[1]
+    assert rel_err(vc, vc_ref) < 1e-10
+
+
+@pytest.mark.gpu
+def test_rccl_world1_direct_coarse():
+    """The partitioned multigrid with the deck's direct coarse solver
+    (glsdist.RedundantCoarseLU: the coarse level and its dense LU on every
+    rank) at world 1 over RCCL, against the single-domain GPU multigrid with
+    the same coarse solver."""
+    import torch
+    import torch.distributed as dist
+    import glsamd
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        meshes, cm, params, w, u, hist, b = _hierarchy(*CASE)
+        dmg = glsdist.DistributedMultigrid(meshes, cm, "f32", dist, 0, 1, coarse_n_iterations=-1)
+        top = dmg.levels[-1]
+        dmg.set_linearization_point(params, top.scatter_global(u),
+                                    [top.scatter_global(h) for h in hist], w)
+        dmg.setup()
+        mg, ops = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f32",
+                                   coarse_n_iterations=-1)
+        bd = torch.from_numpy(b).cuda()
+        x1 = torch.zeros_like(bd)
+        dmg.vmult(x1, top.scatter_global(b).double())
+        x2 = torch.zeros_like(bd)
+        mg.vcycle(x2, bd)
+        torch.cuda.synchronize()
+        assert rel_err(top.gather_global(x1).cpu().numpy(), x2.cpu().numpy()) < 1e-3
+    finally:
+        dist.destroy_process_group()
