@@ -562,7 +562,11 @@ def main():
 
     dist_comp = None
     if use_dist and not args.no_companions:
-        dist_comp = dist_size_companion(d, params, weights, n_ref, dist, rank, world)
+        try:  # reported beside the headline, never fatal (failures are symmetric: same
+            # mesh and code on every rank)
+            dist_comp = dist_size_companion(d, params, weights, n_ref, dist, rank, world)
+        except Exception as e:
+            dist_comp = {f"r{n_ref + 1}_f64_dist": {"error": str(e)}}
         log(f"[bench] distributed r{n_ref + 1}: {dist_comp}")
     if use_dist and args.gmres_iteration:
         g = dist_gmres_companion(d, params, weights, n_ref, dist, rank, world)
