@@ -557,8 +557,30 @@ struct Impl
     a.have_prev     = op->have_prev ? 1 : 0;
     a.have_old_grad = (op->have_old_grad && op->prm.theta != 1.0) ? 1 : 0;
     a.diag_ndof     = nq * (dim + 1);
+    a.emat          = nullptr;
     a.sh            = make_shape<T, n>(op->basis);
     return a;
+  }
+
+  // element matrices of cells [b, e) into out (device, op precision), one
+  // unit-vector cell apply per (cell, local dof) (k_apply<DIAG> with emat)
+  static void
+  element_matrices(const glsOp_ *op, int mode, void *out, int64_t b, int64_t e, hipStream_t s)
+  {
+    if (e <= b)
+      return;
+    auto a       = args(op);
+    a.emat       = (T *)out;
+    a.cell_begin = b;
+    a.cell_end   = e;
+    constexpr int CPB = (64 / nq > 0 ? 64 / nq : 1) * (BLOCK / 64);
+    const int64_t nv  = (e - b) * (int64_t)nq * (dim + 1);
+    const dim3    grid((unsigned)((nv + CPB - 1) / CPB));
+    if (mode == MODE_NEWTON)
+      hipLaunchKernelGGL((k_apply<dim, k, T, MODE_NEWTON, true>), grid, dim3(BLOCK), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_apply<dim, k, T, MODE_FIXED, true>), grid, dim3(BLOCK), 0, s, a);
+    HIP_THROW(hipGetLastError());
   }
 
   static void
@@ -802,6 +824,24 @@ select_diag_t(int dim, int k)
   return nullptr;
 }
 using ProduceFn = void (*)(const glsOp_ *, int, const void *, hipStream_t);
+using EmatFn    = void (*)(const glsOp_ *, int, void *, int64_t, int64_t, hipStream_t);
+
+template <typename T>
+EmatFn
+select_emat_t(int dim, int k)
+{
+#define GLS_CASE(D, K)     \
+  if (dim == D && k == K)  \
+    return &Impl<D, K, T>::element_matrices;
+  GLS_CASE(2, 1)
+  GLS_CASE(2, 2)
+  GLS_CASE(2, 3)
+  GLS_CASE(3, 1)
+  GLS_CASE(3, 2)
+  GLS_CASE(3, 3)
+#undef GLS_CASE
+  return nullptr;
+}
 
 template <typename T>
 void
@@ -2048,6 +2088,152 @@ gls_discover_bricks(int dim, int degree, int64_t n_cells, const uint32_t *cell_n
       for (int a = 0; a < 3; ++a)
         shape[a] = plan.shape[a];
       std::copy(plan.perm.begin(), plan.perm.end(), perm);
+    }
+  GLS_CATCH
+}
+
+// element matrices of every cell, FP64 host [cell][col j][row i], i, j =
+// local dofs p * (dim + 1) + component (the caller's cell order); computed
+// on the device in chunks of cells
+static void
+element_matrices_host(glsOp op, double *out)
+{
+  const int     ndof  = op->nq * (op->dim + 1);
+  const size_t  per   = (size_t)ndof * ndof;
+  const int64_t chunk = std::max<int64_t>(1, (int64_t)((256u << 20) / (per * op->tsize())));
+  EmatFn        fn    = op->prec == GLS_F64 ? select_emat_t<double>(op->dim, op->degree) :
+                                              select_emat_t<float>(op->dim, op->degree);
+  if (!fn)
+    throw std::runtime_error("no kernel instantiation for this (dim, degree)");
+  void *buf = nullptr;
+  HIP_THROW(hipMalloc(&buf, (size_t)std::min(chunk, op->n_cells) * per * op->tsize()));
+  std::vector<double> tmp;
+  std::vector<float>  tmpf;
+  try
+    {
+      for (int64_t b = 0; b < op->n_cells; b += chunk)
+        {
+          const int64_t e = std::min(op->n_cells, b + chunk);
+          fn(op, op_vmult_mode(op), buf, b, e, nullptr);
+          const size_t cnt = (size_t)(e - b) * per;
+          if (op->prec == GLS_F64)
+            {
+              tmp.resize(cnt);
+              HIP_THROW(hipMemcpy(tmp.data(), buf, cnt * 8, hipMemcpyDeviceToHost));
+            }
+          else
+            {
+              tmpf.resize(cnt);
+              HIP_THROW(hipMemcpy(tmpf.data(), buf, cnt * 4, hipMemcpyDeviceToHost));
+              tmp.assign(tmpf.begin(), tmpf.end());
+            }
+          for (int64_t c = b; c < e; ++c)
+            std::copy(tmp.begin() + (size_t)(c - b) * per, tmp.begin() + (size_t)(c - b + 1) * per,
+                      out + (size_t)ext_cell(op, c) * per);
+        }
+    }
+  catch (...)
+    {
+      (void)hipFree(buf);
+      throw;
+    }
+  HIP_THROW(hipFree(buf));
+}
+
+glsStatus
+gls_op_element_matrices(glsOp op, double *out)
+{
+  GLS_TRY
+  if (!op || !out)
+    throw std::runtime_error("gls_op_element_matrices: null argument");
+  if (!op->have_lin)
+    throw std::runtime_error("gls_op_element_matrices before set_linearization_point");
+  element_matrices_host(op, out);
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_system_matrix(glsOp op, int64_t *nnz, int64_t *row_ptr, int64_t *cols, double *vals)
+{
+  GLS_TRY
+  if (!op || !nnz)
+    throw std::runtime_error("gls_op_system_matrix: null argument");
+  if (op->n_owned_nodes != op->n_nodes)
+    throw std::runtime_error("gls_op_system_matrix: single-domain operators only");
+  const int     nc = op->dim + 1, nq = op->nq, ndof = nq * nc;
+  const int64_t N  = op->n_dofs;
+  // sparsity: the node couplings of the cells, every component pair; rows
+  // and columns of constrained dofs hold only their unit diagonal (the
+  // identity rows of vmult, operator_ns.cc:719-721)
+  std::vector<std::vector<uint32_t>> adj((size_t)op->n_nodes);
+  for (int64_t c = 0; c < op->n_cells; ++c)
+    for (int i = 0; i < nq; ++i)
+      for (int j = 0; j < nq; ++j)
+        adj[op->h_cell_nodes[(size_t)c * nq + i]].push_back(op->h_cell_nodes[(size_t)c * nq + j]);
+  for (auto &a : adj)
+    {
+      std::sort(a.begin(), a.end());
+      a.erase(std::unique(a.begin(), a.end()), a.end());
+    }
+  auto constrained = [&](int64_t dof) { return (op->h_cmask[dof / nc] >> (dof % nc)) & 1; };
+  std::vector<int64_t> rp((size_t)N + 1, 0);
+  for (int64_t r = 0; r < N; ++r)
+    {
+      int64_t cnt = 0;
+      if (constrained(r))
+        cnt = 1;
+      else
+        for (uint32_t m : adj[(size_t)(r / nc)])
+          for (int cc = 0; cc < nc; ++cc)
+            cnt += constrained((int64_t)m * nc + cc) ? 0 : 1;
+      rp[(size_t)r + 1] = rp[(size_t)r] + cnt;
+    }
+  *nnz = rp.back();
+  if (!row_ptr)
+    return 0; // sizing call
+  if (!cols || !vals)
+    throw std::runtime_error("gls_op_system_matrix: null output arrays");
+  std::copy(rp.begin(), rp.end(), row_ptr);
+  for (int64_t r = 0; r < N; ++r)
+    {
+      int64_t k = rp[(size_t)r];
+      if (constrained(r))
+        {
+          cols[k] = r;
+          vals[k] = 1.0;
+          continue;
+        }
+      for (uint32_t m : adj[(size_t)(r / nc)])
+        for (int cc = 0; cc < nc; ++cc)
+          {
+            const int64_t col = (int64_t)m * nc + cc;
+            if (constrained(col))
+              continue;
+            cols[k]   = col;
+            vals[k++] = 0.0;
+          }
+    }
+  std::vector<double> E((size_t)op->n_cells * ndof * ndof);
+  element_matrices_host(op, E.data());
+  for (int64_t c = 0; c < op->n_cells; ++c)
+    {
+      const uint32_t *cn = &op->h_cell_nodes[(size_t)c * nq];
+      const double   *Ec = &E[(size_t)c * ndof * ndof];
+      for (int i = 0; i < ndof; ++i)
+        {
+          const int64_t r = (int64_t)cn[i / nc] * nc + i % nc;
+          if (constrained(r))
+            continue;
+          const int64_t *cb = cols + rp[(size_t)r], *ce = cols + rp[(size_t)r + 1];
+          for (int j = 0; j < ndof; ++j)
+            {
+              const int64_t col = (int64_t)cn[j / nc] * nc + j % nc;
+              if (constrained(col))
+                continue;
+              const int64_t *it = std::lower_bound(cb, ce, col);
+              vals[it - cols] += Ec[(size_t)j * ndof + i];
+            }
+        }
     }
   GLS_CATCH
 }

@@ -122,6 +122,10 @@ struct ApplyArgs
   T               nu, w0, theta;
   int             td, cw, have_prev, have_old_grad;
   int             diag_ndof;
+  // DIAG with emat set: the whole column j of the element matrix instead of
+  // its diagonal entry (MatrixFreeTools::compute_matrix, operator_ns.cc:
+  // 1407-1430): emat[((cell - cell_begin) * ndof + j) * ndof + p * nc + c]
+  T              *emat;
   Shape<T, n>     sh;
 };
 
@@ -789,7 +793,14 @@ __global__ void __launch_bounds__(BLOCK)
   // ---- scatter (distribute_local_to_global, constrained dofs skipped)
   if (!active)
     return;
-  if (DIAG)
+  if (DIAG && a.emat)
+    {
+      T *col = a.emat + ((size_t)(cell - a.cell_begin) * a.diag_ndof + jdiag) * a.diag_ndof;
+#pragma unroll
+      for (int c = 0; c < nc; ++c)
+        col[p * nc + c] = in[c * nq + p];
+    }
+  else if (DIAG)
     {
       const int c = jdiag % nc;
       if (p == jdiag / nc && !((cm >> c) & 1))

@@ -36,7 +36,8 @@ EXPORTS = [
     "gls_op_get_max_u", "gls_mg_set_vector_layout", "gls_dist_update_ghost_values",
     "gls_dist_get_max_u", "gls_op_compute_diagonal", "gls_op_invert_diagonal", "gls_mg_relax",
     "gls_dist_compress_add", "gls_op_brick_shape", "gls_op_cell_permutation",
-    "gls_discover_bricks", "gls_mg_coarse_statistics",
+    "gls_discover_bricks", "gls_mg_coarse_statistics", "gls_op_element_matrices",
+    "gls_op_system_matrix",
 ]
 
 GLS_MEM_DEVICE, GLS_MEM_HOST = 0, 1
@@ -144,6 +145,8 @@ def lib():
         L.gls_dist_compress_add.argtypes = [vp, vp, vp]
         L.gls_op_brick_shape.argtypes = [vp, vp]
         L.gls_op_cell_permutation.argtypes = [vp, vp]
+        L.gls_op_element_matrices.argtypes = [vp, vp]
+        L.gls_op_system_matrix.argtypes = [vp, C.POINTER(i64), vp, vp, vp]
         L.gls_mg_coarse_statistics.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.gls_discover_bricks.argtypes = [C.c_int, C.c_int, i64, vp, vp, vp]
         L.gls_last_error.restype = C.c_char_p
@@ -233,6 +236,27 @@ class NavierStokesOperator:
         dims = (C.c_int * 3)()
         _check(lib().gls_op_brick_shape(h, dims))
         self.brick_shape = tuple(dims)  # what runs: (0, 0, 0) = per-cell kernel
+
+    def element_matrices(self):
+        """[cell][row i][col j] element matrices (gls_op_element_matrices;
+        local dof = point * (dim+1) + component)."""
+        nd = (self.degree + 1) ** self.dim * (self.dim + 1)
+        out = np.empty((self.n_cells, nd, nd))
+        _check(lib().gls_op_element_matrices(self.h, out.ctypes.data))
+        return np.ascontiguousarray(out.transpose(0, 2, 1))
+
+    def system_matrix(self):
+        """OperatorBase::get_system_matrix as a scipy CSR matrix over the
+        node-major dofs (gls_op_system_matrix)."""
+        import scipy.sparse as sp
+        nnz = C.c_int64()
+        _check(lib().gls_op_system_matrix(self.h, C.byref(nnz), None, None, None))
+        rp = np.empty(self.n_dofs + 1, dtype=np.int64)
+        cols = np.empty(nnz.value, dtype=np.int64)
+        vals = np.empty(nnz.value)
+        _check(lib().gls_op_system_matrix(self.h, C.byref(nnz), rp.ctypes.data, cols.ctypes.data,
+                                          vals.ctypes.data))
+        return sp.csr_matrix((vals, cols, rp), shape=(self.n_dofs, self.n_dofs))
 
     def cell_permutation(self):
         """perm[internal cell] = caller cell (identity unless bricks were

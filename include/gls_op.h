@@ -230,6 +230,19 @@ glsStatus gls_op_geometry_counts(glsOp op, int64_t *n_general,
 /* algorithmic bytes of one vmult (SURVEY §8d B_tab) */
 double gls_op_vmult_bytes(glsOp op);
 
+/* OperatorBase::get_system_matrix (operator_ns.cc:1407-1430,
+ * MatrixFreeTools::compute_matrix): the element matrices, from one
+ * unit-vector cell apply per (cell, local dof) on the device, FP64 host
+ * [cell][col j][row i] with local dof = point * (dim+1) + component, cells in
+ * the caller's order (n_cells * ((k+1)^dim (dim+1))^2 entries) ... */
+glsStatus gls_op_element_matrices(glsOp op, double *out);
+/* ... and assembled into CSR over the node-major dofs (single domain):
+ * rows / columns of constrained dofs carry only their unit diagonal, as the
+ * identity rows of vmult.  Call with row_ptr = NULL for *nnz first; then
+ * row_ptr [n_dofs + 1], cols / vals [nnz] (columns sorted per row). */
+glsStatus gls_op_system_matrix(glsOp op, int64_t *nnz, int64_t *row_ptr, int64_t *cols,
+                               double *vals);
+
 /* ------------------------------------------------------------ multigrid */
 typedef struct
 {

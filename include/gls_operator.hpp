@@ -174,6 +174,27 @@ public:
 
   double vmult_bytes() const { return gls_op_vmult_bytes(h); }
 
+  // OperatorBase::get_system_matrix (operator_ns.cc:1407-1430) as CSR over
+  // the node-major dofs; constrained rows / columns carry their unit diagonal
+  struct SparseMatrix
+  {
+    std::vector<int64_t> row_ptr, cols;
+    std::vector<double>  vals;
+  };
+  SparseMatrix
+  get_system_matrix() const
+  {
+    SparseMatrix A;
+    int64_t      nnz = 0;
+    check(gls_op_system_matrix(h, &nnz, nullptr, nullptr, nullptr), "get_system_matrix");
+    A.row_ptr.resize((size_t)m() + 1);
+    A.cols.resize((size_t)nnz);
+    A.vals.resize((size_t)nnz);
+    check(gls_op_system_matrix(h, &nnz, A.row_ptr.data(), A.cols.data(), A.vals.data()),
+          "get_system_matrix");
+    return A;
+  }
+
 private:
   glsOp h = nullptr;
 };

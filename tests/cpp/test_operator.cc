@@ -218,6 +218,14 @@ run(int argc, char **argv)
   op.evaluate_residual_plain(dres.p, dsrc.p);
   op.compute_inverse_diagonal(ddiag.p);
   HIPCHK(hipDeviceSynchronize());
+  // get_system_matrix through the facade: CSR x == vmult x
+  std::vector<double> g_spmv(ndof, 0.0);
+  {
+    const auto A = op.get_system_matrix();
+    for (size_t r = 0; r < ndof; ++r)
+      for (int64_t q = A.row_ptr[r]; q < A.row_ptr[r + 1]; ++q)
+        g_spmv[r] += A.vals[(size_t)q] * src[(size_t)A.cols[(size_t)q]];
+  }
   const std::vector<double> g_dst = ddst.down(), g_res = dres.down(), g_diag = ddiag.down();
   for (DevVec *p : dh)
     delete p;
@@ -244,9 +252,11 @@ run(int argc, char **argv)
   orc_compute_inverse_diagonal(o, c_diag.data());
   orc_destroy(o);
 
-  const double e0 = rel_err(g_dst, c_dst), e1 = rel_err(g_res, c_res), e2 = rel_err(g_diag, c_diag);
-  std::printf("cells %lld dofs %zu  vmult %.3e  residual %.3e  inverse_diagonal %.3e\n",
-              (long long)nc, ndof, e0, e1, e2);
+  const double e0 = rel_err(g_dst, c_dst), e1 = rel_err(g_res, c_res), e2 = rel_err(g_diag, c_diag),
+               e8 = rel_err(g_spmv, c_dst);
+  std::printf("cells %lld dofs %zu  vmult %.3e  residual %.3e  inverse_diagonal %.3e  "
+              "system matrix %.3e\n",
+              (long long)nc, ndof, e0, e1, e2, e8);
 
   // ---- the reference's vector layout: host memory (LA::distributed::Vector
   // in host memory, config.h:9-10) in a non-node-major numbering (a
@@ -407,7 +417,7 @@ run(int argc, char **argv)
   // 1/d amplifies the round-off of near-cancelling diagonal entries:
   // 10x the FP64 bound, as tests/test_gpu_parity.py
   return (e0 < 1e-12 && e1 < 1e-12 && e2 < 1e-11 && e3 < 1e-12 && e4 < 1e-12 && e5 < 1e-11 &&
-          e6 < 1e-13 && e7 < 1.05) ?
+          e6 < 1e-13 && e7 < 1.05 && e8 < 1e-12) ?
            0 :
            1;
 }
