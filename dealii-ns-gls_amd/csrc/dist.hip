@@ -317,6 +317,8 @@ gls_dist_create(glsOp op, const glsDistDesc *desc, glsDist *out)
   GLS_TRY
   if (!op || !desc || !out)
     throw std::runtime_error("gls_dist_create: null argument");
+  if (op->faces.n)
+    throw std::runtime_error("gls_dist_create: outflow faces are single-domain only");
   if (desc->world < 1 || desc->rank < 0 || desc->rank >= desc->world)
     throw std::runtime_error("gls_dist_create: bad rank / world");
   HIP_THROW(hipSetDevice(op->device));

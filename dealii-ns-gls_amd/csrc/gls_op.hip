@@ -952,6 +952,7 @@ op_vmult_device(glsOp op, void *dst, const void *src, hipStream_t s)
       init_dst(op, dst, src, s);
       af(op, vmult_mode(op), false, dst, src, 0, op->n_cells, s);
     }
+  faces_apply(op, false, dst, src, s);
 }
 
 // the pieces of vmult dist.hip orchestrates around the ghost exchange
@@ -1515,6 +1516,7 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
   op->prm.nu    = 1.0;
   op->prm.theta = 1.0;
   op->prm.dt    = 1.0;
+  gls::faces_setup(op, caller);
   *out          = op;
   GLS_CATCH
 }
@@ -1535,6 +1537,7 @@ gls_op_destroy(glsOp op)
     if (b)
       (void)hipFree(b);
   op->stage.release();
+  gls::faces_release(op);
   delete op;
 }
 
@@ -1586,7 +1589,9 @@ gls_op_set_linearization_point(glsOp op, const void *vec, void *stream)
   ProduceFn   pf;
   hipStream_t s = (hipStream_t)stream;
   select(op, af, pf);
-  pf(op, 0, op->stage.in_vec(vec, 0, s), s);
+  const void *x = op->stage.in_vec(vec, 0, s);
+  pf(op, 0, x, s);
+  gls::faces_linearization(op, x, s);
   op->stage.done(s);
   op->have_lin = true;
   op->t1_valid = false;
@@ -1687,6 +1692,8 @@ gls_op_vmult_cells(glsOp op, void *dst, const void *src, int64_t b, int64_t e, v
     throw std::runtime_error("vmult before set_linearization_point");
   if (b < 0 || e > op->n_cells || b > e)
     throw std::runtime_error("gls_op_vmult_cells: bad cell range");
+  if (op->faces.n)
+    throw std::runtime_error("gls_op_vmult_cells: operators with outflow faces run gls_op_vmult");
   ApplyFn   af;
   ProduceFn pf;
   select(op, af, pf);
@@ -1796,6 +1803,7 @@ residual_cells(glsOp op, void *dst, const void *src, hipStream_t s)
       HIP_THROW(hipMemsetAsync(dst, 0, (size_t)op->n_dofs * op->tsize(), s));
       af(op, MODE_RESIDUAL, false, dst, src, 0, op->n_cells, s);
     }
+  gls::faces_apply(op, true, dst, src, s);
 }
 
 extern "C" {
@@ -1879,6 +1887,7 @@ gls_op_compute_diagonal(glsOp op, void *diag, void *stream)
   HIP_THROW(hipMemsetAsync(d64, 0, (size_t)op->n_dofs * sizeof(double), s));
   (op->prec == GLS_F64 ? select_diag_t<double>(op->dim, op->degree) :
                          select_diag_t<float>(op->dim, op->degree))(op, vmult_mode(op), d64, s);
+  gls::faces_diagonal(op, d64, true, s);
   if (op->prec == GLS_F64)
     hipLaunchKernelGGL(k_diag_out<double>, grid1d(op->n_dofs), dim3(256), 0, s, (double *)diag,
                        (const double *)d64, op->d_cbits, op->n_owned_dofs, op->n_dofs);
@@ -1945,6 +1954,7 @@ op_inverse_diagonal_device(glsOp op, void *diag, hipStream_t s)
       HIP_THROW(hipMemsetAsync(d64, 0, (size_t)op->n_dofs * sizeof(double), s));
       (op->prec == GLS_F64 ? select_diag_t<double>(op->dim, op->degree) :
                              select_diag_t<float>(op->dim, op->degree))(op, vmult_mode(op), d64, s);
+      faces_diagonal(op, d64, true, s);
       if (op->prec == GLS_F64)
         hipLaunchKernelGGL(k_invert_diag64<double>, grid1d(op->n_dofs), dim3(256), 0, s,
                            (double *)diag, (const double *)d64, op->d_cbits, op->n_owned_dofs,
@@ -1961,6 +1971,7 @@ op_inverse_diagonal_device(glsOp op, void *diag, hipStream_t s)
     }
   HIP_THROW(hipMemsetAsync(diag, 0, (size_t)op->n_dofs * op->tsize(), s));
   af(op, vmult_mode(op), true, diag, diag, 0, op->n_cells, s);
+  faces_diagonal(op, diag, false, s);
   if (op->prec == GLS_F64)
     hipLaunchKernelGGL(k_invert_diag<double>, grid1d(op->n_dofs), dim3(256), 0, s,
                        (double *)diag, op->d_cbits, op->n_owned_dofs, op->n_dofs);
@@ -2115,6 +2126,7 @@ element_matrices_host(glsOp op, double *out)
         {
           const int64_t e = std::min(op->n_cells, b + chunk);
           fn(op, op_vmult_mode(op), buf, b, e, nullptr);
+          faces_element_matrices(op, buf, b, e, nullptr);
           const size_t cnt = (size_t)(e - b) * per;
           if (op->prec == GLS_F64)
             {

@@ -529,7 +529,7 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
   auto  relax = mg->prec == GLS_F64 ? relax_t<double> : relax_t<float>;
   glsOp op    = mg->ops[level];
   void *tmp   = mg->tmp[level];
-  if (!op->use_brick || op->n_owned_dofs != op->n_dofs)
+  if (!gls::fused_relax_ok(op))
     {
       int it = 0;
       if (start_in_tmp)
@@ -927,7 +927,7 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
   smooth(mg, l, mg->sol[l], mg->def[l], true, nit, s);
   // residual t = defect - A solution (fused into the brick vmult's write-out
   // and shared-node reduction for brick operators)
-  if (mg->ops[l]->use_brick && mg->ops[l]->n_owned_dofs == mg->ops[l]->n_dofs)
+  if (gls::fused_relax_ok(mg->ops[l]))
     {
       gls::RelaxStep rs;
       rs.b     = mg->def[l];
@@ -952,8 +952,7 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
   // prolongate and add the coarse correction; with an odd number of fused
   // smoothing steps to follow it goes out of place into tmp, so the
   // ping-pong ends in sol without a copy
-  const bool odd = mg->ops[l]->use_brick && nit % 2 == 1 &&
-                   mg->ops[l]->n_owned_dofs == mg->ops[l]->n_dofs;
+  const bool odd = gls::fused_relax_ok(mg->ops[l]) && nit % 2 == 1;
   if (odd)
     transfer(mg, 0, l, mg->tmp[l], mg->sol[l - 1], s, mg->sol[l]);
   else

@@ -41,6 +41,25 @@ struct VecStage
   void        done(hipStream_t s);
   void        release();
 };
+
+// outflow boundary faces (faces.hip): per face the internal cell, the kind
+// (cut / Nitsche), effective_beta_face and the face geometry at the
+// QGauss(k+1)^(dim-1) points, in the operator's precision
+struct OutflowFaces
+{
+  int64_t             n   = 0;
+  int                 nqf = 0;
+  std::vector<double> h_points; // [n][nqf][dim] face quadrature points
+  int64_t            *d_cell   = nullptr;
+  int32_t            *d_kind   = nullptr;
+  void               *d_beta   = nullptr; // [n]
+  void               *d_jxw    = nullptr; // [n][nqf]
+  void               *d_normal = nullptr; // [n][nqf][dim]
+  void               *d_phi    = nullptr; // [n][nqf][nq] cell basis at the face points
+  void               *d_dn     = nullptr; // [n][nqf][nq] its physical normal derivative
+  void               *d_ustar  = nullptr; // [n][nqf][dim] face_velocity
+  void               *d_target = nullptr; // [n][nqf][dim] face_target_velocity
+};
 } // namespace gls
 
 struct glsOp_
@@ -88,6 +107,7 @@ struct glsOp_
                                     // (values on constrained dofs), or null = all zero
   int       device     = 0;
   gls::VecStage stage; // caller vector layout (host memory / dof permutation)
+  gls::OutflowFaces faces; // weak outflow boundary faces (faces.hip)
   // gls_gmres_solve workspace (Krylov basis and vectors), grown on demand
   void     *gmres_ws       = nullptr;
   size_t    gmres_ws_bytes = 0;
@@ -163,6 +183,21 @@ int  op_vmult_mode(const glsOp_ *op);
 // one V-cycle on node-major device vectors of the multigrid's outer
 // precision (gls_mg_vcycle without the caller-layout staging; GMRES calls it)
 void mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s);
+// outflow boundary-face terms (faces.hip), launched after the cell kernels
+void faces_setup(glsOp_ *op, const glsOpDesc *d);
+void faces_release(glsOp_ *op);
+void faces_linearization(const glsOp_ *op, const void *lin, hipStream_t s);
+void faces_apply(const glsOp_ *op, bool residual, void *dst, const void *src, hipStream_t s);
+void faces_diagonal(const glsOp_ *op, void *diag, bool f64_out, hipStream_t s);
+void faces_element_matrices(const glsOp_ *op, void *emat, int64_t b, int64_t e, hipStream_t s);
+// the brick vmult with the smoother step fused into its write-out needs the
+// whole A x inside the kernel: single domain, no face terms
+inline bool
+fused_relax_ok(const glsOp_ *op)
+{
+  return op->use_brick && op->n_owned_dofs == op->n_dofs && op->faces.n == 0;
+}
+
 // the same operator pieces without staging (GMRES, multigrid)
 void op_vmult_device(glsOp op, void *dst, const void *src, hipStream_t s);
 void op_inverse_diagonal_device(glsOp op, void *diag, hipStream_t s);

@@ -37,7 +37,8 @@ EXPORTS = [
     "gls_dist_get_max_u", "gls_op_compute_diagonal", "gls_op_invert_diagonal", "gls_mg_relax",
     "gls_dist_compress_add", "gls_op_brick_shape", "gls_op_cell_permutation",
     "gls_discover_bricks", "gls_mg_coarse_statistics", "gls_op_element_matrices",
-    "gls_op_system_matrix",
+    "gls_op_system_matrix", "gls_op_n_outflow_faces", "gls_op_outflow_face_points",
+    "gls_op_set_outflow_target",
 ]
 
 GLS_MEM_DEVICE, GLS_MEM_HOST = 0, 1
@@ -48,7 +49,11 @@ class OpDesc(C.Structure):
                 ("n_cells", C.c_int64), ("n_nodes", C.c_int64), ("n_owned_nodes", C.c_int64),
                 ("cell_nodes", C.c_void_p), ("node_coords", C.c_void_p),
                 ("node_cmask", C.c_void_p), ("cell_measure", C.c_void_p),
-                ("cell_hmin", C.c_void_p), ("brick", C.c_int * 3)]
+                ("cell_hmin", C.c_void_p), ("brick", C.c_int * 3),
+                ("n_outflow_faces", C.c_int64), ("outflow_cells", C.c_void_p),
+                ("outflow_face_no", C.c_void_p), ("outflow_kind", C.c_void_p)]
+
+OUTFLOW_KIND = {"cut": 1, "nitsche": 2}
 
 
 class OpParams(C.Structure):
@@ -147,6 +152,9 @@ def lib():
         L.gls_op_cell_permutation.argtypes = [vp, vp]
         L.gls_op_element_matrices.argtypes = [vp, vp]
         L.gls_op_system_matrix.argtypes = [vp, C.POINTER(i64), vp, vp, vp]
+        L.gls_op_n_outflow_faces.argtypes = [vp, C.POINTER(i64), C.POINTER(C.c_int)]
+        L.gls_op_outflow_face_points.argtypes = [vp, vp]
+        L.gls_op_set_outflow_target.argtypes = [vp, vp, vp]
         L.gls_mg_coarse_statistics.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.gls_discover_bricks.argtypes = [C.c_int, C.c_int, i64, vp, vp, vp]
         L.gls_last_error.restype = C.c_char_p
@@ -201,7 +209,7 @@ class NavierStokesOperator:
     (MG levels, MGNumber=float, config.h:6-7)."""
 
     def __init__(self, mesh, cmask, precision="f64", cells=None, n_owned_nodes=None,
-                 brick=None):
+                 brick=None, outflow=None):
         import torch
         if not torch.cuda.is_available():
             raise GlsError("NavierStokesOperator needs a GPU (no CPU fallback by design)")
@@ -229,6 +237,19 @@ class NavierStokesOperator:
                    mesh.n_nodes if n_owned_nodes is None else n_owned_nodes,
                    k[0].ctypes.data, k[1].ctypes.data, k[2].ctypes.data, k[3].ctypes.data,
                    k[4].ctypes.data, (C.c_int * 3)(*self.brick))
+        if outflow is not None:
+            # (cells, face_no, kind): the weak outflow faces (all_outflow_bcs_*,
+            # operator_ns.cc:79-95); kind "cut" / "nitsche" or per face 1 / 2
+            fc, fn, kind = outflow
+            fc = np.ascontiguousarray(fc, dtype=np.int64)
+            fn = np.ascontiguousarray(fn, dtype=np.int32)
+            if isinstance(kind, str):
+                kind = np.full(len(fc), OUTFLOW_KIND[kind], dtype=np.int32)
+            kind = np.ascontiguousarray(kind, dtype=np.int32)
+            self._keep += [fc, fn, kind]
+            d.n_outflow_faces = len(fc)
+            d.outflow_cells, d.outflow_face_no, d.outflow_kind = (
+                fc.ctypes.data, fn.ctypes.data, kind.ctypes.data)
         h = C.c_void_p()
         _check(lib().gls_op_create(C.byref(d), C.byref(h)))
         self.h = h
@@ -236,6 +257,28 @@ class NavierStokesOperator:
         dims = (C.c_int * 3)()
         _check(lib().gls_op_brick_shape(h, dims))
         self.brick_shape = tuple(dims)  # what runs: (0, 0, 0) = per-cell kernel
+
+    @property
+    def n_outflow_faces(self):
+        n, q = C.c_int64(), C.c_int()
+        _check(lib().gls_op_n_outflow_faces(self.h, C.byref(n), C.byref(q)))
+        return n.value, q.value
+
+    def outflow_face_points(self):
+        """[face][point][dim] face quadrature points (gls_op_outflow_face_points)."""
+        n, q = self.n_outflow_faces
+        x = np.empty((n, q, self.dim))
+        _check(lib().gls_op_outflow_face_points(self.h, x.ctypes.data))
+        return x
+
+    def set_outflow_target(self, target, stream=None):
+        """Nitsche target velocity at the face points, [face][point][dim]
+        (face_target_velocity, operator_ns.cc:478-521)."""
+        n, q = self.n_outflow_faces
+        t = np.ascontiguousarray(target, dtype=np.float64)
+        if t.size != n * q * self.dim:
+            raise GlsError("set_outflow_target: expected [faces][points][dim]")
+        _check(lib().gls_op_set_outflow_target(self.h, t.ctypes.data, stream))
 
     def element_matrices(self):
         """[cell][row i][col j] element matrices (gls_op_element_matrices;
@@ -574,19 +617,26 @@ class Multigrid:
 
 
 def build_gmg(meshes, cmasks, params, u_star_fine, history_fine=None, weights=None,
-              precision="f32", coarse_iso_q1=False, **mg_kwargs):
+              precision="f32", coarse_iso_q1=False, outflow=None, **mg_kwargs):
     """Level operators + transfers for a mesh hierarchy (coarse -> fine), the
     linearization point / history interpolated down level by level
     (interpolate_to_mg, main.cc:772-803, 815-832).  coarse_iso_q1: the
     coarsest level with FE_Q_iso_Q1 (glsmesh.IsoQ1Mesh, main.cc:436-446).
-    Returns (mg, level_ops)."""
+    outflow: None, or (kind, boundary id): every level operator gets its
+    mesh's outflow faces (the level operators take the outflow sets too,
+    main.cc:520-527).  Returns (mg, level_ops)."""
     import torch
     if coarse_iso_q1:
         import glsmesh
         meshes = [glsmesh.IsoQ1Mesh(meshes[0])] + list(meshes[1:])
     ops = []
     for m, cm in zip(meshes, cmasks):
-        op = NavierStokesOperator(m, cm, precision)
+        of = None
+        if outflow is not None:
+            import glsmesh
+            fc, fn = glsmesh.boundary_faces(m, outflow[1])
+            of = (fc, fn, outflow[0])
+        op = NavierStokesOperator(m, cm, precision, outflow=of)
         op.set_parameters(**params)
         ops.append(op)
     child = [meshes[l - 1].child_lattice(meshes[l]) for l in range(1, len(meshes))]

@@ -252,6 +252,29 @@ def hypercube(dim, degree, n_ref):
     return Mesh(h.value, "hypercube", dict(dim=dim, degree=degree, n_ref=n_ref))
 
 
+def boundary_faces(mesh, bid):
+    """(cells, face_no) of the cell faces on boundary id `bid`: the faces
+    whose (k+1)^(dim-1) nodes all carry the id (node_boundary bit), numbered
+    as deal.II numbers the faces of a hex / quad, face_no = 2 * axis + side
+    (what a caller collects from cell->face(f)->boundary_id())."""
+    n, k, dim = mesh.degree + 1, mesh.degree, mesh.dim
+    on = ((np.asarray(mesh.node_boundary) >> bid) & 1).astype(bool)
+    cn = np.asarray(mesh.cell_nodes, dtype=np.int64)
+    p = np.arange(n ** dim)
+    ia = [p % n, (p // n) % n, p // (n * n)]
+    cells, faces = [], []
+    for a in range(dim):
+        for side in range(2):
+            sel = ia[a] == side * k
+            hit = np.nonzero(on[cn[:, sel]].all(axis=1))[0]
+            cells.append(hit)
+            faces.append(np.full(len(hit), 2 * a + side))
+    cells = np.concatenate(cells).astype(np.int64)
+    faces = np.concatenate(faces).astype(np.int32)
+    order = np.lexsort((faces, cells))
+    return cells[order], faces[order]
+
+
 # --------------------------------------------------------------------- decks
 # the five input decks of the reference (input/*.json), shipped as package data
 DECK_DIR = os.path.normpath(os.path.join(_HERE, "..", "data", "decks"))
@@ -280,12 +303,59 @@ class Deck:
     cylinder_shift: float = 0.005
     u_max: float = 1.0
     t_init: float = 0.0
+    outflow_bc: object = None  # override of the deck's outflow switches ("" = none)
     raw: dict = field(default_factory=dict)
 
     @property
     def increment_form(self):
         # main.cc:331
         return self.nonlinear_solver == "Newton"
+
+    @property
+    def outflow(self):
+        """The outflow boundary (id 1) treatment of SimulationCylinder
+        (simulation.cc:270-278, 394-403): "cut" (weak, all_outflow_bcs_cut),
+        "nitsche" (weak, all_outflow_bcs_nitsche with the inflow function as
+        target), "strong" (inhomogeneous Dirichlet with the inflow function)
+        or None (homogeneous Neumann: the pressure is constrained).  A
+        dataclass-level override (deck.outflow_bc = ...) wins."""
+        if self.outflow_bc is not None:
+            return self.outflow_bc or None
+        r = self.raw
+        if r.get("simulation use outflow bc weak cut", False):
+            return "cut"
+        if r.get("simulation use outflow bc weak nitsche", False):
+            return "nitsche"
+        if r.get("simulation use outflow bc strong", False):
+            return "strong"
+        return None
+
+    def outflow_faces(self, mesh):
+        """(cells, face_no) of the weak outflow faces (boundary id 1), or None."""
+        if self.simulation != "cylinder" or self.outflow not in ("cut", "nitsche"):
+            return None
+        return boundary_faces(mesh, 1)
+
+    def inflow_velocity(self, points, t=0.0, height=0.41):
+        """InflowBoundaryValues::Channel (simulation.cc:25-76, built at
+        simulation.cc:384-392) at points [..., dim]: velocity [..., dim]
+        (component 0 only).  Also the Nitsche outflow target
+        (simulation.cc:398) and the strong outflow's Dirichlet values."""
+        x = np.asarray(points, dtype=np.float64)
+        factor = np.ones(x.shape[:-1])
+        if self.t_init != 0:  # ramp up
+            factor *= min(t / self.t_init, 1.0)
+        if self.no_slip_wall:  # parabolic profile
+            H = height
+            shift = -H / 2.0 + self.cylinder_shift
+            y = x[..., 1] - shift
+            factor *= 4 * y * (H - y) / H / H
+            if x.shape[-1] == 3:
+                z = x[..., 2] + H / 2.0
+                factor *= 4 * z * (H - z) / H / H
+        v = np.zeros(x.shape)
+        v[..., 0] = self.u_max * factor
+        return v
 
     @property
     def use_fe_q_iso_q1(self):
@@ -306,7 +376,11 @@ class Deck:
         walls = list(range(3, 3 + 2 * self.dim))
         (vel if self.no_slip_wall else slip).extend(walls)
         (vel if self.no_slip_cylinder else slip).append(2)
-        p = [1]  # outflow: homogeneous "NBC" constrains the pressure
+        p = []
+        if self.outflow is None:
+            p = [1]  # outflow: homogeneous "NBC" constrains the pressure
+        elif self.outflow == "strong":
+            vel.append(1)  # inhomogeneous DBC with the inflow function
         return vel, p, slip
 
     def constraint_values(self, mesh, t=0.0):
@@ -323,30 +397,24 @@ class Deck:
         vel, p, slip = self.boundary_descriptor()
         inflow_id = 1 if self.simulation == "sphere" else 0
         full = mesh.constraint_mask(vel, p, slip)
-        copy = mesh.constraint_mask([i for i in vel if i != inflow_id], p, slip)
+        inhom = {inflow_id} | ({1} if self.simulation == "cylinder" and self.outflow == "strong"
+                               else set())
+        copy = mesh.constraint_mask([i for i in vel if i not in inhom], p, slip)
         inflow = ((mesh.node_boundary >> inflow_id) & 1) != 0
         if self.simulation == "sphere":  # Channel(0.0, 1.0): uniform, u_max 1
             g = np.zeros(mesh.n_dofs)
             sel = inflow & ((full & 1) != 0) & ((copy & 1) == 0)
             g[np.nonzero(sel)[0] * (mesh.dim + 1)] = 1.0
             return g
-        x = mesh.coords
-        factor = np.ones(mesh.n_nodes)
-        if self.t_init != 0:  # ramp up
-            factor *= min(t / self.t_init, 1.0)
-        if self.no_slip_wall:  # parabolic profile
-            H = mesh.params["height"]
-            shift = -H / 2.0 + self.cylinder_shift
-            y = x[:, 1] - shift
-            factor *= 4 * y * (H - y) / H / H
-            if mesh.dim == 3:
-                z = x[:, 2] + H / 2.0
-                factor *= 4 * z * (H - z) / H / H
+        v = self.inflow_velocity(mesh.coords, t, mesh.params["height"])
         g = np.zeros(mesh.n_dofs)
         nc = mesh.dim + 1
-        # component 0 carries u_max * factor, the other velocity components 0
+        # component 0 carries u_max * factor, the other velocity components 0;
+        # a strong outflow (id 1) takes the same function (simulation.cc:399-401)
         sel = inflow & ((full & 1) != 0) & ((copy & 1) == 0)
-        g[np.nonzero(sel)[0] * nc] = self.u_max * factor[sel]
+        if self.outflow == "strong":
+            sel |= (((mesh.node_boundary >> 1) & 1) != 0) & ((full & 1) != 0) & ((copy & 1) == 0)
+        g[np.nonzero(sel)[0] * nc] = v[sel, 0]
         return g
 
     def time_integrator(self, dt=2.5e-4, n_steps=None):
@@ -473,6 +541,7 @@ class ShuffledMesh:
         self.new_of_old = new_of_old
         self.cell_nodes = new_of_old[cn].astype(np.uint32)
         self.coords = np.asarray(mesh.coords)[order_old]
+        self.node_boundary = np.asarray(mesh.node_boundary)[order_old]
         self._cached = None
 
     @property

@@ -114,7 +114,23 @@ typedef struct
                                  cells run in brick order internally
                                  (gls_op_cell_permutation).  {0,0,0}: no
                                  structure, per-cell kernel.                */
+  /* weak outflow boundaries (constructor arguments all_outflow_bcs_cut /
+   * all_outflow_bcs_nitsche, operator_ns.cc:79-95; needs_face_integrals):
+   * the boundary faces on them, as (caller cell, face number 2*axis + side,
+   * deal.II's face numbering of a hex / quad) with their kind
+   * (glsOutflow).  0 faces: cell integrals only (cell_loop).  Single-domain
+   * operators only (n_owned_nodes == n_nodes).                             */
+  int64_t         n_outflow_faces;
+  const int64_t  *outflow_cells;   /* host [n_outflow_faces]                 */
+  const int32_t  *outflow_face_no; /* host [n_outflow_faces] 0 .. 2*dim-1    */
+  const int32_t  *outflow_kind;    /* host [n_outflow_faces] glsOutflow      */
 } glsOpDesc;
+
+enum glsOutflow
+{
+  GLS_OUTFLOW_CUT     = 1, /* beta min(0, u*.n) u on the face, :1201-1240    */
+  GLS_OUTFLOW_NITSCHE = 2  /* Nitsche with target g, :1241-1287              */
+};
 
 typedef struct
 {
@@ -229,6 +245,17 @@ glsStatus gls_op_geometry_counts(glsOp op, int64_t *n_general,
                                  int64_t *n_cartesian);
 /* algorithmic bytes of one vmult (SURVEY §8d B_tab) */
 double gls_op_vmult_bytes(glsOp op);
+
+/* Outflow faces (glsOpDesc.n_outflow_faces): the count and the face
+ * quadrature points per face ((k+1)^(dim-1), QGauss(k+1) on the face, first
+ * tangential axis fastest), the points [face][point][dim] in the
+ * descriptor's face order; the caller evaluates the Nitsche target there
+ * (face_target_velocity, operator_ns.cc:478-521: the boundary function of
+ * all_outflow_bcs_nitsche at time t, main.cc:935-939) and hands the
+ * velocity [face][point][dim] over, host memory.  Default target: zero. */
+glsStatus gls_op_n_outflow_faces(glsOp op, int64_t *n_faces, int *n_face_points);
+glsStatus gls_op_outflow_face_points(glsOp op, double *xyz);
+glsStatus gls_op_set_outflow_target(glsOp op, const double *target, void *stream);
 
 /* OperatorBase::get_system_matrix (operator_ns.cc:1407-1430,
  * MatrixFreeTools::compute_matrix): the element matrices, from one

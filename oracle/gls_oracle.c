@@ -210,7 +210,22 @@ struct orc_op
   int        have_prev;
   int        have_old_grad;
   double    *old_grad; /* [cell][q][dim*dim + dim] grad u_old, grad p_old  */
+  /* outflow boundary faces (orc_set_outflow_faces) */
+  int64_t    n_faces;
+  int        nqf;
+  int64_t   *fcell;    /* [f] cell                                          */
+  int       *fkind;    /* [f] ORC_OUTFLOW_CUT / ORC_OUTFLOW_NITSCHE          */
+  double    *fbeta;    /* [f] effective_beta_face                           */
+  double    *fjxw;     /* [f][qf] face JxW                                  */
+  double    *fnormal;  /* [f][qf][dim] outward unit normal                  */
+  double    *fphi;     /* [f][qf][nq] cell basis values at the face points  */
+  double    *fdn;      /* [f][qf][nq] normal derivatives of the cell basis  */
+  double    *fpts;     /* [f][qf][dim] face quadrature points               */
+  double    *fustar;   /* [f][qf][dim] face_velocity (linearization point)  */
+  double    *ftarget;  /* [f][qf][dim] face_target_velocity                 */
 };
+
+static void faces_linearization(orc_op *op, const double *vec);
 
 static int
 nfields(int dim)
@@ -304,6 +319,8 @@ orc_destroy(orc_op *op)
   free(op->tab);
   free(op->cellwise);
   free(op->old_grad);
+  free(op->fcell), free(op->fkind), free(op->fbeta), free(op->fjxw), free(op->fnormal);
+  free(op->fphi), free(op->fdn), free(op->fpts), free(op->fustar), free(op->ftarget);
   free(op);
 }
 
@@ -392,7 +409,7 @@ orc_set_linearization_point(orc_op *op, const double *vec)
           T[q * nf + F_D1] = 1. / sqrt(stau * stau + 4. * u2 / h / h + 9. * a * a);
           T[q * nf + F_D2] = sqrt(u2) * h * 0.5;
         }
-    }
+    }  faces_linearization(op, vec);
 }
 
 void
@@ -608,6 +625,322 @@ cell_apply(const orc_op *op, int64_t c, const double uloc[][MAXNQ],
     integrate_scalar(dim, &op->b, V[comp], &Gq[comp][0][0], out[comp]);
 }
 
+/* ------------------------------------------------------------ outflow faces
+ * Boundary-face terms of the outflow boundaries, do_vmult_boundary
+ * operator_ns.cc:1195-1295: "cut" (:1201-1240) submits
+ *   beta_F min(0, u* . n) u                        (velocity components)
+ * with u* = face_velocity (the linearization point, :459-477) in vmult and the
+ * current value in evaluate_residual; "Nitsche" (:1241-1287) submits
+ *   value    beta_F (u - g) - nu (grad u) n
+ *   gradient -nu (u - g) (x) n
+ * with g = face_target_velocity (:478-521) in the residual only.
+ * beta_F = 1 / h^(k+1), h = (4|K|/pi)^(1/2) / k (2D), (6|K|/pi)^(1/3) / k
+ * (3D) of the face's cell (:423-457).  FEFaceEvaluation on QGauss(k+1)^(dim-1)
+ * is restated as direct sums of the cell basis at the face points; faces are
+ * identified by (cell, face number 2 * axis + side) as deal.II numbers them. */
+
+/* 1D Lagrange basis function i on the GLL nodes and its derivative at x */
+static void
+lagrange1d(const basis1d *b, int i, double x, double *v, double *d)
+{
+  double vv = 1, dd = 0;
+  for (int j = 0; j < b->n; ++j)
+    if (j != i)
+      {
+        double prod = 1.0 / (b->nodes[i] - b->nodes[j]);
+        for (int m = 0; m < b->n; ++m)
+          if (m != i && m != j)
+            prod *= (x - b->nodes[m]) / (b->nodes[i] - b->nodes[m]);
+        dd += prod;
+        vv *= (x - b->nodes[j]) / (b->nodes[i] - b->nodes[j]);
+      }
+  *v = vv;
+  *d = dd;
+}
+
+int
+orc_set_outflow_faces(orc_op *op, int64_t n, const int64_t *cells, const int32_t *face_no,
+                      const int32_t *kind)
+{
+  const int dim = op->m.dim, nq = op->nq, n1 = op->b.n, k = op->m.degree;
+  const int nqf = dim == 3 ? n1 * n1 : n1;
+  for (int64_t f = 0; f < n; ++f)
+    if (cells[f] < 0 || cells[f] >= op->m.n_cells || face_no[f] < 0 || face_no[f] >= 2 * dim ||
+        (kind[f] != ORC_OUTFLOW_CUT && kind[f] != ORC_OUTFLOW_NITSCHE))
+      return -1;
+  op->n_faces = n;
+  op->nqf     = nqf;
+#define ORC_REALLOC(p, cnt) p = realloc(p, sizeof(*p) * (size_t)((cnt) > 0 ? (cnt) : 1))
+  ORC_REALLOC(op->fcell, n);
+  ORC_REALLOC(op->fkind, n);
+  ORC_REALLOC(op->fbeta, n);
+  ORC_REALLOC(op->fjxw, n * nqf);
+  ORC_REALLOC(op->fnormal, n * nqf * dim);
+  ORC_REALLOC(op->fphi, n * nqf * nq);
+  ORC_REALLOC(op->fdn, n * nqf * nq);
+  ORC_REALLOC(op->fpts, n * nqf * dim);
+  ORC_REALLOC(op->fustar, n * nqf * dim);
+  ORC_REALLOC(op->ftarget, n * nqf * dim);
+#undef ORC_REALLOC
+  memset(op->fustar, 0, sizeof(double) * (size_t)(n * nqf * dim));
+  memset(op->ftarget, 0, sizeof(double) * (size_t)(n * nqf * dim));
+  for (int64_t f = 0; f < n; ++f)
+    {
+      const int64_t c = cells[f];
+      const int     a = face_no[f] / 2, side = face_no[f] % 2;
+      int           tang[2] = {0, 0}, nt = 0;
+      for (int e = 0; e < dim; ++e)
+        if (e != a)
+          tang[nt++] = e;
+      op->fcell[f] = c;
+      op->fkind[f] = kind[f];
+      {
+        const double meas = op->m.cell_measure[c];
+        const double h    = dim == 2 ? sqrt(4. * meas / M_PI) / k : pow(6. * meas / M_PI, 1. / 3.) / k;
+        op->fbeta[f]      = 1.0 / pow(h, (double)(k + 1));
+      }
+      for (int qf = 0; qf < nqf; ++qf)
+        {
+          double xi[3] = {0, 0, 0}, w = 1;
+          xi[a] = side;
+          const int qt[2] = {qf % n1, qf / n1};
+          for (int t = 0; t < nt; ++t)
+            {
+              xi[tang[t]] = op->b.qp[qt[t]];
+              w *= op->b.qw[qt[t]];
+            }
+          double phi[MAXNQ], gref[MAXNQ][3], J[3][3] = {{0}}, x[3] = {0, 0, 0};
+          for (int i = 0; i < nq; ++i)
+            {
+              const int ia[3] = {i % n1, (i / n1) % n1, dim == 3 ? i / (n1 * n1) : 0};
+              double    v[3] = {1, 1, 1}, d[3] = {0, 0, 0};
+              for (int e = 0; e < dim; ++e)
+                lagrange1d(&op->b, ia[e], xi[e], &v[e], &d[e]);
+              phi[i] = v[0] * v[1] * v[2];
+              for (int e = 0; e < dim; ++e)
+                {
+                  double g = d[e];
+                  for (int e2 = 0; e2 < dim; ++e2)
+                    if (e2 != e)
+                      g *= v[e2];
+                  gref[i][e] = g;
+                }
+              const double *X = op->m.coords + (size_t)op->m.cell_nodes[c * nq + i] * dim;
+              for (int dd = 0; dd < dim; ++dd)
+                {
+                  x[dd] += X[dd] * phi[i];
+                  for (int e = 0; e < dim; ++e)
+                    J[dd][e] += X[dd] * gref[i][e];
+                }
+            }
+          double inv[3][3] = {{0}}, det;
+          if (dim == 2)
+            {
+              det       = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+              inv[0][0] = J[1][1] / det, inv[0][1] = -J[0][1] / det;
+              inv[1][0] = -J[1][0] / det, inv[1][1] = J[0][0] / det;
+            }
+          else
+            {
+              det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) -
+                    J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+                    J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+              inv[0][0] = (J[1][1] * J[2][2] - J[1][2] * J[2][1]) / det;
+              inv[0][1] = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) / det;
+              inv[0][2] = (J[0][1] * J[1][2] - J[0][2] * J[1][1]) / det;
+              inv[1][0] = (J[1][2] * J[2][0] - J[1][0] * J[2][2]) / det;
+              inv[1][1] = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) / det;
+              inv[1][2] = (J[0][2] * J[1][0] - J[0][0] * J[1][2]) / det;
+              inv[2][0] = (J[1][0] * J[2][1] - J[1][1] * J[2][0]) / det;
+              inv[2][1] = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) / det;
+              inv[2][2] = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) / det;
+            }
+          /* J^{-T} n_ref with n_ref = (2 side - 1) e_a: its length is the
+           * face area element over |det J|, its direction the normal */
+          double m[3] = {0, 0, 0}, mn = 0;
+          for (int e = 0; e < dim; ++e)
+            {
+              m[e] = (2 * side - 1) * inv[a][e];
+              mn += m[e] * m[e];
+            }
+          mn                          = sqrt(mn);
+          const size_t fq             = (size_t)f * nqf + qf;
+          op->fjxw[fq]                = fabs(det) * mn * w;
+          for (int e = 0; e < dim; ++e)
+            {
+              op->fnormal[fq * dim + e] = m[e] / mn;
+              op->fpts[fq * dim + e]    = x[e];
+            }
+          for (int i = 0; i < nq; ++i)
+            {
+              double dn = 0;
+              for (int e = 0; e < dim; ++e)
+                {
+                  double gx = 0;
+                  for (int b2 = 0; b2 < dim; ++b2)
+                    gx += inv[b2][e] * gref[i][b2];
+                  dn += gx * m[e] / mn;
+                }
+              op->fphi[fq * nq + i] = phi[i];
+              op->fdn[fq * nq + i]  = dn;
+            }
+        }
+    }
+  return 0;
+}
+
+void
+orc_outflow_face_points(const orc_op *op, double *xyz)
+{
+  memcpy(xyz, op->fpts, sizeof(double) * (size_t)(op->n_faces * op->nqf * op->m.dim));
+}
+
+void
+orc_set_outflow_target(orc_op *op, const double *target)
+{
+  memcpy(op->ftarget, target, sizeof(double) * (size_t)(op->n_faces * op->nqf * op->m.dim));
+}
+
+/* face_velocity: the linearization point's velocity at the face points
+ * (read_dof_values_plain + evaluate(values), operator_ns.cc:465-476) */
+static void
+faces_linearization(orc_op *op, const double *vec)
+{
+  const int dim = op->m.dim, nq = op->nq, nc = dim + 1, nqf = op->nqf;
+  for (int64_t f = 0; f < op->n_faces; ++f)
+    for (int qf = 0; qf < nqf; ++qf)
+      for (int d = 0; d < dim; ++d)
+        {
+          double        u   = 0;
+          const double *phi = op->fphi + ((size_t)f * nqf + qf) * nq;
+          for (int i = 0; i < nq; ++i)
+            u += phi[i] * vec[(size_t)op->m.cell_nodes[op->fcell[f] * nq + i] * nc + d];
+          op->fustar[((size_t)f * nqf + qf) * dim + d] = u;
+        }
+}
+
+/* do_vmult_boundary on face f for the cell-local dof values uloc (velocity
+ * components; the pressure takes no face term): out += face integrals */
+static void
+face_apply(const orc_op *op, int64_t f, const double uloc[][MAXNQ], double out[][MAXNQ],
+           int residual)
+{
+  const int    dim = op->m.dim, nq = op->nq, nqf = op->nqf;
+  const double beta = op->fbeta[f], nu = op->prm.nu;
+  for (int qf = 0; qf < nqf; ++qf)
+    {
+      const size_t  fq  = (size_t)f * nqf + qf;
+      const double *phi = op->fphi + fq * nq, *dn = op->fdn + fq * nq, *nrm = op->fnormal + fq * dim;
+      double        u[3] = {0, 0, 0}, un[3] = {0, 0, 0}, vr[3] = {0, 0, 0}, gc[3] = {0, 0, 0};
+      for (int d = 0; d < dim; ++d)
+        for (int i = 0; i < nq; ++i)
+          {
+            u[d] += phi[i] * uloc[d][i];
+            un[d] += dn[i] * uloc[d][i];
+          }
+      if (op->fkind[f] == ORC_OUTFLOW_CUT)
+        {
+          const double *star = residual ? u : op->fustar + fq * dim;
+          double        on   = 0;
+          for (int d = 0; d < dim; ++d)
+            on += star[d] * nrm[d];
+          on = on < 0 ? on : 0.0;
+          for (int d = 0; d < dim; ++d)
+            vr[d] = beta * on * u[d];
+        }
+      else
+        {
+          if (residual)
+            for (int d = 0; d < dim; ++d)
+              u[d] -= op->ftarget[fq * dim + d];
+          for (int d = 0; d < dim; ++d)
+            {
+              vr[d] = beta * u[d] - nu * un[d];
+              gc[d] = -nu * u[d]; /* gradient_result = gc (x) n, tested: gc dn */
+            }
+        }
+      const double jxw = op->fjxw[fq];
+      for (int d = 0; d < dim; ++d)
+        for (int i = 0; i < nq; ++i)
+          out[d][i] += jxw * (vr[d] * phi[i] + gc[d] * dn[i]);
+    }
+}
+
+/* the face loop of MatrixFree::loop (boundary faces, do_vmult_boundary_range
+ * operator_ns.cc:849-879): read_dof_values(_plain), distribute_local_to_global */
+static void
+face_loop(const orc_op *op, double *dst, const double *src, int residual)
+{
+  const int dim = op->m.dim, nq = op->nq, nc = dim + 1;
+  for (int64_t f = 0; f < op->n_faces; ++f)
+    {
+      const int64_t c = op->fcell[f];
+      double        uloc[4][MAXNQ], out[4][MAXNQ];
+      memset(out, 0, sizeof(out));
+      for (int i = 0; i < nq; ++i)
+        {
+          const uint32_t node = op->m.cell_nodes[c * nq + i];
+          const uint8_t  cm   = op->m.cmask[node];
+          for (int comp = 0; comp < nc; ++comp)
+            uloc[comp][i] = (!residual && ((cm >> comp) & 1)) ? 0.0 : src[(size_t)node * nc + comp];
+        }
+      face_apply(op, f, (const double(*)[MAXNQ])uloc, out, residual);
+      for (int i = 0; i < nq; ++i)
+        {
+          const uint32_t node = op->m.cell_nodes[c * nq + i];
+          const uint8_t  cm   = op->m.cmask[node];
+          for (int comp = 0; comp < dim; ++comp)
+            if (!((cm >> comp) & 1))
+              dst[(size_t)node * nc + comp] += out[comp][i];
+        }
+    }
+}
+
+/* face part of the element matrix of cell c (compute_matrix with a
+ * boundary worker, operator_ns.cc:1380-1400) and of the diagonal
+ * (compute_diagonal's boundary_function, :202-218) */
+static void
+face_cell_matrix_add(const orc_op *op, int64_t c, double *mat)
+{
+  const int nq = op->nq, nc = op->m.dim + 1, nd = nq * nc;
+  for (int64_t f = 0; f < op->n_faces; ++f)
+    {
+      if (op->fcell[f] != c)
+        continue;
+      for (int j = 0; j < nd; ++j)
+        {
+          double uloc[4][MAXNQ] = {{0}}, out[4][MAXNQ];
+          memset(out, 0, sizeof(out));
+          uloc[j % nc][j / nc] = 1.0;
+          face_apply(op, f, (const double(*)[MAXNQ])uloc, out, 0);
+          for (int i = 0; i < nd; ++i)
+            mat[(size_t)i * nd + j] += out[i % nc][i / nc];
+        }
+    }
+}
+
+static void
+face_diagonal_add(const orc_op *op, double *diag)
+{
+  const int nq = op->nq, dim = op->m.dim, nc = dim + 1;
+  for (int64_t f = 0; f < op->n_faces; ++f)
+    {
+      const int64_t c = op->fcell[f];
+      for (int i = 0; i < nq; ++i)
+        for (int comp = 0; comp < dim; ++comp)
+          {
+            const uint32_t node = op->m.cell_nodes[c * nq + i];
+            if ((op->m.cmask[node] >> comp) & 1)
+              continue;
+            double uloc[4][MAXNQ] = {{0}}, out[4][MAXNQ];
+            memset(out, 0, sizeof(out));
+            uloc[comp][i] = 1.0;
+            face_apply(op, f, (const double(*)[MAXNQ])uloc, out, 0);
+            diag[(size_t)node * nc + comp] += out[comp][i];
+          }
+    }
+}
+
 static inline void
 atomic_add(double *p, double v)
 {
@@ -652,7 +985,7 @@ cell_loop(const orc_op *op, double *dst, const double *src, int residual)
                   dst[(size_t)node * nc + comp] += out[comp][i];
               }
         }
-    }
+    }  face_loop(op, dst, src, residual);
 }
 
 void
@@ -692,7 +1025,7 @@ orc_cell_matrix(const orc_op *op, int64_t c, double *mat)
       cell_apply(op, c, (const double(*)[MAXNQ])uloc, out, 0);
       for (int i = 0; i < nd; ++i)
         mat[(size_t)i * nd + j] = out[i % nc][i / nc];
-    }
+    }  face_cell_matrix_add(op, c, mat);
 }
 
 /* the assembled diagonal before the inversion (constrained components: 1 on
@@ -717,6 +1050,7 @@ orc_compute_diagonal(const orc_op *op, int64_t n_owned_nodes, double *diag)
         cell_apply(op, c, (const double(*)[MAXNQ])uloc, out, 0);
         diag[(size_t)node * nc + comp] += out[comp][j / nc];
       }
+  face_diagonal_add(op, diag);
   for (int64_t node = 0; node < n_owned_nodes; ++node)
     for (int comp = 0; comp < nc; ++comp)
       if ((op->m.cmask[node] >> comp) & 1)
@@ -747,6 +1081,7 @@ orc_compute_inverse_diagonal(const orc_op *op, double *diag)
         else
           diag[(size_t)node * nc + comp] += out[comp][j / nc];
       }
+  face_diagonal_add(op, diag);
   for (int64_t node = 0; node < op->m.n_nodes; ++node)
     for (int comp = 0; comp < nc; ++comp)
       if ((op->m.cmask[node] >> comp) & 1)

@@ -76,6 +76,20 @@ void orc_set_previous_solution(orc_op *op, const double *const *hist,
 void orc_vmult(const orc_op *op, double *dst, const double *src);
 /* operator_ns.cc:648-682 (src already carries the inhomogeneous values) */
 void orc_evaluate_residual(const orc_op *op, double *dst, const double *src);
+/* Outflow boundary faces (all_outflow_bcs_cut / all_outflow_bcs_nitsche,
+ * operator_ns.cc:79-95, do_vmult_boundary :1195-1295): face_no = 2 * axis +
+ * side of cells[f]; kind per face.  Their terms enter vmult, the residual,
+ * the diagonal and orc_cell_matrix (the element matrix of a cell includes its
+ * outflow faces).  Call before orc_set_linearization_point.  Returns 0. */
+enum { ORC_OUTFLOW_CUT = 1, ORC_OUTFLOW_NITSCHE = 2 };
+int  orc_set_outflow_faces(orc_op *op, int64_t n, const int64_t *cells, const int32_t *face_no,
+                           const int32_t *kind);
+/* [f][qf][dim] face quadrature points (QGauss(k+1)^(dim-1), first tangential
+ * axis fastest) ... */
+void orc_outflow_face_points(const orc_op *op, double *xyz);
+/* ... and the Nitsche target velocity there (face_target_velocity,
+ * :478-521), [f][qf][dim] */
+void orc_set_outflow_target(orc_op *op, const double *target);
 /* operator_ns.cc:195-225 */
 void orc_compute_inverse_diagonal(const orc_op *op, double *inv_diag);
 void orc_compute_diagonal(const orc_op *op, int64_t n_owned_nodes, double *diag);

@@ -50,6 +50,10 @@ def lib():
         L.orc_get_max_u.argtypes = [vp, vp]
         L.orc_get_max_u.restype = C.c_double
         L.orc_cell_matrix.argtypes = [vp, C.c_int64, vp]
+        L.orc_set_outflow_faces.argtypes = [vp, C.c_int64, vp, vp, vp]
+        L.orc_set_outflow_faces.restype = C.c_int
+        L.orc_outflow_face_points.argtypes = [vp, vp]
+        L.orc_set_outflow_target.argtypes = [vp, vp]
         L.orc_get_tables.argtypes = [vp, vp, vp]
         L.orc_get_tables.restype = C.c_int
         L.orc_get_geometry.argtypes = [vp, vp]
@@ -110,6 +114,30 @@ class Oracle:
             lib().orc_destroy(self.h)
         except Exception:
             pass
+
+    def set_outflow_faces(self, cells, face_no, kind):
+        """Outflow boundary faces (orc_set_outflow_faces); kind "cut" /
+        "nitsche" or a per-face array of 1 / 2."""
+        cells = np.ascontiguousarray(cells, dtype=np.int64)
+        face_no = np.ascontiguousarray(face_no, dtype=np.int32)
+        if isinstance(kind, str):
+            kind = np.full(len(cells), {"cut": 1, "nitsche": 2}[kind], dtype=np.int32)
+        kind = np.ascontiguousarray(kind, dtype=np.int32)
+        self._faces = (cells, face_no, kind)
+        if lib().orc_set_outflow_faces(self.h, len(cells), _p(cells), _p(face_no), _p(kind)):
+            raise ValueError("orc_set_outflow_faces: bad faces")
+        self.n_faces = len(cells)
+        self.nqf = (self.m.degree + 1) ** (self.m.dim - 1)
+
+    def outflow_face_points(self):
+        x = np.empty((self.n_faces, self.nqf, self.m.dim))
+        lib().orc_outflow_face_points(self.h, _p(x))
+        return x
+
+    def set_outflow_target(self, target):
+        t = np.ascontiguousarray(target, dtype=np.float64)
+        assert t.size == self.n_faces * self.nqf * self.m.dim
+        lib().orc_set_outflow_target(self.h, _p(t))
 
     def set_linearization_point(self, vec):
         vec = np.ascontiguousarray(vec, dtype=np.float64)

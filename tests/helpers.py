@@ -24,18 +24,21 @@ class Case:
         self.u_star = gi.linearization_point(mesh.n_nodes, mesh.dim, u_inf)
         self.hist = gi.history(self.u_star, params["order"])
 
-    def oracle(self):
+    def oracle(self, outflow=None):
         om = orc.OracleMesh(self.mesh, self.cmask)
         o = orc.Oracle(om, **self.params)
+        if outflow is not None:
+            o.set_outflow_faces(*outflow)
         o.set_linearization_point(self.u_star)
         if self.params["order"] > 0:
             o.set_previous_solution(self.hist, self.weights)
         self._om = om
         return o
 
-    def gpu(self, precision="f64", brick=None):
+    def gpu(self, precision="f64", brick=None, outflow=None):
         import glsamd
-        op = glsamd.NavierStokesOperator(self.mesh, self.cmask, precision, brick=brick)
+        op = glsamd.NavierStokesOperator(self.mesh, self.cmask, precision, brick=brick,
+                                         outflow=outflow)
         op.set_parameters(**self.params)
         op.set_linearization_point(self.u_star)
         if self.params["order"] > 0:
