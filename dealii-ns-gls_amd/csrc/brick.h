@@ -559,6 +559,38 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
         for (int c = 0; c < nc; ++c)
           u[it][c] = T(0);
     }
+  // FP32 (multigrid levels): the fused relaxation's operands b, d and the
+  // unmodified src of the exclusive nodes are loaded here, behind the
+  // gather, instead of after the cell rounds (one memory round trip less at
+  // the end of every brick; FP64 has no registers to spare for them)
+#ifndef GLS_RELAX_PREFETCH
+#define GLS_RELAX_PREFETCH 1
+#endif
+  constexpr bool PRE = GLS_RELAX_PREFETCH && sizeof(T) == 4 && !R;
+  constexpr int  NPR = PRE ? NI : 1;
+  T              xb[NPR][nc], xd[NPR][nc], xs[NPR][nc];
+  if constexpr (PRE)
+    {
+#pragma unroll
+      for (int it = 0; it < NI; ++it)
+        {
+          const int  i    = t + it * BLOCK;
+          const bool excl = i < L && tg[it] != UNUSED_NODE && !(tg[it] & SHARED_BIT);
+#pragma unroll
+          for (int c = 0; c < nc; ++c)
+            {
+              xs[it][c] = u[it][c];
+              xb[it][c] = T(0);
+              xd[it][c] = T(1);
+            }
+          if (excl && a.rb)
+            {
+              load_node<T, nc>(a.rb, tg[it], xb[it]);
+              if (a.rd)
+                load_node<T, nc>(a.rd, tg[it], xd[it]);
+            }
+        }
+    }
   LaneData<dim, T, MODE> cur;
   load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, wave * CPW + slot, in_wave, p, pa,
                              cur);
@@ -864,9 +896,19 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
             {
               r[c] = (T)(R ? -s_acc[c * LP + ip] : s_acc[c * LP + ip]);
               if ((cm >> c) & 1)
-                r[c] = R ? T(0) : a.src[(size_t)tgt * nc + c];
+                r[c] = R ? T(0) : (PRE ? xs[PRE ? it : 0][c] : a.src[(size_t)tgt * nc + c]);
             }
-          if constexpr (!R)
+          if constexpr (PRE)
+            {
+              if (a.rb)
+#pragma unroll
+                for (int c = 0; c < nc; ++c)
+                  {
+                    const T base = a.rkeep ? xs[it][c] : T(0);
+                    r[c]         = base + a.romega * xd[it][c] * (xb[it][c] - r[c]);
+                  }
+            }
+          else if constexpr (!R)
             if (a.rb)
 #pragma unroll
               for (int c = 0; c < nc; ++c)

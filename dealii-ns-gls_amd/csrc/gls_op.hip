@@ -624,12 +624,19 @@ struct Impl
   static void
   launch_persistent(K kernel, int64_t n_bricks, size_t lds, hipStream_t s, const Args &a)
   {
-    int dev = 0, n_cu = 0, per_cu = 0;
-    HIP_THROW(hipGetDevice(&dev));
-    HIP_THROW(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    HIP_THROW(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, BLOCK, lds));
-    const int64_t slots = (int64_t)std::max(1, per_cu) * std::max(1, n_cu);
-    const int64_t g     = GLS_PERSISTENT ? std::max<int64_t>(1, std::min(n_bricks, slots)) : n_bricks;
+    // the occupancy query costs several microseconds of host time per
+    // launch, which the multigrid's short coarse-level launches cannot hide:
+    // only the persistent diagnostic build asks it
+    int64_t g = n_bricks;
+    if (GLS_PERSISTENT)
+      {
+        int dev = 0, n_cu = 0, per_cu = 0;
+        HIP_THROW(hipGetDevice(&dev));
+        HIP_THROW(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+        HIP_THROW(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, BLOCK, lds));
+        const int64_t slots = (int64_t)std::max(1, per_cu) * std::max(1, n_cu);
+        g                   = std::max<int64_t>(1, std::min(n_bricks, slots));
+      }
     hipLaunchKernelGGL(kernel, dim3((unsigned)g), dim3(BLOCK), lds, s, a);
   }
 

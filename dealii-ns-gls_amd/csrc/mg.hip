@@ -58,10 +58,32 @@ __global__ void __launch_bounds__(256)
 {
   constexpr int n = k + 1, nq = ipow(n, dim), nc = dim + 1, L = 2 * k + 1;
   constexpr int nl = ipow(L, dim);
+  constexpr int NIT = (nl + 255) / 256; // lattice points per thread (blockDim 256)
   __shared__ T  u[nc][nq];
   __shared__ T  sP[L][n];
   const int64_t c = blockIdx.x;
   const int     t = threadIdx.x;
+  // the lattice's fine node ids and their weights / base values do not
+  // depend on the coarse gather: issued first, in flight together with it
+  // (one memory round trip before the sweeps instead of two)
+  uint32_t fe[NIT];
+  T        wv[NIT][nc], bv[NIT][nc];
+#pragma unroll
+  for (int r = 0; r < NIT; ++r)
+    {
+      const int I = t + r * 256;
+      fe[r]       = I < nl ? a.child[c * nl + I] : NOT_OWNER;
+    }
+#pragma unroll
+  for (int r = 0; r < NIT; ++r)
+#pragma unroll
+    for (int comp = 0; comp < nc; ++comp)
+      {
+        const size_t j = (size_t)(fe[r] & ~NOT_OWNER) * nc + comp;
+        const bool   o = !(fe[r] & NOT_OWNER);
+        wv[r][comp]    = o ? a.weight[j] : T(0);
+        bv[r][comp]    = o ? (base ? base[j] : dst_f[j]) : T(0);
+      }
   if (t < L * n)
     sP[t / n][t % n] = a.P[t / n][t % n];
   if (t < nq)
@@ -73,8 +95,12 @@ __global__ void __launch_bounds__(256)
         u[comp][t] = ((cm >> comp) & 1) ? T(0) : src_c[(size_t)node * nc + comp];
     }
   __syncthreads();
-  for (int I = t; I < nl; I += blockDim.x)
+#pragma unroll
+  for (int r = 0; r < NIT; ++r)
     {
+      const int I = t + r * 256;
+      if (I >= nl)
+        break;
       const int Ix = I % L, Iy = (I / L) % L, Iz = dim == 3 ? I / (L * L) : 0;
       T         px[n], py[n], pz[n];
 #pragma unroll
@@ -84,13 +110,12 @@ __global__ void __launch_bounds__(256)
           py[i] = sP[Iy][i];
           pz[i] = dim == 3 ? sP[Iz][i] : T(0);
         }
-      const uint32_t fe = a.child[c * nl + I];
       // a fine node shared by several coarse cells is written by its owner
       // only (conforming interpolation: all give the same value), so the
       // update is a plain read-modify-write, no atomics
-      if (fe & NOT_OWNER)
+      if (fe[r] & NOT_OWNER)
         continue;
-      const uint32_t fn = fe;
+      const uint32_t fn = fe[r];
 #pragma unroll
       for (int comp = 0; comp < nc; ++comp)
         {
@@ -110,12 +135,12 @@ __global__ void __launch_bounds__(256)
                 }
               s += (dim == 3 ? pz[iz] : T(1)) * sy;
             }
-          const T      w = a.weight[(size_t)fn * nc + comp];
+          const T      w = wv[r][comp];
           const size_t j = (size_t)fn * nc + comp;
           if (base) // out of place: dst = base + w P src
-            dst_f[j] = base[j] + (w != T(0) ? w * s : T(0));
+            dst_f[j] = bv[r][comp] + (w != T(0) ? w * s : T(0));
           else if (w != T(0))
-            dst_f[j] += w * s;
+            dst_f[j] = bv[r][comp] + w * s;
         }
     }
 }
@@ -130,6 +155,10 @@ __global__ void __launch_bounds__(256)
   __shared__ T  sP[L][n];
   const int64_t c = blockIdx.x;
   const int     t = threadIdx.x;
+  // this thread's coarse dof (node id, constraint bits) is independent of
+  // the fine gather: loaded up front (blockDim 256 >= nq * nc, k <= 2 in 3D)
+  constexpr bool ONE = nq * nc <= 256;
+  const uint32_t pk0 = ONE && t < nq * nc ? a.coarse_nodes[c * nq + t % nq] : 0u;
   if (t < L * n)
     sP[t / n][t % n] = a.P[t / n][t % n];
   for (int I = t; I < nl; I += blockDim.x)
@@ -149,7 +178,7 @@ __global__ void __launch_bounds__(256)
   for (int i = t; i < nq * nc; i += blockDim.x)
     {
       const int      ii = i % nq, comp = i / nq;
-      const uint32_t packed = a.coarse_nodes[c * nq + ii];
+      const uint32_t packed = ONE ? pk0 : a.coarse_nodes[c * nq + ii];
       const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
       if ((cm >> comp) & 1)
         continue;
@@ -219,6 +248,33 @@ k_relax(T *__restrict__ x, const T *__restrict__ b, const T *__restrict__ t,
     x[i] = omega * d[i] * b[i];
   else
     x[i] += omega * d[i] * (b[i] - t[i]);
+}
+
+// The zero-start relaxation of a level's pre-smoothing with two neighbours of
+// the V-cycle folded in: the next coarser defect, which the restriction then
+// accumulates into, is zeroed here (zero_words), and on the finest level the
+// outer FP64 defect is converted here (copy_to_mg): b = (T) b64, written to
+// bout.  One launch instead of three.
+template <typename T>
+__global__ void
+k_relax_first(T *__restrict__ x, const T *__restrict__ b, const T *__restrict__ d, T omega,
+              int64_t n, uint32_t *__restrict__ zero, int64_t zero_words,
+              const double *__restrict__ b64, T *__restrict__ bout)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < zero_words)
+    zero[i] = 0u;
+  if (i >= n)
+    return;
+  T bi;
+  if (b64)
+    {
+      bi      = (T)b64[i];
+      bout[i] = bi;
+    }
+  else
+    bi = b[i];
+  x[i] = omega * d[i] * bi;
 }
 
 // t = b - t  (Multigrid residual step)
@@ -418,6 +474,9 @@ struct glsMG_
   double        *d_rhs  = nullptr; // [(2 + GEMV_CHUNKS) n0]: rhs | solution | partials
   // coarse GMRES (coarse_iterate): FP64 Krylov workspace, two level-
   // precision operand buffers, statistics of the last solve
+  // finest-level FP64 defect for the fused copy_to_mg (mg_vcycle_device; null:
+  // def[top] already holds the defect)
+  const double *top_b64 = nullptr;
   double *cg_ws    = nullptr;
   void   *cg_lvl   = nullptr;
   int     cg_iters = 0, cg_conv = 0;
@@ -519,14 +578,42 @@ relax_t(const glsMG_ *mg, int level, void *x, const void *b, int first, hipStrea
   HIP_THROW(hipGetLastError());
 }
 
+// what the zero-start relaxation folds in (k_relax_first)
+struct FirstRelax
+{
+  uint32_t     *zero       = nullptr;
+  int64_t       zero_words = 0;
+  const double *b64        = nullptr; // FP64 defect to convert into b
+};
+
+template <typename T>
+void
+relax_first_t(const glsMG_ *mg, int level, void *x, void *b, const FirstRelax &fr, hipStream_t s)
+{
+  const int64_t n = mg->ops[level]->n_dofs;
+  hipLaunchKernelGGL(k_relax_first<T>, g1(std::max(n, fr.zero_words)), dim3(256), 0, s, (T *)x,
+                     (const T *)b, (const T *)mg->invdiag[level], (T)mg->omega[level], n,
+                     fr.zero, fr.zero_words, fr.b64, (T *)b);
+  HIP_THROW(hipGetLastError());
+}
+
 // PreconditionRelaxation::vmult (zero start) / step, `iters` iterations;
 // the result in x.  x_in (step only): the starting iterate is in tmp[level]
 // instead of x (the multigrid's out-of-place prolongation put it there).
-void
+// fr (zero start only): folded into the first relaxation; false when there
+// was none (iters == 0), so the caller does that work itself
+bool
 smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int iters,
-       hipStream_t s, bool start_in_tmp = false)
+       hipStream_t s, bool start_in_tmp = false, const FirstRelax *fr = nullptr)
 {
   auto  relax = mg->prec == GLS_F64 ? relax_t<double> : relax_t<float>;
+  auto  first = [&](void *xx) {
+    if (fr)
+      (mg->prec == GLS_F64 ? relax_first_t<double> : relax_first_t<float>)(mg, level, xx,
+                                                                          (void *)b, *fr, s);
+    else
+      relax(mg, level, xx, b, 1, s);
+  };
   glsOp op    = mg->ops[level];
   void *tmp   = mg->tmp[level];
   if (!gls::fused_relax_ok(op))
@@ -541,7 +628,7 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
         }
       if (zero_start && iters > 0)
         {
-          relax(mg, level, x, b, 1, s);
+          first(x);
           it = 1;
         }
       for (; it < iters; ++it)
@@ -549,7 +636,7 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
           gls::op_vmult_device(op, tmp, x, s);
           relax(mg, level, x, b, 0, s);
         }
-      return;
+      return zero_start && iters > 0;
     }
   // brick operators: the step x + omega D^{-1} (b - A x) is fused into the
   // vmult's write-out (k_brick, k_shared_reduce_cls), ping-ponging between x
@@ -561,7 +648,7 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
   if (zero_start && iters > 0)
     {
       cur = ((iters - 1) % 2 == 1) ? tmp : x;
-      relax(mg, level, cur, b, 1, s);
+      first(cur);
       it = 1;
     }
   gls::RelaxStep rx;
@@ -581,6 +668,7 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
       hipLaunchKernelGGL(k_copy, g1(w), dim3(256), 0, s, (uint32_t *)x, (const uint32_t *)cur, w);
       HIP_THROW(hipGetLastError());
     }
+  return zero_start && iters > 0;
 }
 
 void
@@ -923,8 +1011,21 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
       return;
     }
   const int nit = mg->desc.smoothing_n_iterations;
-  // pre-smoothing from a zero initial guess (MGSmootherPrecondition::apply)
-  smooth(mg, l, mg->sol[l], mg->def[l], true, nit, s);
+  // pre-smoothing from a zero initial guess (MGSmootherPrecondition::apply);
+  // its first relaxation also zeroes the coarser defect for the restriction
+  // (and on the finest level converts the outer defect, mg->top_b64)
+  FirstRelax fr;
+  fr.zero       = (uint32_t *)mg->def[l - 1];
+  fr.zero_words = (int64_t)((size_t)mg->ops[l - 1]->n_dofs * mg->ts() / 4);
+  fr.b64        = l == (int)mg->ops.size() - 1 ? mg->top_b64 : nullptr;
+  const bool folded = smooth(mg, l, mg->sol[l], mg->def[l], true, nit, s, false, &fr);
+  if (!folded && fr.b64)
+    {
+      const int64_t n = mg->ops[l]->n_dofs;
+      hipLaunchKernelGGL((k_convert<double, float>), g1(n), dim3(256), 0, s,
+                         (float *)mg->def[l], fr.b64, n);
+      HIP_THROW(hipGetLastError());
+    }
   // residual t = defect - A solution (fused into the brick vmult's write-out
   // and shared-node reduction for brick operators)
   if (gls::fused_relax_ok(mg->ops[l]))
@@ -942,11 +1043,12 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
       residual(mg, l, mg->tmp[l], mg->def[l], s);
     }
   // restrict
-  {
-    const int64_t w = (int64_t)((size_t)mg->ops[l - 1]->n_dofs * mg->ts() / 4);
-    hipLaunchKernelGGL(k_zero, g1(w), dim3(256), 0, s, (uint32_t *)mg->def[l - 1], w);
-    HIP_THROW(hipGetLastError());
-  }
+  if (!folded)
+    {
+      const int64_t w = (int64_t)((size_t)mg->ops[l - 1]->n_dofs * mg->ts() / 4);
+      hipLaunchKernelGGL(k_zero, g1(w), dim3(256), 0, s, (uint32_t *)mg->def[l - 1], w);
+      HIP_THROW(hipGetLastError());
+    }
   transfer(mg, 1, l, mg->def[l - 1], mg->tmp[l], s);
   v_step(mg, l - 1, s);
   // prolongate and add the coarse correction; with an odd number of fused
@@ -1430,14 +1532,31 @@ mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s)
   const int     top = (int)mg->ops.size() - 1;
   const int64_t n   = mg->ops[top]->n_dofs;
   const bool    cvt = mg->desc.outer_precision == GLS_F64 && mg->prec == GLS_F32;
-  // copy_to_mg
-  if (cvt)
+  // copy_to_mg: folded into the finest level's first relaxation (v_step)
+  // when the V-cycle runs directly with a smoothing level on top; a captured
+  // graph would freeze src's address, the coarse-only hierarchy has no
+  // relaxation to fold into
+  const char *ge     = getenv("GLS_MG_GRAPH");
+  const bool  graph  = ge && std::atoi(ge) != 0;
+  const bool  folded = cvt && top > 0 && !graph && mg->desc.smoothing_n_iterations > 0;
+  if (folded)
+    mg->top_b64 = (const double *)src;
+  else if (cvt)
     hipLaunchKernelGGL((k_convert<double, float>), g1(n), dim3(256), 0, s,
                        (float *)mg->def[top], (const double *)src, n);
   else
     HIP_THROW(hipMemcpyAsync(mg->def[top], src, n * mg->ts(), hipMemcpyDeviceToDevice, s));
   HIP_THROW(hipGetLastError());
-  run_v_step(mg, top, s);
+  try
+    {
+      run_v_step(mg, top, s);
+    }
+  catch (...)
+    {
+      mg->top_b64 = nullptr;
+      throw;
+    }
+  mg->top_b64 = nullptr;
   // copy_from_mg
   if (cvt)
     hipLaunchKernelGGL((k_convert<float, double>), g1(n), dim3(256), 0, s, (double *)dst,

@@ -12,7 +12,11 @@ echo "base $(ms gpurun_out/f32/base.json)"
 for v in occ32_4 occ32_5; do
   GLS_AMD_LIB=dealii-ns-gls_amd/lib/var/$v.so timeout -k 10 120 python bench.py $B > gpurun_out/f32/$v.json 2>/dev/null || exit $?
   echo "$v $(ms gpurun_out/f32/$v.json)"
+  GLS_PAD32=0 GLS_AMD_LIB=dealii-ns-gls_amd/lib/var/$v.so timeout -k 10 120 python bench.py $B > gpurun_out/f32/${v}_nopad.json 2>/dev/null || exit $?
+  echo "$v nopad $(ms gpurun_out/f32/${v}_nopad.json)"
 done
+GLS_PAD32=0 timeout -k 10 120 python bench.py $B > gpurun_out/f32/base_nopad.json 2>/dev/null || exit $?
+echo "base nopad $(ms gpurun_out/f32/base_nopad.json)"
 for sp in 0 224 448 800 1600; do
   GLS_BRICK_SPLIT=$sp timeout -k 10 120 python bench.py $B > gpurun_out/f32/split$sp.json 2>/dev/null || exit $?
   echo "split$sp $(ms gpurun_out/f32/split$sp.json)"
