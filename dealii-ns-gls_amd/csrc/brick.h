@@ -131,8 +131,62 @@ struct BrickArgs
   int             PLx, PLy, LP; // padded LDS lattice strides / size (>= L)
   T               nu, w0, theta, stau;
   int             td, cw, have_prev, have_old_grad;
+  // fused shared-node reduction (single-domain full vmult): per shared node
+  // an arrival counter (zero between launches); the brick whose arrival
+  // completes a node sums its partial slots and writes dst there, instead of
+  // k_shared_reduce_cls.  null: partial slots only.
+  uint32_t       *counters;
+  uint32_t        partial_bytes;
+  ReduceClasses   rc;
   Shape<T, n>     sh;
 };
+
+// partial slots of the fused reduction: written through to memory (sc1) and
+// read back the same way, so a brick on another XCD sees them once the
+// writer's arrival is counted (MI355X_MICROARCH.md, inter-workgroup
+// visibility: sc1 stores, vmcnt(0) + barrier before the counter add, sc1
+// loads by the last arriver after its add returned)
+typedef unsigned int U4 __attribute__((ext_vector_type(4)));
+
+template <typename T, int nc>
+__device__ __forceinline__ void
+store_slot_wt(__amdgpu_buffer_rsrc_t rs, uint32_t slot, const T (&r)[nc])
+{
+  constexpr int NB = nc * sizeof(T) / 16; // the fused path runs whole 16-byte slots only
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+    {
+      U4 v;
+      __builtin_memcpy(&v, reinterpret_cast<const char *>(r) + 16 * b, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(slot * (uint32_t)(nc * sizeof(T)) + 16 * b),
+                                             0, 16);
+    }
+}
+
+template <typename T, int nc>
+__device__ __forceinline__ void
+load_slot_wt(__amdgpu_buffer_rsrc_t rs, uint32_t slot, T (&r)[nc])
+{
+  constexpr int NB = nc * sizeof(T) / 16;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+    {
+      const U4 v = __builtin_amdgcn_raw_buffer_load_b128(
+        rs, (int)(slot * (uint32_t)(nc * sizeof(T)) + 16 * b), 0, 16);
+      __builtin_memcpy(reinterpret_cast<char *>(r) + 16 * b, &v, 16);
+    }
+}
+
+__device__ __forceinline__ int
+slot_class(const ReduceClasses &rc, uint32_t slot)
+{
+  int kc = 0;
+#pragma unroll
+  for (int j = 1; j < ReduceClasses::MAX; ++j)
+    if (j < rc.n && slot >= rc.slot0[j])
+      kc = j;
+  return kc;
+}
 
 // 1D coefficient tables in LDS: S, S^T, Dq, Dq^T, each row padded to whole
 // 16-byte packs (RP values) so that a lane's row M[pa][*] (or M[*][pa]) is
@@ -452,6 +506,28 @@ to_packs(const T (&x)[nc], V (&v)[NP])
 #pragma unroll
     for (int w = 0; w < W; ++w)
       v[kp][w] = kp * W + w < nc ? x[kp * W + w] : T(0);
+}
+
+// a shared node's final value from its summed partials (constraints, then
+// the fused relaxation), as k_shared_reduce_cls writes it
+template <typename T, int nc, bool R, typename Args>
+__device__ __forceinline__ void
+finish_shared(const Args &a, uint32_t packed, T (&r)[nc])
+{
+  const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
+#pragma unroll
+  for (int c = 0; c < nc; ++c)
+    if ((cm >> c) & 1)
+      r[c] = R ? T(0) : a.src[(size_t)node * nc + c];
+  if (!R && a.rb)
+#pragma unroll
+    for (int c = 0; c < nc; ++c)
+      {
+        const size_t j = (size_t)node * nc + c;
+        r[c]           = (a.rkeep ? a.src[j] : T(0)) + a.romega * (a.rd ? a.rd[j] : T(1)) *
+                                                       (a.rb[j] - r[c]);
+      }
+  store_node<T, nc>(a.dst, node, r);
 }
 
 #ifndef GLS_BRICK_OCC
@@ -868,6 +944,9 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
   GLS_STAMP(brick, 6);
 
   // ---- write out: exclusive nodes -> dst, boundary nodes -> partials
+  constexpr bool FUSE = nc * sizeof(T) % 16 == 0; // 3D: 4 components per slot
+  const __amdgpu_buffer_rsrc_t prs =
+    __builtin_amdgcn_make_buffer_rsrc(a.partial, 0, (int)a.partial_bytes, 0x00020000);
 #pragma unroll
   for (int it = 0; it < NI; ++it)
     {
@@ -885,7 +964,16 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
 #pragma unroll
           for (int c = 0; c < nc; ++c)
             r[c] = (T)(R ? -s_acc[c * LP + ip] : s_acc[c * LP + ip]);
-          store_node<T, nc>(a.partial, tgt & ~SHARED_BIT, r);
+          if (FUSE && a.counters)
+            {
+              const uint32_t slot = tgt & ~SHARED_BIT;
+              if (a.rc.mult[slot_class(a.rc, slot)] == 1)
+                finish_shared<T, nc, R>(a, pk[it], r); // the node's only brick
+              else
+                store_slot_wt<T, nc>(prs, slot, r);
+            }
+          else
+            store_node<T, nc>(a.partial, tgt & ~SHARED_BIT, r);
         }
       else
         {
@@ -918,6 +1006,69 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
                   r[c]           = base + a.romega * (a.rd ? a.rd[j] : T(1)) * (a.rb[j] - r[c]);
                 }
           store_node<T, nc>(a.dst, tgt, r);
+        }
+    }
+  if (FUSE && a.counters)
+    {
+      // every wave's slot stores have reached memory before any arrival of
+      // this brick is counted
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < NI; ++it)
+        {
+          const int i = t + it * BLOCK;
+          if (i >= L)
+            break;
+          const uint32_t tgt = tg[it];
+          if (tgt == UNUSED_NODE || !(tgt & SHARED_BIT))
+            continue;
+          const uint32_t slot = tgt & ~SHARED_BIT;
+          const int      kc   = slot_class(a.rc, slot);
+          const uint32_t m    = a.rc.mult[kc];
+          if (m == 1)
+            continue;
+          const uint32_t sn  = a.rc.first[kc] + (slot - a.rc.slot0[kc]) / m;
+          const uint32_t b0s = a.rc.slot0[kc] + (sn - a.rc.first[kc]) * m;
+          const uint32_t old = __hip_atomic_fetch_add(a.counters + sn, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+          if (old != m - 1)
+            continue;
+          // last arrival: the node's slots in slot order, summed as
+          // k_shared_reduce_cls sums them
+          T        sum[nc] = {};
+          uint32_t j       = 0;
+          for (; j + 4 <= m; j += 4)
+            {
+              T x0[nc], x1[nc], x2[nc], x3[nc];
+              load_slot_wt<T, nc>(prs, b0s + j, x0);
+              load_slot_wt<T, nc>(prs, b0s + j + 1, x1);
+              load_slot_wt<T, nc>(prs, b0s + j + 2, x2);
+              load_slot_wt<T, nc>(prs, b0s + j + 3, x3);
+#pragma unroll
+              for (int c = 0; c < nc; ++c)
+                sum[c] += (x0[c] + x1[c]) + (x2[c] + x3[c]);
+            }
+          if (j + 2 <= m)
+            {
+              T x0[nc], x1[nc];
+              load_slot_wt<T, nc>(prs, b0s + j, x0);
+              load_slot_wt<T, nc>(prs, b0s + j + 1, x1);
+#pragma unroll
+              for (int c = 0; c < nc; ++c)
+                sum[c] += x0[c] + x1[c];
+              j += 2;
+            }
+          if (j < m)
+            {
+              T x0[nc];
+              load_slot_wt<T, nc>(prs, b0s + j, x0);
+#pragma unroll
+              for (int c = 0; c < nc; ++c)
+                sum[c] += x0[c];
+            }
+          finish_shared<T, nc, R>(a, pk[it], sum);
+          __hip_atomic_store(a.counters + sn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
   GLS_STAMP(brick, 7);

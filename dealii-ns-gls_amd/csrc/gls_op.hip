@@ -369,6 +369,10 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
   upload((void **)&op->d_shared_off, off);
   HIP_THROW(hipMalloc(&op->d_partial,
                       std::max<size_t>(1, (size_t)slot * (dim + 1) * op->tsize())));
+  // arrival counters of the fused reduction (k_brick, BrickArgs::counters):
+  // zero between launches, every completing brick resets its nodes'
+  HIP_THROW(hipMalloc((void **)&op->d_counters, std::max<size_t>(1, shared_nodes.size() * 4)));
+  HIP_THROW(hipMemset(op->d_counters, 0, std::max<size_t>(1, shared_nodes.size() * 4)));
 }
 
 // storage field (kernels.h Fields) of canonical host field f: the host
@@ -618,6 +622,9 @@ struct Impl
 #ifndef GLS_PERSISTENT
 #define GLS_PERSISTENT 0
 #endif
+#ifndef GLS_FUSED_REDUCE_DEFAULT
+#define GLS_FUSED_REDUCE_DEFAULT 0
+#endif
   // persistent brick kernel: one workgroup per resident slot (occupancy x
   // CUs of the current device), each walking bricks g, g + grid, ...
   template <typename K, typename Args>
@@ -693,6 +700,23 @@ struct Impl
         a.have_prev     = op->have_prev ? 1 : 0;
         a.have_old_grad = (op->have_old_grad && op->prm.theta != 1.0) ? 1 : 0;
         a.sh            = make_shape<T, n>(op->basis);
+        // fused shared-node reduction: a whole single-domain vmult whose
+        // shared nodes all have at least one brick (GLS_FUSED_REDUCE=0: the
+        // separate k_shared_reduce_cls launch)
+        static const int fuse_env = getenv("GLS_FUSED_REDUCE") ? std::atoi(getenv("GLS_FUSED_REDUCE"))
+                                                               : GLS_FUSED_REDUCE_DEFAULT;
+        const size_t pbytes = (size_t)op->n_slots * (dim + 1) * sizeof(T);
+        const ReduceClasses &rc0 = op->reduce_classes;
+        const bool fused = fuse_env != 0 && ((dim + 1) * sizeof(T)) % 16 == 0 &&
+                           what == (BRICK_RUN | BRICK_REDUCE) && b0 == 0 &&
+                           b1 == op->n_bricks && op->n_owned_nodes == op->n_nodes &&
+                           rc0.n > 0 && rc0.mult[0] > 0 && pbytes < ((size_t)1 << 31) &&
+                           op->d_counters;
+        a.counters      = fused ? op->d_counters : nullptr;
+        a.partial_bytes = (uint32_t)std::min<size_t>(pbytes, ((size_t)1 << 31) - 1);
+        a.rc            = rc0;
+        if (fused)
+          what = BRICK_RUN;
         const size_t lds = BrickLDS<dim, k, T>::bytes(a.LP);
         if ((what & BRICK_RUN) && b1 > b0 && mode == MODE_NEWTON && GLS_NEWTON_T1)
           {
@@ -1539,7 +1563,8 @@ gls_op_destroy(glsOp op)
                   op->d_brick_target, op->d_shared_nodes, op->d_shared_off,
                   op->d_partial,      op->d_bgeo_cart,    op->d_bgeo_gen,
                   op->d_brick_geo,    op->d_brick_cell0,  op->d_brick_chunk0, op->d_tab_cbase,
-                  op->d_node_cmask,   op->d_inhom,        op->gmres_ws};
+                  op->d_node_cmask,   op->d_inhom,        op->gmres_ws,
+                  op->d_counters};
   for (void *b : bufs)
     if (b)
       (void)hipFree(b);
