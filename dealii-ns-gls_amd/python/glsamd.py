@@ -258,6 +258,15 @@ class NavierStokesOperator:
         _check(lib().gls_op_brick_shape(h, dims))
         self.brick_shape = tuple(dims)  # what runs: (0, 0, 0) = per-cell kernel
 
+    def extract_constant_modes(self):
+        """NavierStokesOperator::extract_constant_modes (operator_ns.cc:
+        175-193, DoFTools::extract_constant_modes over all dim+1 components):
+        one boolean dof mask per component, node-major numbering (the AMG
+        near-null space a Trilinos coarse solver takes)."""
+        nc = self.dim + 1
+        comp = np.arange(self.n_dofs) % nc
+        return [comp == c for c in range(nc)]
+
     @property
     def n_outflow_faces(self):
         n, q = C.c_int64(), C.c_int()
