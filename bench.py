@@ -336,6 +336,11 @@ def dist_size_companion(d, params, weights, n_ref, dist, rank, world, reps=30):
         "ms": ms, "dofs": m.n_dofs, "cells": m.n_cells, "dofs_per_s": m.n_dofs / (ms * 1e-3),
         "n_gpus": world, "algorithmic_bytes_all_ranks": float(b.item()),
         "roofline_frac_aggregate": float(b.item()) / (ms * 1e-3) / (HBM_PEAK * world),
+        "cells_per_gpu": m.n_cells / world,
+        # at 8 ranks r{n+1} gives every GPU the single-GPU headline's cell
+        # count: the weak-scaling point of SURVEY §8e beside the strong-scaled
+        # headline (8x the DoFs in the same per-GPU work)
+        "weak_scaling_point": world == 8,
         "note": "DistributedOperator (native RCCL halo import overlapped with interior bricks, "
                 "export-add), wall clock max over ranks"}}
 
