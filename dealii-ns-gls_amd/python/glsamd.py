@@ -372,6 +372,21 @@ class NavierStokesOperator:
         _check(lib().gls_op_vmult(self.h, _vptr(dst), _vptr(src), _stream()))
         return dst
 
+    def Tvmult(self, dst, src):
+        """OperatorBase::Tvmult forwards to vmult (operator_base.cc:12-18)."""
+        self.vmult(dst, src)
+
+    def invalidate_system(self):
+        """OperatorBase::invalidate_system (operator_ns.cc:229-232): the
+        reference drops its cached system matrix; system_matrix() here is
+        assembled on every call, so there is nothing to drop."""
+
+    def get_constraints(self):
+        """The homogeneous constraints the operator resolves
+        (get_constraints, operator_ns.cc:157-160): per node the constrained
+        component bits, node-major."""
+        return np.asarray(self._keep[2])
+
     def vmult_init(self, dst, src):
         _check(lib().gls_op_vmult_init(self.h, _ptr(dst), _ptr(src), _stream()))
 

@@ -174,6 +174,13 @@ public:
 
   double vmult_bytes() const { return gls_op_vmult_bytes(h); }
 
+  // OperatorBase::Tvmult forwards to vmult (operator_base.cc:12-18)
+  void
+  Tvmult(void *dst, const void *src, void *stream = nullptr) const
+  {
+    vmult(dst, src, stream);
+  }
+
   // OperatorBase::get_system_matrix (operator_ns.cc:1407-1430) as CSR over
   // the node-major dofs; constrained rows / columns carry their unit diagonal
   struct SparseMatrix
