@@ -1329,6 +1329,17 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
     }
   d = &dd;
   auto *op          = new glsOp_();
+  // an invalid descriptor found below (bricks, outflow faces, allocation
+  // failures) frees what was built so far
+  struct CreateGuard
+  {
+    glsOp_ *p;
+    ~CreateGuard()
+    {
+      if (p)
+        gls_op_destroy(p);
+    }
+  } guard{op};
   if (!p_nodes.empty())
     op->cell_perm = std::move(plan.perm);
   op->dim           = d->dim;
@@ -1548,6 +1559,7 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
   op->prm.theta = 1.0;
   op->prm.dt    = 1.0;
   gls::faces_setup(op, caller);
+  guard.p       = nullptr;
   *out          = op;
   GLS_CATCH
 }

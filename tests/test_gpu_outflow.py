@@ -127,3 +127,18 @@ def test_outflow_gmres_gmg():
     print("outflow gmres", st)
     assert st["converged"] == 1
     assert true_res <= 64 * st["tolerance"], (true_res, st)
+
+
+def test_outflow_bad_face_rejected():
+    """An invalid outflow face fails gls_op_create loudly (and frees what the
+    create had built); a partitioned operator refuses faces."""
+    import glsamd
+    case, (cells, fno, kind) = _case("input_turek_2D_Re20_stat.json", 0, "nitsche")
+    bad = fno.copy()
+    bad[0] = 7
+    with pytest.raises(glsamd.GlsError, match="outflow face"):
+        case.gpu("f64", outflow=(cells, bad, kind))
+    with pytest.raises(glsamd.GlsError, match="single domain"):
+        glsamd.NavierStokesOperator(case.mesh, case.cmask, "f64",
+                                    n_owned_nodes=case.mesh.n_nodes - 1,
+                                    outflow=(cells, fno, kind))
