@@ -247,8 +247,9 @@ def mg_companions(d, params, weights, n_ref, reps=20):
     vc_graph = vcycles()
     os.environ.pop("GLS_MG_GRAPH")
     # the deck's own coarse solver ("gmg coarse grid solver": "direct",
-    # multigrid.cc:448-455): a dense LU of the assembled r0 operator
-    # (rocSOLVER getrf once in the setup, getrs per V-cycle)
+    # multigrid.cc:448-455): the assembled r0 operator's free-dof block
+    # LU-factorised and inverted once in the setup (rocSOLVER getrf/getri),
+    # one GEMV over the FP32-stored inverse per V-cycle
     lu = {}
     try:
         mg_lu, _ = glsamd.build_gmg(meshes, cm, params, u, hist, weights, precision="f32",
@@ -271,7 +272,39 @@ def mg_companions(d, params, weights, n_ref, reps=20):
             t.append(e0.elapsed_time(e1))
         lu["ms"] = float(np.median(t))
         lu["coarse_dofs"] = meshes[0].n_dofs
+        lu["coarse_free_dofs"] = int(sum(((c >> k) & 1 == 0).sum() for c in [cm[0]]
+                                         for k in range(4)))
+        lu["inverse_storage"] = "f32 (FP64 sums), free dofs only"
+        y32 = torch.zeros_like(x)
+        mg_lu.vcycle(y32, b)
         del mg_lu
+        # the same with the FP64-stored inverse: time and the V-cycle's
+        # relative difference to the default FP32-stored inverse
+        os.environ["GLS_COARSE_INV_F32"] = "0"
+        try:
+            mg_lu, _ = glsamd.build_gmg(meshes, cm, params, u, hist, weights, precision="f32",
+                                        coarse_n_iterations=-1)
+            mg_lu.setup()
+            for _ in range(3):
+                mg_lu.vcycle(x, b)
+            torch.cuda.synchronize()
+            t = []
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                mg_lu.vcycle(x, b)
+                e1.record()
+                torch.cuda.synchronize()
+                t.append(e0.elapsed_time(e1))
+            y64 = torch.zeros_like(x)
+            mg_lu.vcycle(y64, b)
+            torch.cuda.synchronize()
+            lu["ms_inv_f64"] = float(np.median(t))
+            lu["inv_f32_rel_diff"] = float(torch.linalg.norm((y32 - y64).double()) /
+                                           torch.linalg.norm(y64.double()))
+            del mg_lu
+        finally:
+            os.environ.pop("GLS_COARSE_INV_F32")
     except Exception as e:  # reported, never fatal
         lu = {"error": str(e)}
     # GMRES: fixed 28 iterations (one restart cycle), wall time per iteration

@@ -468,10 +468,14 @@ struct glsMG_
   // dense LU coarse solver (coarse_n_iterations < 0): the substitute for the
   // reference's Trilinos direct solver (multigrid.cc:448-455, 477-481)
   rocblas_handle blas   = nullptr;
-  double        *d_lu   = nullptr; // [n0][n0] column major, LU factors
+  double        *d_lu   = nullptr; // [nf][nf] column major: LU factors, then the inverse
   rocblas_int   *d_ipiv = nullptr;
   rocblas_int   *d_info = nullptr;
-  double        *d_rhs  = nullptr; // [(2 + GEMV_CHUNKS) n0]: rhs | solution | partials
+  double        *d_rhs  = nullptr; // [(2 + GEMV_CHUNKS) nf]: rhs | solution | partials
+  int32_t       *d_free = nullptr; // [nf] the free (unconstrained) coarse dofs
+  int64_t        n_free = 0, ld_free = 0; // ld_free: nf rounded up to 4
+  float         *d_inv32 = nullptr; // [nf][nf] FP32 copy of the inverse (inv_f32)
+  bool           inv_f32 = false;
   // coarse GMRES (coarse_iterate): FP64 Krylov workspace, two level-
   // precision operand buffers, statistics of the last solve
   // finest-level FP64 defect for the fused copy_to_mg (mg_vcycle_device; null:
@@ -701,15 +705,17 @@ k_set_unit(T *x, int64_t j, int64_t n, int on)
     x[i] = on ? T(1) : T(0);
 }
 
-// y = M x for the dense coarse inverse (column major, n x n): the rows
-// split over threads (coalesced column reads) and the columns over
-// blockIdx.y chunks, partial sums reduced in a fixed order by k_gemv_sum;
-// with ~64 chunks the launch has enough waves to stream the matrix at HBM
-// rate (rocBLAS dgemv: 0.86 ms for the 2.2 GB inverse at n = 16,704)
+// y = M x for the dense coarse inverse (column major, n x n, FP64 or FP32
+// storage, FP64 sums): the rows split over threads (coalesced column reads)
+// and the columns over blockIdx.y chunks, partial sums reduced in a fixed
+// order by k_gemv_sum; with ~64 chunks the launch has enough waves to stream
+// the matrix at HBM rate (rocBLAS dgemv: 0.86 ms for the 2.2 GB inverse at
+// n = 16,704)
 constexpr int GEMV_CHUNKS = 64;
+template <typename TM>
 __global__ void __launch_bounds__(256)
-  k_gemv_part(const double *__restrict__ M, const double *__restrict__ x,
-              double *__restrict__ part, int64_t n)
+  k_gemv_part(const TM *__restrict__ M, const double *__restrict__ x,
+              double *__restrict__ part, int64_t n, int64_t ld)
 {
   const int64_t i  = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t cw = (n + GEMV_CHUNKS - 1) / GEMV_CHUNKS;
@@ -720,61 +726,168 @@ __global__ void __launch_bounds__(256)
   int64_t j  = j0;
   for (; j + 4 <= j1; j += 4)
     {
-      s0 += M[j * n + i] * x[j];
-      s1 += M[(j + 1) * n + i] * x[j + 1];
-      s2 += M[(j + 2) * n + i] * x[j + 2];
-      s3 += M[(j + 3) * n + i] * x[j + 3];
+      s0 += (double)M[j * n + i] * x[j];
+      s1 += (double)M[(j + 1) * n + i] * x[j + 1];
+      s2 += (double)M[(j + 2) * n + i] * x[j + 2];
+      s3 += (double)M[(j + 3) * n + i] * x[j + 3];
     }
   for (; j < j1; ++j)
-    s0 += M[j * n + i] * x[j];
-  part[blockIdx.y * n + i] = (s0 + s1) + (s2 + s3);
+    s0 += (double)M[j * n + i] * x[j];
+  part[blockIdx.y * ld + i] = (s0 + s1) + (s2 + s3);
 }
 
+// the FP32-stored inverse (leading dimension ld, a multiple of 4, padded
+// rows zero): one thread per 4 consecutive rows, 16-byte column reads
+__global__ void __launch_bounds__(256)
+  k_gemv_part_f32x4(const float4 *__restrict__ M, const double *__restrict__ x,
+                    double *__restrict__ part, int64_t n, int64_t ld)
+{
+  const int64_t r  = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; // rows 4r .. 4r+3
+  const int64_t l4 = ld / 4;
+  const int64_t cw = (n + GEMV_CHUNKS - 1) / GEMV_CHUNKS;
+  const int64_t j0 = blockIdx.y * cw, j1 = j0 + cw < n ? j0 + cw : n;
+  if (r >= l4)
+    return;
+  // eight 16-byte column reads in flight per thread (the 0.8 GB inverse
+  // streams from HBM: bytes in flight, not arithmetic, set the rate)
+  double  a[2][4] = {};
+  int64_t j       = j0;
+  for (; j + 8 <= j1; j += 8)
+    {
+      float4 m[8];
+      double xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        m[u] = M[(j + u) * l4 + r];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        xv[u] = x[j + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        {
+          a[u & 1][0] += (double)m[u].x * xv[u];
+          a[u & 1][1] += (double)m[u].y * xv[u];
+          a[u & 1][2] += (double)m[u].z * xv[u];
+          a[u & 1][3] += (double)m[u].w * xv[u];
+        }
+    }
+  for (; j < j1; ++j)
+    {
+      const float4 m0 = M[j * l4 + r];
+      const double x0 = x[j];
+      a[0][0] += (double)m0.x * x0;
+      a[0][1] += (double)m0.y * x0;
+      a[0][2] += (double)m0.z * x0;
+      a[0][3] += (double)m0.w * x0;
+    }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    part[blockIdx.y * ld + 4 * r + k] = a[0][k] + a[1][k];
+}
+
+// y[free[i]] = sum of the chunk partials (leading dimension ld, fixed
+// order), converted to the level precision
+template <typename T>
 __global__ void
-k_gemv_sum(const double *__restrict__ part, double *__restrict__ y, int64_t n)
+k_gemv_sum(const double *__restrict__ part, T *__restrict__ y, const int32_t *__restrict__ free,
+           int64_t n, int64_t ld)
 {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n)
     return;
+  // eight independent partial loads per step, summed in a fixed order
   double s = 0;
-  for (int c = 0; c < GEMV_CHUNKS; ++c)
-    s += part[c * n + i];
-  y[i] = s;
+  for (int c = 0; c < GEMV_CHUNKS; c += 8)
+    {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = part[(c + u) * ld + i];
+      s += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+    }
+  y[free[i]] = (T)s;
 }
 
-// Assemble the coarse level operator column by column (A e_j, including the
-// identity rows of constrained dofs) into FP64 and LU-factorise it.
+// out[i] = in[free[i]] (FP64): the free rows of an assembled column, or the
+// free entries of the coarse right-hand side
+template <typename T>
+__global__ void
+k_gather_free(double *__restrict__ out, const T *__restrict__ in, const int32_t *__restrict__ free,
+              int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    out[i] = (double)in[free[i]];
+}
+
+// out (leading dimension ld >= n, padded rows zero) = in (n x n, column
+// major) rounded to FP32
+__global__ void
+k_narrow(float *__restrict__ out, const double *__restrict__ in, int64_t n, int64_t ld)
+{
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * ld)
+    return;
+  const int64_t j = e / ld, i = e - j * ld;
+  out[e] = i < n ? (float)in[j * n + i] : 0.0f;
+}
+
+// Assemble the coarse level operator into FP64 and LU-factorise it.  Only
+// the free (unconstrained) dofs take part: a constrained dof's row and
+// column of A are both the unit vector (identity rows of vmult, homogeneous
+// constraints read as 0), so A = diag(A_ff, I) in free / constrained order
+// and the direct solve is x_c = b_c, x_f = A_ff^{-1} b_f — the same solution
+// as the full matrix, on nf^2 instead of n^2 entries (Re3900 r0: 14,206 of
+// 16,704 dofs free, 1.61 instead of 2.23 GB).
 template <typename T>
 void
 coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
 {
   glsOp         op = mg->ops[0];
   const int64_t n  = op->n_dofs;
+  const int     nc = op->dim + 1;
   if (n > 40000)
     throw std::runtime_error("dense LU coarse solver: coarse level too large");
+  std::vector<int32_t> freel;
+  freel.reserve((size_t)n);
+  for (int64_t d = 0; d < n; ++d)
+    if (!((op->h_cmask[(size_t)(d / nc)] >> (d % nc)) & 1))
+      freel.push_back((int32_t)d);
+  const int64_t nf = (int64_t)freel.size();
+  if (nf == 0)
+    throw std::runtime_error("dense LU coarse solver: no free coarse dofs");
   if (!mg->blas)
     check_blas(rocblas_create_handle(&mg->blas), "rocblas_create_handle");
   check_blas(rocblas_set_stream(mg->blas, s), "rocblas_set_stream");
   if (!mg->d_lu)
     {
-      HIP_THROW(hipMalloc((void **)&mg->d_lu, (size_t)n * n * sizeof(double)));
-      HIP_THROW(hipMalloc((void **)&mg->d_ipiv, (size_t)n * sizeof(rocblas_int)));
+      HIP_THROW(hipMalloc((void **)&mg->d_lu, (size_t)nf * nf * sizeof(double)));
+      HIP_THROW(hipMalloc((void **)&mg->d_ipiv, (size_t)nf * sizeof(rocblas_int)));
       HIP_THROW(hipMalloc((void **)&mg->d_info, sizeof(rocblas_int)));
-      HIP_THROW(hipMalloc((void **)&mg->d_rhs, (size_t)(2 + GEMV_CHUNKS) * n * sizeof(double)));
+      mg->ld_free = (nf + 3) / 4 * 4;
+      HIP_THROW(hipMalloc((void **)&mg->d_rhs,
+                          (size_t)(2 + GEMV_CHUNKS) * mg->ld_free * sizeof(double)));
+      HIP_THROW(hipMalloc((void **)&mg->d_free, (size_t)nf * sizeof(int32_t)));
+      mg->n_free = nf;
     }
+  if (mg->n_free != nf)
+    throw std::runtime_error("dense LU coarse solver: constrained dofs changed");
+  HIP_THROW(hipMemcpyAsync(mg->d_free, freel.data(), (size_t)nf * sizeof(int32_t),
+                           hipMemcpyHostToDevice, s));
   T *e = (T *)mg->sol[0], *col = (T *)mg->tmp[0];
   HIP_THROW(hipMemsetAsync(e, 0, n * sizeof(T), s));
-  for (int64_t j = 0; j < n; ++j)
+  for (int64_t j = 0; j < nf; ++j)
     {
-      hipLaunchKernelGGL(k_set_unit<T>, g1(n), dim3(256), 0, s, e, j, n, 1);
+      const int64_t dj = freel[(size_t)j];
+      hipLaunchKernelGGL(k_set_unit<T>, g1(n), dim3(256), 0, s, e, dj, n, 1);
       gls::op_vmult_device(op, col, e, s);
-      hipLaunchKernelGGL((k_convert<T, double>), g1(n), dim3(256), 0, s,
-                         mg->d_lu + (size_t)j * n, col, n);
-      hipLaunchKernelGGL(k_set_unit<T>, g1(n), dim3(256), 0, s, e, j, n, 0);
+      hipLaunchKernelGGL(k_gather_free<T>, g1(nf), dim3(256), 0, s, mg->d_lu + (size_t)j * nf,
+                         (const T *)col, (const int32_t *)mg->d_free, nf);
+      hipLaunchKernelGGL(k_set_unit<T>, g1(n), dim3(256), 0, s, e, dj, n, 0);
     }
   HIP_THROW(hipGetLastError());
-  check_blas(rocsolver_dgetrf(mg->blas, (rocblas_int)n, (rocblas_int)n, mg->d_lu,
-                              (rocblas_int)n, mg->d_ipiv, mg->d_info),
+  check_blas(rocsolver_dgetrf(mg->blas, (rocblas_int)nf, (rocblas_int)nf, mg->d_lu,
+                              (rocblas_int)nf, mg->d_ipiv, mg->d_info),
              "rocsolver_dgetrf");
   rocblas_int info = 0;
   HIP_THROW(hipMemcpyAsync(&info, mg->d_info, sizeof(info), hipMemcpyDeviceToHost, s));
@@ -783,10 +896,10 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
     throw std::runtime_error("dense LU coarse solver: singular coarse matrix (info " +
                              std::to_string(info) + ")");
   // the inverse from the LU factors, once: every coarse solve is then one
-  // GEMV streaming the n x n matrix at HBM rate (the two triangular solves
+  // GEMV streaming the nf x nf matrix at HBM rate (the two triangular solves
   // of getrs ran 33.7 ms per V-cycle at n = 16,704 on MI355X; the GEMV,
-  // k_gemv_part, streams the 2.2 GB matrix instead)
-  check_blas(rocsolver_dgetri(mg->blas, (rocblas_int)n, mg->d_lu, (rocblas_int)n, mg->d_ipiv,
+  // k_gemv_part, streams the matrix instead)
+  check_blas(rocsolver_dgetri(mg->blas, (rocblas_int)nf, mg->d_lu, (rocblas_int)nf, mg->d_ipiv,
                               mg->d_info),
              "rocsolver_dgetri");
   HIP_THROW(hipMemcpyAsync(&info, mg->d_info, sizeof(info), hipMemcpyDeviceToHost, s));
@@ -794,21 +907,46 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
   if (info != 0)
     throw std::runtime_error("dense LU coarse solver: singular coarse matrix in getri (info " +
                              std::to_string(info) + ")");
+  // FP32 levels keep an FP32 copy of the inverse (FP64 sums): half the bytes
+  // per coarse solve; the Re3900 r0..r2 V-cycle differs from the FP64-stored
+  // inverse's by 2.1e-7 (relative l2), the FP32 level arithmetic's own
+  // round-off.  GLS_COARSE_INV_F32=0 keeps the FP64 inverse.
+  const char *e32 = getenv("GLS_COARSE_INV_F32");
+  mg->inv_f32     = !(e32 && e32[0] == '0') && mg->prec == GLS_F32;
+  if (mg->inv_f32)
+    {
+      const int64_t ld = mg->ld_free;
+      if (!mg->d_inv32)
+        HIP_THROW(hipMalloc((void **)&mg->d_inv32, (size_t)nf * ld * sizeof(float)));
+      hipLaunchKernelGGL(k_narrow, g1(nf * ld), dim3(256), 0, s, mg->d_inv32,
+                         (const double *)mg->d_lu, nf, ld);
+      HIP_THROW(hipGetLastError());
+    }
 }
 
 template <typename T>
 void
 coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
 {
-  const int64_t n = mg->ops[0]->n_dofs;
-  hipLaunchKernelGGL((k_convert<T, double>), g1(n), dim3(256), 0, s, mg->d_rhs,
-                     (const T *)mg->def[0], n);
-  hipLaunchKernelGGL(k_gemv_part, dim3((unsigned)((n + 255) / 256), GEMV_CHUNKS), dim3(256), 0,
-                     s, (const double *)mg->d_lu, (const double *)mg->d_rhs, mg->d_rhs + 2 * n, n);
-  hipLaunchKernelGGL(k_gemv_sum, g1(n), dim3(256), 0, s, (const double *)(mg->d_rhs + 2 * n),
-                     mg->d_rhs + n, n);
-  hipLaunchKernelGGL((k_convert<double, T>), g1(n), dim3(256), 0, s, (T *)mg->sol[0],
-                     mg->d_rhs + n, n);
+  const int64_t n = mg->ops[0]->n_dofs, nf = mg->n_free;
+  // constrained dofs: x_c = b_c (their rows of A are the identity)
+  const int64_t w = n * (int64_t)sizeof(T) / 4;
+  hipLaunchKernelGGL(k_copy, g1(w), dim3(256), 0, s, (uint32_t *)mg->sol[0],
+                     (const uint32_t *)mg->def[0], w);
+  hipLaunchKernelGGL(k_gather_free<T>, g1(nf), dim3(256), 0, s, mg->d_rhs,
+                     (const T *)mg->def[0], (const int32_t *)mg->d_free, nf);
+  const int64_t ld = mg->ld_free;
+  double       *part = mg->d_rhs + 2 * ld;
+  if (mg->inv_f32)
+    hipLaunchKernelGGL(k_gemv_part_f32x4, dim3((unsigned)((ld / 4 + 255) / 256), GEMV_CHUNKS),
+                       dim3(256), 0, s, (const float4 *)mg->d_inv32, (const double *)mg->d_rhs,
+                       part, nf, ld);
+  else
+    hipLaunchKernelGGL(k_gemv_part<double>, dim3((unsigned)((nf + 255) / 256), GEMV_CHUNKS),
+                       dim3(256), 0, s, (const double *)mg->d_lu, (const double *)mg->d_rhs, part,
+                       nf, ld);
+  hipLaunchKernelGGL(k_gemv_sum<T>, g1(nf), dim3(256), 0, s, (const double *)part,
+                     (T *)mg->sol[0], (const int32_t *)mg->d_free, nf, ld);
   HIP_THROW(hipGetLastError());
 }
 
@@ -1342,7 +1480,7 @@ gls_mg_destroy(glsMG mg)
   for (hipEvent_t ev : mg->side_ev)
     (void)hipEventDestroy(ev);
   for (void *p : {(void *)mg->d_lu, (void *)mg->d_ipiv, (void *)mg->d_info, (void *)mg->d_rhs,
-                  (void *)mg->cg_ws, mg->cg_lvl})
+                  (void *)mg->d_free, (void *)mg->d_inv32, (void *)mg->cg_ws, mg->cg_lvl})
     if (p)
       (void)hipFree(p);
   if (mg->blas)

@@ -19,8 +19,11 @@ vel, p, slip = d.boundary_descriptor()
 cm = [m.constraint_mask(vel, p, slip) for m in meshes]
 params, w = d.operator_parameters(2.5e-4)
 u = gi.linearization_point(meshes[-1].n_nodes, 3, d.u_max)
+# argv[1]: coarse solver (10 relaxation sweeps by default; -1 = the deck's
+# direct solver, the dense free-dof inverse GEMV)
+coarse = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 mg, ops = glsamd.build_gmg(meshes, cm, params, u, gi.history(u, 2), w, precision="f32",
-                           coarse_n_iterations=10)
+                           coarse_n_iterations=coarse)
 b = ops[-1]._dev(gi.src_vector(meshes[-1].n_dofs)).double()
 x = torch.empty_like(b)
 for _ in range(3):

@@ -61,6 +61,7 @@ def test_transfer(name, n_ref):
 
 @pytest.mark.parametrize("name,n_ref,coarse", [
     ("input_turek_2D_Re20_stat.json", 2, -1),   # dense LU coarse solve ("direct")
+    ("input_turek_2D_Re100.json", 2, -1),       # direct, a third of the coarse dofs constrained
     ("input_turek_2D_Re20_stat.json", 2, 0),    # identity coarse solve
     ("input_hoffmann_3D_Re3900.json", 1, 10),   # relaxation sweeps
 ])
