@@ -1528,9 +1528,12 @@ gls_mg_setup(glsMG mg, void *stream)
   HIP_THROW(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
   HIP_THROW(hipEventRecord(fork, s));
   std::vector<char> estimate(nl, 0);
-  for (size_t l = 0; l < nl; ++l)
+  // enqueued finest level first: its kernels (the longest chain) start while
+  // the host is still enqueueing the coarser levels' ~100 short launches each
+  for (size_t li = nl; li-- > 0;)
     {
-      hipStream_t ls = mg->side[l];
+      const size_t l  = li;
+      hipStream_t  ls = mg->side[l];
       HIP_THROW(hipStreamWaitEvent(ls, fork, 0));
       // compute_inverse_diagonal (multigrid.cc:290-293)
       gls::op_inverse_diagonal_device(mg->ops[l], mg->invdiag[l], ls);
