@@ -1580,6 +1580,8 @@ gls_op_destroy(glsOp op)
   for (void *b : bufs)
     if (b)
       (void)hipFree(b);
+  if (op->gmres_host)
+    (void)hipHostFree(op->gmres_host);
   op->stage.release();
   gls::faces_release(op);
   delete op;

@@ -5,7 +5,8 @@
 // Every vector (the Krylov basis V, the preconditioned direction, the
 // solution) stays in HBM; per iteration only the j+1 Hessenberg entries and a
 // norm cross to the host (what deal.II's MPI_Allreduce of the dots returns on
-// every rank).  Orthogonalisation is classical Gram-Schmidt with one
+// every rank), and the next Arnoldi step is already enqueued while the host
+// waits for them (the device does not idle through the round trip).  Orthogonalisation is classical Gram-Schmidt with one
 // re-orthogonalisation (CGS2): two GEMVs over the contiguous basis per
 // iteration instead of j+1 dependent dot/axpy pairs — the same projector as
 // deal.II's modified Gram-Schmidt in exact arithmetic, and the stable choice
@@ -70,6 +71,18 @@ k_residual(double *__restrict__ r, const double *__restrict__ b, int64_t n)
     r[i] = b[i] - r[i];
 }
 
+// v = w / |w| with the norm read on the device (|w| = 0, the lucky
+// breakdown: v = 0, never used); the same 1/hn multiply as a host dscal
+__global__ void
+k_unit_col(double *__restrict__ v, const double *__restrict__ w, const double *__restrict__ hn,
+           int64_t n)
+{
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const double  h = *hn;
+  if (i < n)
+    v[i] = h > 0 ? w[i] * (1.0 / h) : 0.0;
+}
+
 dim3
 grid1(int64_t n)
 {
@@ -114,7 +127,9 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   // device and costs more than the solve's setup)
   HIP_THROW(hipSetDevice(op->device));
   rocblas_handle h  = blas_handle(op->device, s);
-  const size_t   ws = ((size_t)(m + 3) * n + 2 * (m + 1)) * sizeof(double);
+  // dh: the two CGS passes' coefficients and |w| (HC values, one D2H copy)
+  const int      HC = 2 * (m + 1) + 1;
+  const size_t   ws = ((size_t)(m + 3) * n + HC) * sizeof(double);
   if (op->gmres_ws_bytes < ws)
     {
       if (op->gmres_ws)
@@ -125,6 +140,17 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
         }
       HIP_THROW(hipMalloc(&op->gmres_ws, ws));
       op->gmres_ws_bytes = ws;
+    }
+  if (op->gmres_host_count < (size_t)(2 * HC))
+    {
+      if (op->gmres_host)
+        {
+          HIP_THROW(hipStreamSynchronize(s));
+          HIP_THROW(hipHostFree(op->gmres_host));
+          op->gmres_host = nullptr;
+        }
+      HIP_THROW(hipHostMalloc((void **)&op->gmres_host, 2 * HC * sizeof(double)));
+      op->gmres_host_count = 2 * HC;
     }
   struct View
   {
@@ -158,11 +184,50 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   const double tol   = std::max(desc->relative_tolerance * bnorm, desc->absolute_tolerance);
   HIP_THROW(hipMemsetAsync(x, 0, n * sizeof(double), s));
 
-  std::vector<double> H((size_t)(m + 1) * m), g(m + 1), cs(m), sn(m), hc(2 * (m + 1)), y(m);
+  std::vector<double> H((size_t)(m + 1) * m), g(m + 1), cs(m), sn(m), y(m);
   int    it    = 0;
   double res   = bnorm; // x = 0: r = b
   bool   conv  = res <= tol;
   int    n_rst = 0;
+  // Arnoldi step j, enqueued only: w = A M^{-1} v_j, CGS2 (h = V^T w;
+  // w -= V h; twice), |w| on the device, the Hessenberg column to pinned
+  // host buffer j % 2 (event ev[j % 2]), v_{j+1} = w / |w|
+  struct Events
+  {
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ~Events()
+    {
+      for (hipEvent_t x : e)
+        if (x)
+          (void)hipEventDestroy(x);
+    }
+  } evs;
+  hipEvent_t *ev = evs.e;
+  for (int i = 0; i < 2; ++i)
+    HIP_THROW(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+  auto arnoldi = [&](int j) {
+    precondition(z.d(), vcol(j));
+    gls::op_vmult_device(op, w.d(), z.d(), s);
+    const double one = 1.0, zero = 0.0, mone = -1.0;
+    for (int pass = 0; pass < 2; ++pass)
+      {
+        double *hp = dh.d() + pass * (m + 1);
+        RB_THROW(rocblas_dgemv(h, rocblas_operation_transpose, (rocblas_int)n, j + 1, &one, V.d(),
+                               (rocblas_int)n, w.d(), 1, &zero, hp, 1));
+        RB_THROW(rocblas_dgemv(h, rocblas_operation_none, (rocblas_int)n, j + 1, &mone, V.d(),
+                               (rocblas_int)n, hp, 1, &one, w.d(), 1));
+      }
+    double *hn = dh.d() + 2 * (m + 1);
+    RB_THROW(rocblas_set_pointer_mode(h, rocblas_pointer_mode_device));
+    RB_THROW(rocblas_dnrm2(h, (rocblas_int)n, w.d(), 1, hn));
+    RB_THROW(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host));
+    HIP_THROW(hipMemcpyAsync(op->gmres_host + (j % 2) * HC, dh.d(), HC * sizeof(double),
+                             hipMemcpyDeviceToHost, s));
+    HIP_THROW(hipEventRecord(ev[j % 2], s));
+    hipLaunchKernelGGL(k_unit_col, grid1(n), dim3(256), 0, s, vcol(j + 1), (const double *)w.d(),
+                       (const double *)hn, n);
+    HIP_THROW(hipGetLastError());
+  };
   // r (in column 0 of V) = b - A x
   HIP_THROW(hipMemcpyAsync(vcol(0), b, n * sizeof(double), hipMemcpyDeviceToDevice, s));
   while (!conv && it < desc->max_iterations)
@@ -175,36 +240,23 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
       std::fill(g.begin(), g.end(), 0.0);
       g[0]   = beta;
       int jd = 0; // columns of this cycle
+      // software pipeline: step j + 1 is enqueued before the host waits for
+      // step j's Hessenberg column, so the device never idles through the
+      // host round trip; when step j converges, the enqueued step j + 1 runs
+      // to completion and is discarded (its basis column is never used)
+      if (m > 0)
+        arnoldi(0);
       for (int j = 0; j < m && it < desc->max_iterations; ++j)
         {
-          // w = A M^{-1} v_j
-          precondition(z.d(), vcol(j));
-          gls::op_vmult_device(op, w.d(), z.d(), s);
-          // CGS2: h = V^T w; w -= V h; twice
-          const double one = 1.0, zero = 0.0, mone = -1.0;
-          for (int pass = 0; pass < 2; ++pass)
-            {
-              double *hp = dh.d() + pass * (m + 1);
-              RB_THROW(rocblas_dgemv(h, rocblas_operation_transpose, (rocblas_int)n, j + 1, &one,
-                                     V.d(), (rocblas_int)n, w.d(), 1, &zero, hp, 1));
-              RB_THROW(rocblas_dgemv(h, rocblas_operation_none, (rocblas_int)n, j + 1, &mone,
-                                     V.d(), (rocblas_int)n, hp, 1, &one, w.d(), 1));
-            }
-          HIP_THROW(hipMemcpyAsync(hc.data(), dh.d(), 2 * (m + 1) * sizeof(double),
-                                   hipMemcpyDeviceToHost, s));
-          const double hn = nrm2(w.d()); // host pointer mode: waits for the stream
-          HIP_THROW(hipStreamSynchronize(s)); // and the D2H copy of hc
-          double      *Hj = &H[(size_t)j * (m + 1)];
+          if (j + 1 < m && it + 1 < desc->max_iterations)
+            arnoldi(j + 1);
+          HIP_THROW(hipEventSynchronize(ev[j % 2]));
+          const double *hc = op->gmres_host + (j % 2) * HC;
+          const double  hn = hc[2 * (m + 1)];
+          double       *Hj = &H[(size_t)j * (m + 1)];
           for (int i = 0; i <= j; ++i)
             Hj[i] = hc[i] + hc[(m + 1) + i];
           Hj[j + 1] = hn;
-          if (hn > 0)
-            {
-              const double sc = 1.0 / hn;
-              HIP_THROW(hipMemcpyAsync(vcol(j + 1), w.d(), n * sizeof(double),
-                                       hipMemcpyDeviceToDevice, s));
-              RB_THROW(rocblas_dscal(h, (rocblas_int)n, &sc, vcol(j + 1), 1));
-            }
           // Givens rotations on the new Hessenberg column
           for (int i = 0; i < j; ++i)
             {

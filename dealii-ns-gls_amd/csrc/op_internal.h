@@ -111,6 +111,9 @@ struct glsOp_
   // gls_gmres_solve workspace (Krylov basis and vectors), grown on demand
   void     *gmres_ws       = nullptr;
   size_t    gmres_ws_bytes = 0;
+  // pinned host staging of the per-iteration Hessenberg column (two buffers)
+  double   *gmres_host       = nullptr;
+  size_t    gmres_host_count = 0;
 
   // brick decomposition (csrc/brick.h)
   bool      use_brick = false;
