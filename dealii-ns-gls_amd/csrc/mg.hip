@@ -736,53 +736,67 @@ __global__ void __launch_bounds__(256)
   part[blockIdx.y * ld + i] = (s0 + s1) + (s2 + s3);
 }
 
-// the FP32-stored inverse (leading dimension ld, a multiple of 4, padded
-// rows zero): one thread per 4 consecutive rows, 16-byte column reads
+// The FP32-stored inverse, row major (row stride ld, a multiple of 4,
+// padded columns zero): one wavefront per row streams the row as 16-byte
+// loads (contiguous), x (FP32, the coarse defect's free entries: exact for
+// FP32 levels) from L2, FP64 sums in a fixed order (lane partials, then a
+// fixed shuffle tree), and writes y[free[row]] itself: no partial-sum pass.
+template <typename T>
 __global__ void __launch_bounds__(256)
-  k_gemv_part_f32x4(const float4 *__restrict__ M, const double *__restrict__ x,
-                    double *__restrict__ part, int64_t n, int64_t ld)
+  k_gemv_rows_f32(const float4 *__restrict__ M, const float4 *__restrict__ x,
+                  T *__restrict__ y, const int32_t *__restrict__ free, int64_t n, int64_t ld)
 {
-  const int64_t r  = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; // rows 4r .. 4r+3
-  const int64_t l4 = ld / 4;
-  const int64_t cw = (n + GEMV_CHUNKS - 1) / GEMV_CHUNKS;
-  const int64_t j0 = blockIdx.y * cw, j1 = j0 + cw < n ? j0 + cw : n;
-  if (r >= l4)
+  const int64_t row  = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int     lane = threadIdx.x & 63;
+  if (row >= n)
     return;
-  // eight 16-byte column reads in flight per thread (the 0.8 GB inverse
-  // streams from HBM: bytes in flight, not arithmetic, set the rate)
-  double  a[2][4] = {};
-  int64_t j       = j0;
-  for (; j + 8 <= j1; j += 8)
+  const int64_t l4 = ld / 4;
+  const float4 *mr = M + row * l4;
+  double        a0 = 0, a1 = 0;
+  int64_t       c  = lane;
+  // four 16-byte row loads in flight per lane
+  for (; c + 192 < l4; c += 256)
     {
-      float4 m[8];
-      double xv[8];
+      float4 m[4], xv[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        m[u] = M[(j + u) * l4 + r];
+      for (int u = 0; u < 4; ++u)
+        m[u] = mr[c + 64 * u];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        xv[u] = x[j + u];
+      for (int u = 0; u < 4; ++u)
+        xv[u] = x[c + 64 * u];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < 4; ++u)
         {
-          a[u & 1][0] += (double)m[u].x * xv[u];
-          a[u & 1][1] += (double)m[u].y * xv[u];
-          a[u & 1][2] += (double)m[u].z * xv[u];
-          a[u & 1][3] += (double)m[u].w * xv[u];
+          a0 += (double)m[u].x * (double)xv[u].x + (double)m[u].y * (double)xv[u].y;
+          a1 += (double)m[u].z * (double)xv[u].z + (double)m[u].w * (double)xv[u].w;
         }
     }
-  for (; j < j1; ++j)
+  for (; c < l4; c += 64)
     {
-      const float4 m0 = M[j * l4 + r];
-      const double x0 = x[j];
-      a[0][0] += (double)m0.x * x0;
-      a[0][1] += (double)m0.y * x0;
-      a[0][2] += (double)m0.z * x0;
-      a[0][3] += (double)m0.w * x0;
+      const float4 m0 = mr[c], x0 = x[c];
+      a0 += (double)m0.x * (double)x0.x + (double)m0.y * (double)x0.y;
+      a1 += (double)m0.z * (double)x0.z + (double)m0.w * (double)x0.w;
     }
+  double v = a0 + a1;
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    part[blockIdx.y * ld + 4 * r + k] = a[0][k] + a[1][k];
+  for (int off = 32; off > 0; off >>= 1)
+    v += __shfl_down(v, off);
+  if (lane == 0)
+    y[free[row]] = (T)v;
+}
+
+// coarse solve prologue for the row GEMV: sol = def on every dof (the
+// constrained rows keep it), xf[i] = def[free[i]] in FP32 (padded to ld)
+template <typename T>
+__global__ void
+k_coarse_prep(T *__restrict__ sol, const T *__restrict__ def, float *__restrict__ xf,
+              const int32_t *__restrict__ free, int64_t n, int64_t nf, int64_t ld)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    sol[i] = def[i];
+  if (i < ld)
+    xf[i] = i < nf ? (float)def[free[i]] : 0.0f;
 }
 
 // y[free[i]] = sum of the chunk partials (leading dimension ld, fixed
@@ -820,16 +834,17 @@ k_gather_free(double *__restrict__ out, const T *__restrict__ in, const int32_t 
     out[i] = (double)in[free[i]];
 }
 
-// out (leading dimension ld >= n, padded rows zero) = in (n x n, column
-// major) rounded to FP32
+// out = in^T rounded to FP32, row major with row stride ld >= n (padded
+// columns zero): in is the n x n column-major inverse, so out's row i is
+// in's row i (setup only; the strided reads do not matter)
 __global__ void
 k_narrow(float *__restrict__ out, const double *__restrict__ in, int64_t n, int64_t ld)
 {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n * ld)
     return;
-  const int64_t j = e / ld, i = e - j * ld;
-  out[e] = i < n ? (float)in[j * n + i] : 0.0f;
+  const int64_t i = e / ld, j = e - i * ld; // row i, column j
+  out[e] = j < n ? (float)in[j * n + i] : 0.0f;
 }
 
 // Assemble the coarse level operator into FP64 and LU-factorise it.  Only
@@ -928,23 +943,30 @@ template <typename T>
 void
 coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
 {
-  const int64_t n = mg->ops[0]->n_dofs, nf = mg->n_free;
+  const int64_t n = mg->ops[0]->n_dofs, nf = mg->n_free, ld = mg->ld_free;
+  if (mg->inv_f32)
+    {
+      // sol = def (constrained dofs: x_c = b_c, their rows of A are the
+      // identity), then sol[free] = A_ff^{-1} def[free], one wave per row
+      float *xf = reinterpret_cast<float *>(mg->d_rhs);
+      hipLaunchKernelGGL(k_coarse_prep<T>, g1(std::max(n, ld)), dim3(256), 0, s, (T *)mg->sol[0],
+                         (const T *)mg->def[0], xf, (const int32_t *)mg->d_free, n, nf, ld);
+      hipLaunchKernelGGL(k_gemv_rows_f32<T>, dim3((unsigned)((nf + 3) / 4)), dim3(256), 0, s,
+                         (const float4 *)mg->d_inv32, (const float4 *)xf, (T *)mg->sol[0],
+                         (const int32_t *)mg->d_free, nf, ld);
+      HIP_THROW(hipGetLastError());
+      return;
+    }
   // constrained dofs: x_c = b_c (their rows of A are the identity)
   const int64_t w = n * (int64_t)sizeof(T) / 4;
   hipLaunchKernelGGL(k_copy, g1(w), dim3(256), 0, s, (uint32_t *)mg->sol[0],
                      (const uint32_t *)mg->def[0], w);
   hipLaunchKernelGGL(k_gather_free<T>, g1(nf), dim3(256), 0, s, mg->d_rhs,
                      (const T *)mg->def[0], (const int32_t *)mg->d_free, nf);
-  const int64_t ld = mg->ld_free;
-  double       *part = mg->d_rhs + 2 * ld;
-  if (mg->inv_f32)
-    hipLaunchKernelGGL(k_gemv_part_f32x4, dim3((unsigned)((ld / 4 + 255) / 256), GEMV_CHUNKS),
-                       dim3(256), 0, s, (const float4 *)mg->d_inv32, (const double *)mg->d_rhs,
-                       part, nf, ld);
-  else
-    hipLaunchKernelGGL(k_gemv_part<double>, dim3((unsigned)((nf + 255) / 256), GEMV_CHUNKS),
-                       dim3(256), 0, s, (const double *)mg->d_lu, (const double *)mg->d_rhs, part,
-                       nf, ld);
+  double *part = mg->d_rhs + 2 * ld;
+  hipLaunchKernelGGL(k_gemv_part<double>, dim3((unsigned)((nf + 255) / 256), GEMV_CHUNKS),
+                     dim3(256), 0, s, (const double *)mg->d_lu, (const double *)mg->d_rhs, part,
+                     nf, ld);
   hipLaunchKernelGGL(k_gemv_sum<T>, g1(nf), dim3(256), 0, s, (const double *)part,
                      (T *)mg->sol[0], (const int32_t *)mg->d_free, nf, ld);
   HIP_THROW(hipGetLastError());
