@@ -332,11 +332,13 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   hipEvent_t *ev = evs.e;
   for (int i = 0; i < 2; ++i)
     HIP_THROW(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
-  auto arnoldi = [&](int j) {
+  // GLS_GMRES_ROCBLAS=1: the rocBLAS GEMV orthogonalisation at every length
+  static const bool force_rocblas = getenv_flag("GLS_GMRES_ROCBLAS");
+  auto              arnoldi       = [&](int j) {
     precondition(z.d(), vcol(j));
     gls::op_vmult_device(op, w.d(), z.d(), s);
     double *hn = dh.d() + 2 * (m + 1);
-    if (j + 1 <= CGS_MAXJ && !getenv_flag("GLS_GMRES_ROCBLAS"))
+    if (j + 1 <= CGS_MAXJ && !force_rocblas)
       {
         // fused CGS2: dots, update + dots, update + norm (three basis passes)
         const int J = j + 1;
