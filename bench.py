@@ -455,9 +455,69 @@ def dist_gmres_companion(d, params, weights, n_ref, dist, rank, world, reps=10):
                         "all-reduced CGS2, host-driven, wall clock max over ranks"}}
 
 
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset, N > 1): start
+    N ranks as ONE child process `python -m torch.distributed.run
+    --nproc-per-node N ... bench.py <same arguments>` (the reference's
+    `mpirun -np N`, input_hoffmann_2D_ReInf_3D.sh:8), relay rank 0's JSON line
+    and exit with the child's status.  Called before anything touches the GPU;
+    never exec's (the child is a subprocess).  A line whose n_gpus differs
+    from N fails the run."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", str(max(1, min(16, (os.cpu_count() or 1) // args.gpus))))
+    log(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}")
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip().startswith("{")]
+    if not lines:
+        log(f"[bench] launcher: no JSON line from the ranks (exit {p.returncode})")
+        return p.returncode or 5
+    line = lines[-1]
+    try:
+        n = json.loads(line).get("n_gpus")
+    except ValueError:
+        n = None
+    print(line, flush=True)
+    if n != args.gpus:
+        log(f"[bench] launcher: n_gpus {n} in the line differs from --gpus {args.gpus}")
+        return p.returncode or 6
+    return p.returncode
+
+
+def dry_run(args, out_fd):
+    """--dry-run: the launch plumbing without the GPU (CPU tests): every rank
+    joins a gloo group, checks WORLD_SIZE == --gpus, all-reduces its rank, and
+    rank 0 prints a JSON line of the bench's shape with n_gpus = world."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.tensor([float(rank)])
+        dist.all_reduce(t)
+        assert float(t) == world * (world - 1) / 2
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": 0.0, "unit": "DoF/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "dry_run": True}),
+              file=out_fd, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch plumbing only (gloo, no GPU): the CPU test of --gpus N")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--nref", type=int, default=None)
@@ -477,14 +537,22 @@ def main():
                     help="multi-GPU: on a native/P2P mismatch time the torch P2P path "
                          "instead of failing")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and (world > 1 or args.gpus > 1):
+        log(f"[bench] WORLD_SIZE {world} differs from --gpus {args.gpus}")
+        sys.exit(2)
     # stdout carries exactly one JSON line: everything else the process or
     # its libraries write to fd 1 (RCCL's version banner, ...) goes to stderr
     out_fd = os.fdopen(os.dup(1), "w")
     sys.stdout.flush()
     os.dup2(2, 1)
+    if args.dry_run:
+        dry_run(args, out_fd)
+        return
 
     import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
