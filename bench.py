@@ -273,6 +273,9 @@ def mg_companions(d, params, weights, n_ref, reps=20):
         mg_lu.setup()
         torch.cuda.synchronize()
         lu["setup_ms"] = (time.perf_counter() - t0) * 1e3
+        # the dense coarse setup's parts: free block assembled from the
+        # element matrices (one launch + a scatter per cell colour), getrf, getri
+        lu["coarse_setup"] = mg_lu.coarse_setup_times()
         for _ in range(3):
             mg_lu.vcycle(x, b)
         torch.cuda.synchronize()

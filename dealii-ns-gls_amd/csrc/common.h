@@ -34,6 +34,28 @@ void set_error(const std::string &s);
     }                                             \
   return 0;
 
+// the caller's current device switched to `device` for a scope and restored
+// on every exit path (C-ABI calls that allocate or launch on an operator's
+// device leave the caller's device as they found it)
+struct DeviceScope
+{
+  int prev = -1;
+  explicit DeviceScope(int device)
+  {
+    HIP_THROW(hipGetDevice(&prev));
+    if (prev != device)
+      HIP_THROW(hipSetDevice(device));
+  }
+  ~DeviceScope()
+  {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev)
+      (void)hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope &)            = delete;
+  DeviceScope &operator=(const DeviceScope &) = delete;
+};
+
 enum
 {
   BRICK_RUN    = 1,

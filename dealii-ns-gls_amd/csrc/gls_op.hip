@@ -2026,6 +2026,19 @@ op_inverse_diagonal_device(glsOp op, void *diag, hipStream_t s)
                        op->d_cbits, op->n_owned_dofs, op->n_dofs);
   HIP_THROW(hipGetLastError());
 }
+
+void
+op_element_matrices_device(const glsOp_ *op, void *emat, int64_t b, int64_t e, hipStream_t s)
+{
+  if (!op->have_lin)
+    throw std::runtime_error("element matrices before set_linearization_point");
+  EmatFn fn = op->prec == GLS_F64 ? select_emat_t<double>(op->dim, op->degree) :
+                                    select_emat_t<float>(op->dim, op->degree);
+  if (!fn)
+    throw std::runtime_error("no kernel instantiation for this (dim, degree)");
+  fn(op, vmult_mode(op), emat, b, e, s);
+  faces_element_matrices(op, emat, b, e, s);
+}
 } // namespace gls
 
 extern "C" {

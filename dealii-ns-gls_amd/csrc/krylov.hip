@@ -240,6 +240,11 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
                              "solve needs all-reduced dots)");
   if (desc->max_n_tmp_vectors < 3)
     throw std::runtime_error("gls_gmres_solve: max_n_tmp_vectors must be >= 3");
+  if (mg)
+    gls::mg_check_outer(mg, op); // FP64 outer vectors of op's size, set up
+  // the operator's device for the whole solve (staging buffers included),
+  // the caller's current device restored on return
+  gls::DeviceScope dev(op->device);
   hipStream_t    s = (hipStream_t)stream;
   const int64_t  n = op->n_dofs;
   // deal.II SolverGMRES restarts after max_n_tmp_vectors - 2 iterations
@@ -252,7 +257,6 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   // [V (m+1) n | w n | z n | dh 2 (m+1)] kept on the operator and grown on
   // demand (a hipMalloc/hipFree of the basis per solve synchronises the
   // device and costs more than the solve's setup)
-  HIP_THROW(hipSetDevice(op->device));
   rocblas_handle h  = blas_handle(op->device, s);
   // dh: the two CGS passes' coefficients and |w| (HC values, one D2H copy)
   const int      HC = 2 * (m + 1) + 1;

@@ -17,6 +17,9 @@
 #include "kernels.h"
 #include "op_internal.h"
 
+#include <chrono>
+#include <string>
+
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 
@@ -476,6 +479,9 @@ struct glsMG_
   int64_t        n_free = 0, ld_free = 0; // ld_free: nf rounded up to 4
   float         *d_inv32 = nullptr; // [nf][nf] FP32 copy of the inverse (inv_f32)
   bool           inv_f32 = false;
+  // last dense-coarse setup: assembly / getrf / getri wall ms, cell colours
+  double         coarse_setup_ms[3] = {0, 0, 0};
+  int            coarse_colors      = 0;
   // coarse GMRES (coarse_iterate): FP64 Krylov workspace, two level-
   // precision operand buffers, statistics of the last solve
   // finest-level FP64 defect for the fused copy_to_mg (mg_vcycle_device; null:
@@ -847,6 +853,114 @@ k_narrow(float *__restrict__ out, const double *__restrict__ in, int64_t n, int6
   out[e] = j < n ? (float)in[j * n + i] : 0.0f;
 }
 
+// A_ff[fj][fi] += E[c][j][i] over the cells of one colour (no two of them
+// share a node, so no two threads of a launch touch the same entry): the
+// element matrices scattered into the column-major free-dof block, the
+// colours in a fixed order (deterministic sums)
+template <typename T>
+__global__ void
+k_scatter_emat(double *__restrict__ A, int64_t nf, const T *__restrict__ E,
+               const int32_t *__restrict__ cdof, const int32_t *__restrict__ cells,
+               int64_t n_cells, int ndof)
+{
+  const int64_t per = (int64_t)ndof * ndof;
+  const int64_t g   = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_cells * per)
+    return;
+  const int64_t ci = g / per;
+  const int     r  = (int)(g - ci * per);
+  const int     j = r / ndof, i = r - j * ndof;
+  const int64_t c  = cells[ci];
+  const int32_t fi = cdof[c * ndof + i], fj = cdof[c * ndof + j];
+  if (fi < 0 || fj < 0)
+    return;
+  A[(size_t)fj * nf + fi] += (double)E[(size_t)c * per + r];
+}
+
+// A_ff from the element matrices of the coarse level operator (what the
+// reference's coarse direct solver factorises: get_system_matrix ->
+// MatrixFreeTools::compute_matrix, operator_ns.cc:1407-1430, assembled into
+// the Trilinos matrix, multigrid.cc:448-455): one element-matrix launch over
+// all coarse cells, then one scatter launch per cell colour (greedy colouring
+// on the host, cells of a colour share no node), summed in FP64
+template <typename T>
+void
+assemble_free_block(glsMG_ *mg, const std::vector<int32_t> &freel, hipStream_t s)
+{
+  glsOp         op   = mg->ops[0];
+  const int64_t n    = op->n_dofs, nf = (int64_t)freel.size(), nc_ = op->n_cells;
+  const int     nc   = op->dim + 1, nq = op->nq, ndof = nq * nc;
+  std::vector<int32_t> fidx((size_t)n, -1);
+  for (int64_t j = 0; j < nf; ++j)
+    fidx[(size_t)freel[(size_t)j]] = (int32_t)j;
+  // internal cell c -> free index of each local dof (-1: constrained)
+  std::vector<int32_t> cdof((size_t)nc_ * ndof);
+  std::vector<std::vector<int32_t>> node_cells((size_t)op->n_nodes);
+  for (int64_t c = 0; c < nc_; ++c)
+    {
+      const uint32_t *cn = &op->h_cell_nodes[(size_t)gls::ext_cell(op, c) * nq];
+      for (int p = 0; p < nq; ++p)
+        {
+          node_cells[cn[p]].push_back((int32_t)c);
+          for (int k = 0; k < nc; ++k)
+            cdof[(size_t)c * ndof + p * nc + k] = fidx[(size_t)cn[p] * nc + k];
+        }
+    }
+  // greedy colouring: the smallest colour no node-sharing neighbour has
+  std::vector<int> color((size_t)nc_, -1);
+  int              n_colors = 0;
+  std::vector<int> seen;
+  for (int64_t c = 0; c < nc_; ++c)
+    {
+      seen.assign((size_t)n_colors + 1, 0);
+      const uint32_t *cn = &op->h_cell_nodes[(size_t)gls::ext_cell(op, c) * nq];
+      for (int p = 0; p < nq; ++p)
+        for (int32_t o : node_cells[cn[p]])
+          if (color[(size_t)o] >= 0)
+            seen[(size_t)color[(size_t)o]] = 1;
+      int k = 0;
+      while (seen[(size_t)k])
+        ++k;
+      color[(size_t)c] = k;
+      n_colors         = std::max(n_colors, k + 1);
+    }
+  std::vector<int32_t> order;
+  std::vector<int64_t> cbeg(1, 0);
+  for (int k = 0; k < n_colors; ++k)
+    {
+      for (int64_t c = 0; c < nc_; ++c)
+        if (color[(size_t)c] == k)
+          order.push_back((int32_t)c);
+      cbeg.push_back((int64_t)order.size());
+    }
+  const size_t eb = (size_t)nc_ * ndof * ndof * sizeof(T);
+  void        *E = nullptr, *d_cdof = nullptr, *d_order = nullptr;
+  HIP_THROW(hipMallocAsync(&E, eb, s));
+  HIP_THROW(hipMallocAsync(&d_cdof, cdof.size() * sizeof(int32_t), s));
+  HIP_THROW(hipMallocAsync(&d_order, order.size() * sizeof(int32_t), s));
+  HIP_THROW(hipMemcpyAsync(d_cdof, cdof.data(), cdof.size() * sizeof(int32_t),
+                           hipMemcpyHostToDevice, s));
+  HIP_THROW(hipMemcpyAsync(d_order, order.data(), order.size() * sizeof(int32_t),
+                           hipMemcpyHostToDevice, s));
+  gls::op_element_matrices_device(op, E, 0, nc_, s);
+  HIP_THROW(hipMemsetAsync(mg->d_lu, 0, (size_t)nf * nf * sizeof(double), s));
+  const int64_t per = (int64_t)ndof * ndof;
+  for (int k = 0; k < n_colors; ++k)
+    {
+      const int64_t cnt = cbeg[(size_t)k + 1] - cbeg[(size_t)k];
+      hipLaunchKernelGGL(k_scatter_emat<T>, g1(cnt * per), dim3(256), 0, s, mg->d_lu, nf,
+                         (const T *)E, (const int32_t *)d_cdof,
+                         (const int32_t *)d_order + cbeg[(size_t)k], cnt, ndof);
+    }
+  HIP_THROW(hipGetLastError());
+  HIP_THROW(hipFreeAsync(E, s));
+  HIP_THROW(hipFreeAsync(d_cdof, s));
+  HIP_THROW(hipFreeAsync(d_order, s));
+  mg->coarse_colors = n_colors;
+  // (the synchronised setup of the caller waits for these launches)
+  (void)mg;
+}
+
 // Assemble the coarse level operator into FP64 and LU-factorise it.  Only
 // the free (unconstrained) dofs take part: a constrained dof's row and
 // column of A are both the unit vector (identity rows of vmult, homogeneous
@@ -874,10 +988,15 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
   if (!mg->blas)
     check_blas(rocblas_create_handle(&mg->blas), "rocblas_create_handle");
   check_blas(rocblas_set_stream(mg->blas, s), "rocblas_set_stream");
+  if (mg->d_free && mg->n_free != nf)
+    throw std::runtime_error("dense LU coarse solver: constrained dofs changed");
+  // the FP64 factors are released after an FP32 setup (k_narrow below)
   if (!mg->d_lu)
+    HIP_THROW(hipMalloc((void **)&mg->d_lu, (size_t)nf * nf * sizeof(double)));
+  if (!mg->d_ipiv)
+    HIP_THROW(hipMalloc((void **)&mg->d_ipiv, (size_t)nf * sizeof(rocblas_int)));
+  if (!mg->d_free)
     {
-      HIP_THROW(hipMalloc((void **)&mg->d_lu, (size_t)nf * nf * sizeof(double)));
-      HIP_THROW(hipMalloc((void **)&mg->d_ipiv, (size_t)nf * sizeof(rocblas_int)));
       HIP_THROW(hipMalloc((void **)&mg->d_info, sizeof(rocblas_int)));
       mg->ld_free = (nf + 3) / 4 * 4;
       HIP_THROW(hipMalloc((void **)&mg->d_rhs,
@@ -889,24 +1008,37 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
     throw std::runtime_error("dense LU coarse solver: constrained dofs changed");
   HIP_THROW(hipMemcpyAsync(mg->d_free, freel.data(), (size_t)nf * sizeof(int32_t),
                            hipMemcpyHostToDevice, s));
-  T *e = (T *)mg->sol[0], *col = (T *)mg->tmp[0];
-  HIP_THROW(hipMemsetAsync(e, 0, n * sizeof(T), s));
-  for (int64_t j = 0; j < nf; ++j)
+  const char *ca = getenv("GLS_COARSE_ASSEMBLY");
+  const auto  t0 = std::chrono::steady_clock::now();
+  if (ca && std::string(ca) == "columns")
     {
-      const int64_t dj = freel[(size_t)j];
-      hipLaunchKernelGGL(k_set_unit<T>, g1(n), dim3(256), 0, s, e, dj, n, 1);
-      gls::op_vmult_device(op, col, e, s);
-      hipLaunchKernelGGL(k_gather_free<T>, g1(nf), dim3(256), 0, s, mg->d_lu + (size_t)j * nf,
-                         (const T *)col, (const int32_t *)mg->d_free, nf);
-      hipLaunchKernelGGL(k_set_unit<T>, g1(n), dim3(256), 0, s, e, dj, n, 0);
+      // reference path of the assembly test: A_ff column by column from
+      // unit-vector vmults (nf vmults of the level operator)
+      T *e = (T *)mg->sol[0], *col = (T *)mg->tmp[0];
+      HIP_THROW(hipMemsetAsync(e, 0, n * sizeof(T), s));
+      for (int64_t j = 0; j < nf; ++j)
+        {
+          const int64_t dj = freel[(size_t)j];
+          hipLaunchKernelGGL(k_set_unit<T>, g1(n), dim3(256), 0, s, e, dj, n, 1);
+          gls::op_vmult_device(op, col, e, s);
+          hipLaunchKernelGGL(k_gather_free<T>, g1(nf), dim3(256), 0, s,
+                             mg->d_lu + (size_t)j * nf, (const T *)col,
+                             (const int32_t *)mg->d_free, nf);
+          hipLaunchKernelGGL(k_set_unit<T>, g1(n), dim3(256), 0, s, e, dj, n, 0);
+        }
+      HIP_THROW(hipGetLastError());
     }
-  HIP_THROW(hipGetLastError());
+  else
+    assemble_free_block<T>(mg, freel, s);
+  HIP_THROW(hipStreamSynchronize(s));
+  const auto t1 = std::chrono::steady_clock::now();
   check_blas(rocsolver_dgetrf(mg->blas, (rocblas_int)nf, (rocblas_int)nf, mg->d_lu,
                               (rocblas_int)nf, mg->d_ipiv, mg->d_info),
              "rocsolver_dgetrf");
   rocblas_int info = 0;
   HIP_THROW(hipMemcpyAsync(&info, mg->d_info, sizeof(info), hipMemcpyDeviceToHost, s));
   HIP_THROW(hipStreamSynchronize(s));
+  const auto t2 = std::chrono::steady_clock::now();
   if (info != 0)
     throw std::runtime_error("dense LU coarse solver: singular coarse matrix (info " +
                              std::to_string(info) + ")");
@@ -922,6 +1054,13 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
   if (info != 0)
     throw std::runtime_error("dense LU coarse solver: singular coarse matrix in getri (info " +
                              std::to_string(info) + ")");
+  const auto t3 = std::chrono::steady_clock::now();
+  auto       ms = [](auto a, auto b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+  mg->coarse_setup_ms[0] = ms(t0, t1);
+  mg->coarse_setup_ms[1] = ms(t1, t2);
+  mg->coarse_setup_ms[2] = ms(t2, t3);
   // FP32 levels keep an FP32 copy of the inverse (FP64 sums): half the bytes
   // per coarse solve; the Re3900 r0..r2 V-cycle differs from the FP64-stored
   // inverse's by 2.1e-7 (relative l2), the FP32 level arithmetic's own
@@ -936,6 +1075,13 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
       hipLaunchKernelGGL(k_narrow, g1(nf * ld), dim3(256), 0, s, mg->d_inv32,
                          (const double *)mg->d_lu, nf, ld);
       HIP_THROW(hipGetLastError());
+      // the FP32 solve reads d_inv32 only: release the nf x nf FP64 factors
+      // (1.6 GB at Re3900 r0) and the pivots; a re-setup allocates them again
+      HIP_THROW(hipStreamSynchronize(s));
+      HIP_THROW(hipFree(mg->d_lu));
+      HIP_THROW(hipFree(mg->d_ipiv));
+      mg->d_lu   = nullptr;
+      mg->d_ipiv = nullptr;
     }
 }
 
@@ -1149,6 +1295,14 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
     }
   mg->cg_iters = it;
   mg->cg_conv  = res <= tol;
+  // deal.II's SolverGMRES inside MGCoarseGridIterativeSolver throws
+  // SolverControl::NoConvergence when maxiter is reached (multigrid.cc:
+  // 494-530): the V-cycle fails the same way instead of continuing with an
+  // unconverged coarse correction
+  if (!mg->cg_conv)
+    throw std::runtime_error("coarse GMRES: no convergence in " + std::to_string(it) +
+                             " iterations (residual " + std::to_string(res) + ", tolerance " +
+                             std::to_string(tol) + "; SolverControl::NoConvergence)");
   cvt_in((T *)mg->sol[0], x);
   HIP_THROW(hipGetLastError());
 }
@@ -1688,6 +1842,19 @@ gls_mg_set_vector_layout(glsMG mg, int memory, const int64_t *dof_map)
 namespace gls
 {
 void
+mg_check_outer(glsMG mg, const glsOp_ *op)
+{
+  if (mg->desc.outer_precision != GLS_F64)
+    throw std::runtime_error("gls_gmres_solve: the multigrid's outer_precision must be GLS_F64 "
+                             "(PreconditionerGMG::vmult on VectorType<double>)");
+  if (mg->ops.empty() || mg->ops.back()->n_dofs != op->n_dofs)
+    throw std::runtime_error("gls_gmres_solve: the multigrid's finest level does not match the "
+                             "operator's size");
+  if (!mg->setup_done)
+    throw std::runtime_error("gls_gmres_solve: the multigrid is not set up (gls_mg_setup)");
+}
+
+void
 mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s)
 {
   if (!mg->setup_done)
@@ -1740,6 +1907,19 @@ gls_mg_coarse_statistics(glsMG mg, int *n_iterations, int *converged)
     throw std::runtime_error("gls_mg_coarse_statistics: null argument");
   *n_iterations = mg->cg_iters;
   *converged    = mg->cg_conv;
+  GLS_CATCH
+}
+
+glsStatus
+gls_mg_coarse_setup_times(glsMG mg, double *ms3, int *n_colors)
+{
+  GLS_TRY
+  if (!mg || !ms3)
+    throw std::runtime_error("gls_mg_coarse_setup_times: null argument");
+  for (int i = 0; i < 3; ++i)
+    ms3[i] = mg->coarse_setup_ms[i];
+  if (n_colors)
+    *n_colors = mg->coarse_colors;
   GLS_CATCH
 }
 

@@ -187,6 +187,9 @@ int  op_vmult_mode(const glsOp_ *op);
 // one V-cycle on node-major device vectors of the multigrid's outer
 // precision (gls_mg_vcycle without the caller-layout staging; GMRES calls it)
 void mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s);
+// throws unless mg can precondition op's FP64 Krylov vectors in place: outer
+// precision FP64, finest level of op's size, gls_mg_setup done
+void mg_check_outer(glsMG mg, const glsOp_ *op);
 // outflow boundary-face terms (faces.hip), launched after the cell kernels
 void faces_setup(glsOp_ *op, const glsOpDesc *d);
 void faces_release(glsOp_ *op);
@@ -205,4 +208,10 @@ fused_relax_ok(const glsOp_ *op)
 // the same operator pieces without staging (GMRES, multigrid)
 void op_vmult_device(glsOp op, void *dst, const void *src, hipStream_t s);
 void op_inverse_diagonal_device(glsOp op, void *diag, hipStream_t s);
+// element matrices of internal cells [b, e) into emat (device, the operator's
+// precision, [cell][col j][row i], local dof = point * (dim+1) + component),
+// outflow faces included (MatrixFreeTools::compute_matrix's cell + boundary
+// lambdas, operator_ns.cc:1407-1430)
+void op_element_matrices_device(const glsOp_ *op, void *emat, int64_t b, int64_t e,
+                                hipStream_t s);
 } // namespace gls

@@ -36,7 +36,7 @@ EXPORTS = [
     "gls_op_get_max_u", "gls_mg_set_vector_layout", "gls_dist_update_ghost_values",
     "gls_dist_get_max_u", "gls_op_compute_diagonal", "gls_op_invert_diagonal", "gls_mg_relax",
     "gls_dist_compress_add", "gls_op_brick_shape", "gls_op_cell_permutation",
-    "gls_discover_bricks", "gls_mg_coarse_statistics", "gls_op_element_matrices",
+    "gls_discover_bricks", "gls_mg_coarse_statistics", "gls_mg_coarse_setup_times", "gls_op_element_matrices",
     "gls_op_system_matrix", "gls_op_n_outflow_faces", "gls_op_outflow_face_points",
     "gls_op_set_outflow_target",
 ]
@@ -156,6 +156,7 @@ def lib():
         L.gls_op_outflow_face_points.argtypes = [vp, vp]
         L.gls_op_set_outflow_target.argtypes = [vp, vp, vp]
         L.gls_mg_coarse_statistics.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.gls_mg_coarse_setup_times.argtypes = [vp, vp, C.POINTER(C.c_int)]
         L.gls_discover_bricks.argtypes = [C.c_int, C.c_int, i64, vp, vp, vp]
         L.gls_last_error.restype = C.c_char_p
         _lib = L
@@ -599,6 +600,15 @@ class Multigrid:
         it, cv = C.c_int(), C.c_int()
         _check(lib().gls_mg_coarse_statistics(self.h, C.byref(it), C.byref(cv)))
         return it.value, bool(cv.value)
+
+    def coarse_setup_times(self):
+        """{assembly_ms, getrf_ms, getri_ms, colors} of the last dense-coarse
+        setup (coarse_n_iterations=-1)."""
+        ms = (C.c_double * 3)()
+        nc = C.c_int()
+        _check(lib().gls_mg_coarse_setup_times(self.h, ms, C.byref(nc)))
+        return {"assembly_ms": ms[0], "getrf_ms": ms[1], "getri_ms": ms[2],
+                "colors": nc.value}
 
     def relaxation(self, level):
         w, lam = C.c_double(), C.c_double()

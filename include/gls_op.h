@@ -310,6 +310,10 @@ glsStatus gls_mg_get_relaxation(glsMG mg, int level, double *omega,
 /* GMRES iterations of the last coarse solve (coarse_iterate = 1), and
  * whether it reached the tolerance */
 glsStatus gls_mg_coarse_statistics(glsMG mg, int *n_iterations, int *converged);
+/* the last dense-coarse setup (coarse_n_iterations < 0): wall ms of the
+ * free-block assembly (element matrices of the coarse level scattered per
+ * cell colour), of getrf and of getri, and the number of cell colours */
+glsStatus gls_mg_coarse_setup_times(glsMG mg, double *ms3, int *n_colors);
 /* one V-cycle on the finest level: dst = V(src) (PreconditionMG::vmult) */
 glsStatus gls_mg_vcycle(glsMG mg, void *dst, const void *src, void *stream);
 /* caller vector layout of gls_mg_vcycle's dst / src (as gls_op_set_vector_

@@ -113,20 +113,47 @@ class OracleGMG:
         return x
 
     def coarse_matrix(self):
+        """The assembled coarse operator (dense, FP64): the oracle's element
+        matrices (orc_cell_matrix: unit-vector cell applies,
+        MatrixFreeTools::compute_matrix, operator_ns.cc:1407-1430) summed
+        over the cells on the free dofs; constrained rows and columns are the
+        unit vector (identity rows of vmult, homogeneous constraints read as
+        0).  Equal to the matrix of the oracle's vmult (test_mg_ref.py)."""
         if not hasattr(self, "_A0"):
-            n = self.meshes[0].n_dofs
-            A = np.empty((n, n))
-            e = np.zeros(n)
-            for j in range(n):
-                e[j] = 1.0
-                A[:, j] = self.ops[0].vmult(e)
-                e[j] = 0.0
+            m, o = self.om[0], self.ops[0]
+            nc = m.dim + 1
+            n = m.n_dofs
+            con = ((np.repeat(m.cmask.astype(np.int64), nc) >>
+                    np.tile(np.arange(nc), m.n_nodes)) & 1).astype(bool)
+            A = np.zeros((n, n))
+            for c in range(m.n_cells):
+                dofs = (m.cell_nodes[c].astype(np.int64)[:, None] * nc +
+                        np.arange(nc)[None, :]).reshape(-1)
+                A[np.ix_(dofs, dofs)] += o.cell_matrix(c)
+            A[con, :] = 0.0
+            A[:, con] = 0.0
+            A[con, con] = 1.0
             self._A0 = A
+            self._con0 = con
         return self._A0
+
+    def coarse_direct(self, b):
+        """Direct coarse solve (the decks' "direct", multigrid.cc:448-455):
+        x_c = b_c on the constrained dofs, LU of the free block for the rest
+        (the factorisation cached)."""
+        import scipy.linalg as sla
+        if not hasattr(self, "_lu0"):
+            A = self.coarse_matrix()
+            free = ~self._con0
+            self._lu0 = sla.lu_factor(A[np.ix_(free, free)], check_finite=False)
+            self._free0 = free
+        x = np.asarray(b, dtype=np.float64).copy()
+        x[self._free0] = sla.lu_solve(self._lu0, x[self._free0], check_finite=False)
+        return x
 
     def coarse_precondition(self, b):
         if self.coarse_iters < 0:
-            return np.linalg.solve(self.coarse_matrix(), b)
+            return self.coarse_direct(b)
         if self.coarse_iters == 0:
             return b.copy()
         return self.smooth(0, None, b, True, self.coarse_iters)
@@ -185,11 +212,7 @@ class OracleGMG:
         if l == 0 and self.coarse_gmres_reltol is not None:
             return self.coarse_gmres(b)
         if l == 0:
-            if self.coarse_iters < 0:
-                return np.linalg.solve(self.coarse_matrix(), b)
-            if self.coarse_iters == 0:
-                return b.copy()
-            return self.smooth(0, None, b, True, self.coarse_iters)
+            return self.coarse_precondition(b)
         x = self.smooth(l, None, b, True, self.n_smooth)
         t = b - self.ops[l].vmult(x)
         bc = np.zeros(self.meshes[l - 1].n_dofs)

@@ -63,15 +63,24 @@ def test_turek3d_r3_residual(turek3d_r3):
     assert rel_err(_np(res), ref) < TOL["f64"]
 
 
-def test_sphere_r3_vmult():
+@pytest.fixture(scope="module")
+def sphere_r3():
     # input_sphere_amg.json as configured: mesh/sphere.msh r3 (524,288 cells,
     # 17,073,608 DoFs), every cell general geometry
     d = deck("input_sphere_amg.json")
     assert d.n_refinements == 3
     case = deck_case("input_sphere_amg.json")
     assert case.n_dofs == 17073608
-    ref = case.oracle().vmult(case.src)
-    assert rel_err(_vmult(case, "f64"), ref) < TOL["f64"]
+    return case, case.oracle().vmult(case.src)
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_sphere_r3_vmult(sphere_r3, prec):
+    # FP32: the sphere's multigrid levels run the FP32 operator
+    case, ref = sphere_r3
+    err = rel_err(_vmult(case, prec), ref)
+    print(f"sphere r3 {prec} vmult rel err {err:.2e}")
+    assert err < TOL[prec]
 
 
 @pytest.mark.parametrize("prec", ["f64", "f32"])
@@ -125,3 +134,129 @@ def test_vcycle_re3900_r0_r2():
     torch.cuda.synchronize()
     assert rel_err(_np(x), ref.smooth(L, None, b, True, 5)) < 1e-4
     assert rel_err(_np(dst), ref.vcycle(b)) < 5e-4
+
+
+def _re3900(n_ref=2):
+    d = deck("input_hoffmann_3D_Re3900.json")
+    meshes = [d.mesh(r) for r in range(n_ref + 1)]
+    vel, p, slip = d.boundary_descriptor()
+    cm = [m.constraint_mask(vel, p, slip) for m in meshes]
+    params, w = d.operator_parameters(2.5e-4)
+    u = gi.linearization_point(meshes[-1].n_nodes, 3, d.u_max)
+    hist = gi.history(u, params["order"])
+    return meshes, cm, params, w, u, hist
+
+
+def test_level_diagonals_re3900_r2():
+    """The FP32 level inverse diagonals of the headline hierarchy r0..r2 (the
+    r2 level included) against the oracle multigrid's FP64 ones
+    (compute_inverse_diagonal, operator_ns.cc:195-225, on the linearization
+    point interpolated level by level, main.cc:772-803)."""
+    import glsamd
+    meshes, cm, params, w, u, hist = _re3900(2)
+    mg, ops = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f32")
+    ref = OracleGMG(meshes, cm, params, u, hist, w)
+    for l in range(len(meshes)):
+        dl = ops[l].initialize_dof_vector()
+        ops[l].compute_inverse_diagonal(dl)
+        err = rel_err(_np(dl), ref.invdiag[l])
+        print(f"Re3900 level r{l} FP32 inverse diagonal rel err {err:.2e}")
+        assert err < 1e-6, (l, err)
+
+
+def test_vcycle_re3900_direct_coarse():
+    """The deck's own V-cycle ("gmg coarse grid solver": "direct",
+    multigrid.cc:448-455, 465-481) on the headline hierarchy r0..r2, FP32
+    levels, FP64 in / out: the GPU's dense coarse solve (free-dof block
+    assembled from element matrices, LU-inverted, FP32-stored inverse) and
+    the GPU's own FP32 inverse diagonals against the oracle multigrid with
+    ITS FP64 diagonals and an FP64 LU of the oracle's coarse matrix.  The
+    relaxation factors are the GPU's (checked against the oracle's power
+    iteration to 1e-3 in test_vcycle_re3900_r0_r2)."""
+    import torch
+    import glsamd
+    meshes, cm, params, w, u, hist = _re3900(2)
+    mg, ops = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f32",
+                               coarse_n_iterations=-1)
+    print("coarse setup", mg.coarse_setup_times())
+    ref = OracleGMG(meshes, cm, params, u, hist, w, coarse_iters=-1)
+    ref.set_omega([mg.relaxation(l)[0] for l in range(len(meshes))])
+    b = gi.rnd(11, meshes[-1].n_dofs)
+    src = torch.from_numpy(b).cuda()
+    dst = torch.zeros_like(src)
+    mg.vcycle(dst, src)
+    torch.cuda.synchronize()
+    err = rel_err(_np(dst), ref.vcycle(b))
+    print(f"Re3900 r0..r2 direct-coarse V-cycle rel err {err:.2e}")
+    assert err < 5e-4
+
+
+def test_coarse_assembly_element_matrices():
+    """The dense coarse solver's free-dof block assembled from the level's
+    element matrices (one launch + one scatter per cell colour) against the
+    column-by-column assembly from unit-vector vmults
+    (GLS_COARSE_ASSEMBLY=columns), FP64 levels r0..r1: the V-cycles agree."""
+    import os
+    import torch
+    import glsamd
+    meshes, cm, params, w, u, hist = _re3900(1)
+    b = torch.from_numpy(gi.rnd(11, meshes[-1].n_dofs)).cuda()
+    out = {}
+    for mode in ("columns", "elements"):
+        if mode == "columns":
+            os.environ["GLS_COARSE_ASSEMBLY"] = "columns"
+        try:
+            mg, ops = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f64",
+                                       coarse_n_iterations=-1)
+        finally:
+            os.environ.pop("GLS_COARSE_ASSEMBLY", None)
+        print(mode, mg.coarse_setup_times())
+        x = torch.zeros_like(b)
+        mg.vcycle(x, b)
+        torch.cuda.synchronize()
+        out[mode] = _np(x)
+        del mg, ops
+    err = rel_err(out["elements"], out["columns"])
+    print(f"element vs column coarse assembly: V-cycle rel diff {err:.2e}")
+    assert err < 1e-12
+
+
+def test_vcycle_sphere_iso_q1_r3():
+    """The sphere deck's multigrid at its configured size: FE_Q_iso_Q1 coarse
+    level (main.cc:436-446) under r1..r3 (524,288 fine cells), FP32 levels,
+    coarse GMRES to 1e-4 ("gmg coarse grid iterate", multigrid.cc:491-530)
+    preconditioned by 10 relaxation sweeps (the AMG substitute, DESIGN.md
+    A16), against the oracle multigrid with its own FP64 diagonals."""
+    import torch
+    import glsamd
+    import glsmesh as gm
+    d = deck("input_sphere_amg.json")
+    meshes = [d.mesh(r) for r in range(d.n_refinements + 1)]
+    vel, p, slip = d.boundary_descriptor()
+    cm = [m.constraint_mask(vel, p, slip) for m in meshes]
+    params, w = d.operator_parameters(2.5e-4)
+    u = gi.linearization_point(meshes[-1].n_nodes, 3, d.u_max)
+    hist = gi.history(u, params["order"])
+    mg, ops = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f32",
+                               coarse_n_iterations=10, coarse_iso_q1=True,
+                               coarse_iterate=True, coarse_reltol=1e-4, coarse_maxiter=2000)
+    ref = OracleGMG([gm.IsoQ1Mesh(meshes[0])] + meshes[1:], cm, params, u, hist, w,
+                    coarse_iters=10, coarse_gmres_reltol=1e-4)
+    ref.set_omega([mg.relaxation(l)[0] for l in range(len(meshes))])
+    for l in range(len(meshes)):
+        dl = ops[l].initialize_dof_vector()
+        ops[l].compute_inverse_diagonal(dl)
+        print(f"sphere level {l} FP32 inverse diagonal rel err "
+              f"{rel_err(_np(dl), ref.invdiag[l]):.2e}")
+    b = gi.rnd(11, meshes[-1].n_dofs)
+    src = torch.from_numpy(b).cuda()
+    dst = torch.zeros_like(src)
+    mg.vcycle(dst, src)
+    torch.cuda.synchronize()
+    it, conv = mg.coarse_statistics()
+    xr = ref.vcycle(b)
+    err = rel_err(_np(dst), xr)
+    print(f"sphere r3 iso-Q1 V-cycle rel err {err:.2e}, coarse GMRES {it} vs "
+          f"{ref.coarse_gmres_iterations}")
+    assert conv and abs(it - ref.coarse_gmres_iterations) <= 3
+    assert err < 2e-3
