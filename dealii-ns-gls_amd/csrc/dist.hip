@@ -595,3 +595,133 @@ gls_dist_interior_bricks(glsDist d, int64_t *n_interior, int64_t *n_total)
 }
 
 } // extern "C"
+
+// ---- team primitives of the partitioned multigrid and GMRES (dist_mg.hip):
+// a "team" is the set of ranks this process drives in lockstep — one RCCL
+// rank (n = 1, members[0]->comm), or every member of an in-process group
+namespace gls
+{
+namespace
+{
+constexpr int TEAM_MAX = 16;
+struct SumArgs
+{
+  double *buf[TEAM_MAX];
+};
+// every member's buf[i] <- the sum over the members in member order
+__global__ void
+k_team_sum(SumArgs a, int n, int64_t count)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count)
+    return;
+  double s = 0;
+  for (int r = 0; r < n; ++r)
+    s += a.buf[r][i];
+  for (int r = 0; r < n; ++r)
+    a.buf[r][i] = s;
+}
+
+void
+check_team(glsDist const *m, int n)
+{
+  if (!m || n < 1 || n > TEAM_MAX)
+    throw std::runtime_error("gls_dist team: bad member list");
+  if (n == 1 && m[0]->comm)
+    return;
+  for (int r = 0; r < n; ++r)
+    if (!m[r] || m[r]->comm || !m[r]->group || m[r]->rank != r || m[r]->world != n)
+      throw std::runtime_error("gls_dist team: an in-process group is driven with all its "
+                               "members in rank order; RCCL ranks one at a time");
+}
+} // namespace
+
+glsOp_ *
+dist_op(glsDist d)
+{
+  return d->op;
+}
+
+int
+dist_rank(glsDist d)
+{
+  return d->rank;
+}
+
+int
+dist_world(glsDist d)
+{
+  return d->world;
+}
+
+void
+team_vmult(glsDist const *m, void *const *dst, void *const *src, int n, hipStream_t s)
+{
+  check_team(m, n);
+  glsStatus st = m[0]->comm ? gls_dist_vmult(m[0], dst[0], src[0], s)
+                            : gls_dist_vmult_group(m, dst, src, n, s);
+  if (st)
+    throw std::runtime_error(gls_last_error());
+}
+
+void
+team_update_ghosts(glsDist const *m, void *const *v, int n, hipStream_t s)
+{
+  check_team(m, n);
+  if (m[0]->comm)
+    {
+      if (gls_dist_update_ghost_values(m[0], v[0], s))
+        throw std::runtime_error(gls_last_error());
+      return;
+    }
+  for (int r = 0; r < n; ++r)
+    {
+      m[r]->cur_src = v[r];
+      pack(m[r], v[r], s);
+    }
+  for (int r = 0; r < n; ++r)
+    local_import(m[r], s);
+}
+
+void
+team_compress_add(glsDist const *m, void *const *v, int n, hipStream_t s)
+{
+  check_team(m, n);
+  if (m[0]->comm)
+    {
+      if (gls_dist_compress_add(m[0], v[0], s))
+        throw std::runtime_error(gls_last_error());
+      return;
+    }
+  for (int r = 0; r < n; ++r)
+    m[r]->cur_dst = v[r];
+  for (int r = 0; r < n; ++r)
+    local_export(m[r], s);
+  for (int r = 0; r < n; ++r)
+    unpack(m[r], v[r], s);
+  for (int r = 0; r < n; ++r)
+    zero_ghosts(m[r], v[r], s);
+}
+
+void
+team_allreduce_sum(glsDist const *m, double *const *buf, int64_t count, int n, hipStream_t s)
+{
+  check_team(m, n);
+  if (count <= 0)
+    return;
+  if (m[0]->comm)
+    {
+      if (m[0]->world > 1)
+        NCCL_THROW(ncclAllReduce(buf[0], buf[0], (size_t)count, ncclDouble, ncclSum, m[0]->comm,
+                                 s));
+      return;
+    }
+  SumArgs a{};
+  for (int r = 0; r < n; ++r)
+    a.buf[r] = buf[r];
+  hipLaunchKernelGGL(k_team_sum, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, a, n,
+                     count);
+  HIP_THROW(hipGetLastError());
+}
+} // namespace gls
+

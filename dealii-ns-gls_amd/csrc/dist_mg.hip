@@ -1,0 +1,1137 @@
+// dist_mg.hip — the partitioned geometric multigrid preconditioner and the
+// GMRES solver on rank-local vectors, one rank per GPU (VERDICT
+// r2 item 6): PreconditionerGMG::initialize / vmult (multigrid.cc:247-370,
+// 202-220) over distributed level operators, and LinearSolverGMRES::solve
+// (solver_l.cc:45-74) with MPI_Allreduce'd dots — in native code behind the
+// C-ABI, so that a deal.II caller on N ranks gets the GPU V-cycle and GPU
+// GMRES through the boundary.
+//
+// Every level is a partitioned operator (glsDist) on the same coarse-cell
+// partition (main.cc:398-400); the level transfers are the owner-only
+// lattice kernels of mg.hip on the rank's cells with halo exchanges around
+// them (MGTransferGlobalCoarsening's ghosted level vectors, main.cc:540-563):
+//   prolongate  update_ghost_values(coarse), local prolongate_add
+//   restrict    local restrict_add, compress(add) of the coarse vector
+//   interpolate update_ghost_values(fine), local injection, ghost update
+// Smoother: damped Jacobi with the power-iteration omega, deal.II's start
+// vector on the GLOBAL dof index, dots all-reduced.  Coarse solve:
+// relaxation sweeps, identity, or (coarse_n_iterations < 0, the decks'
+// "direct") the coarse right-hand side all-reduced into a global vector and
+// solved redundantly on every rank by a single-domain dense-LU multigrid of
+// the whole coarse level.
+//
+// All entry points take a TEAM: the handles of the ranks this process
+// drives in lockstep — one RCCL rank (n = 1), or every member of an
+// in-process group on one device (tests: the same data movement as device
+// copies), as gls_dist_vmult / gls_dist_vmult_group.
+#include "../../include/gls_op.h"
+#include "common.h"
+#include "op_internal.h"
+
+#include <rocblas/rocblas.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+struct glsDistMG_
+{
+  glsMGDesc            desc{};
+  int                  prec = GLS_F32, nc = 4, nl = 0;
+  std::vector<glsDist> lv;          // level operators of this rank
+  glsMG                tr = nullptr; // transfers and relaxation kernels (mg.hip)
+  std::vector<void *>  invd, X, B, T, start;
+  std::vector<int64_t> n_dofs, n_owned;
+  std::vector<double>  omega, lambda;
+  double              *red = nullptr; // FP64 reduction scratch [RED]
+  // direct coarse solve, redundant on every rank
+  glsOp                coarse_op = nullptr;
+  glsMG                coarse_mg = nullptr;
+  int64_t              ng0 = 0;         // global coarse dofs
+  int64_t             *d_l2g = nullptr; // level-0 local node -> global node
+  double              *g_buf = nullptr; // [ng0] all-reduced global vector
+  void                *g_rhs = nullptr, *g_sol = nullptr; // [ng0] coarse precision
+  bool                 have_lin = false, setup_done = false;
+  void                *outer = nullptr; // FP64 <-> level conversions: level-precision copy
+  // GMRES workspace: V (m+1) n | w n | z n | y (m+1) (FP64)
+  double              *gm = nullptr;
+  size_t               gm_bytes = 0;
+  rocblas_handle       blas = nullptr;
+
+  size_t
+  ts() const
+  {
+    return prec == GLS_F64 ? 8 : 4;
+  }
+};
+
+namespace
+{
+constexpr int RED = 4096; // reduction scratch (block partials + results)
+constexpr int TEAM_MAX = 16;
+
+dim3
+g1(int64_t n)
+{
+  return dim3((unsigned)((n + 255) / 256));
+}
+
+void
+check(glsStatus st)
+{
+  if (st)
+    throw std::runtime_error(gls_last_error());
+}
+
+void
+check_blas(rocblas_status st, const char *what)
+{
+  if (st != rocblas_status_success)
+    throw std::runtime_error(std::string(what) + ": rocBLAS status " + std::to_string((int)st));
+}
+
+// ---- kernels
+// part[block] = sum of a[i] b[i] over the block's rows (FP64)
+template <typename T>
+__global__ void __launch_bounds__(256)
+  k_dot_part(const T *__restrict__ a, const T *__restrict__ b, int64_t n, double *part)
+{
+  __shared__ double sh[256];
+  double            v = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    v += (double)a[i] * (double)b[i];
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1)
+    {
+      if ((int)threadIdx.x < o)
+        sh[threadIdx.x] += sh[threadIdx.x + o];
+      __syncthreads();
+    }
+  if (threadIdx.x == 0)
+    part[blockIdx.x] = sh[0];
+}
+
+// out[0] = the partials summed in a fixed order
+__global__ void __launch_bounds__(256)
+  k_sum_part(const double *part, int nb, double *out)
+{
+  __shared__ double sh[256];
+  double            v = 0;
+  for (int i = threadIdx.x; i < nb; i += 256)
+    v += part[i];
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1)
+    {
+      if ((int)threadIdx.x < o)
+        sh[threadIdx.x] += sh[threadIdx.x + o];
+      __syncthreads();
+    }
+  if (threadIdx.x == 0)
+    out[0] = sh[0];
+}
+
+template <typename T>
+__global__ void
+k_scale(T *x, double s, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    x[i] = (T)((double)x[i] * s);
+}
+
+template <typename T>
+__global__ void
+k_mul(T *y, const T *d, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    y[i] *= d[i];
+}
+
+// t = b - t
+template <typename T>
+__global__ void
+k_rsub(T *t, const T *b, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    t[i] = b[i] - t[i];
+}
+
+template <typename Tin, typename Tout>
+__global__ void
+k_cvt(Tout *y, const Tin *x, int64_t n)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    y[i] = (Tout)x[i];
+}
+
+// g[l2g[node] nc + c] = v[node nc + c] over the owned nodes (g zeroed)
+template <typename T>
+__global__ void
+k_scatter_owned(double *g, const T *v, const int64_t *l2g, int64_t n_nodes, int nc)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_nodes * nc)
+    return;
+  const int64_t node = i / nc;
+  g[l2g[node] * nc + (i - node * nc)] = (double)v[i];
+}
+
+// v[node nc + c] = g[l2g[node] nc + c] over the local (owned + ghost) nodes
+template <typename T>
+__global__ void
+k_gather_local(T *v, const T *g, const int64_t *l2g, int64_t n_nodes, int nc)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_nodes * nc)
+    return;
+  const int64_t node = i / nc;
+  v[i]               = g[l2g[node] * nc + (i - node * nc)];
+}
+
+int64_t
+owned_nodes0(const glsDistMG_ *x)
+{
+  return gls::dist_op(x->lv[0])->n_owned_nodes;
+}
+
+// ---- team helpers: one operation per member, in member order
+struct Team
+{
+  std::vector<glsDistMG_ *> m;
+  std::vector<glsDist>      lv_tmp;
+  int
+  n() const
+  {
+    return (int)m.size();
+  }
+  // the level's member handles (for the dist team primitives)
+  const glsDist *
+  level(int l)
+  {
+    lv_tmp.clear();
+    for (auto *x : m)
+      lv_tmp.push_back(x->lv[(size_t)l]);
+    return lv_tmp.data();
+  }
+};
+
+Team
+make_team(glsDistMG const *h, int n)
+{
+  if (!h || n < 1 || n > TEAM_MAX)
+    throw std::runtime_error("gls_dist_mg: bad team");
+  Team t;
+  for (int r = 0; r < n; ++r)
+    {
+      if (!h[r])
+        throw std::runtime_error("gls_dist_mg: null team member");
+      t.m.push_back(h[r]);
+    }
+  for (int r = 1; r < n; ++r)
+    if (h[r]->nl != h[0]->nl || h[r]->prec != h[0]->prec)
+      throw std::runtime_error("gls_dist_mg: team members differ in their hierarchy");
+  return t;
+}
+
+template <typename F>
+std::vector<void *>
+per(Team &t, F f)
+{
+  std::vector<void *> v;
+  for (auto *x : t.m)
+    v.push_back(f(x));
+  return v;
+}
+
+// <a, b> over the owned dofs of level l, all-reduced (one host sync)
+double
+team_dot(Team &t, int l, const std::vector<void *> &a, const std::vector<void *> &b, hipStream_t s)
+{
+  std::vector<double *> res;
+  for (int r = 0; r < t.n(); ++r)
+    {
+      glsDistMG_   *x  = t.m[r];
+      const int64_t n  = x->n_owned[(size_t)l];
+      const int     nb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n + 255) / 256));
+      if (x->prec == GLS_F64)
+        hipLaunchKernelGGL(k_dot_part<double>, dim3(nb), dim3(256), 0, s, (const double *)a[r],
+                           (const double *)b[r], n, x->red);
+      else
+        hipLaunchKernelGGL(k_dot_part<float>, dim3(nb), dim3(256), 0, s, (const float *)a[r],
+                           (const float *)b[r], n, x->red);
+      hipLaunchKernelGGL(k_sum_part, dim3(1), dim3(256), 0, s, (const double *)x->red, nb,
+                         x->red + RED - 1);
+      res.push_back(x->red + RED - 1);
+    }
+  HIP_THROW(hipGetLastError());
+  gls::team_allreduce_sum(t.level(l), res.data(), 1, t.n(), s);
+  double v = 0;
+  HIP_THROW(hipMemcpyAsync(&v, res[0], sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_THROW(hipStreamSynchronize(s));
+  return v;
+}
+
+void
+team_scale(Team &t, int l, const std::vector<void *> &x, double a, hipStream_t s)
+{
+  for (int r = 0; r < t.n(); ++r)
+    {
+      const int64_t n = t.m[r]->n_dofs[(size_t)l];
+      if (t.m[r]->prec == GLS_F64)
+        hipLaunchKernelGGL(k_scale<double>, g1(n), dim3(256), 0, s, (double *)x[r], a, n);
+      else
+        hipLaunchKernelGGL(k_scale<float>, g1(n), dim3(256), 0, s, (float *)x[r], a, n);
+    }
+  HIP_THROW(hipGetLastError());
+}
+
+// PreconditionRelaxation::vmult (zero start) / step, `iters` damped-Jacobi
+// iterations x <- x + omega D^-1 (b - A x) on level l (multigrid.cc:347-351)
+void
+smooth(Team &t, int l, bool zero, int iters, hipStream_t s)
+{
+  int it = 0;
+  if (zero && iters > 0)
+    {
+      for (auto *x : t.m)
+        check(gls_mg_relax(x->tr, l, x->X[l], x->B[l], nullptr, x->invd[l], x->omega[l], 1, s));
+      it = 1;
+    }
+  for (; it < iters; ++it)
+    {
+      auto X = per(t, [&](glsDistMG_ *x) { return x->X[l]; });
+      auto T = per(t, [&](glsDistMG_ *x) { return x->T[l]; });
+      gls::team_vmult(t.level(l), T.data(), X.data(), t.n(), s);
+      for (auto *x : t.m)
+        check(gls_mg_relax(x->tr, l, x->X[l], x->B[l], x->T[l], x->invd[l], x->omega[l], 0, s));
+    }
+}
+
+void
+copy_vec(void *dst, const void *src, size_t bytes, hipStream_t s)
+{
+  HIP_THROW(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+}
+
+// the coarse solve on level 0 (multigrid.cc:465-489): X[0] from B[0]
+void
+coarse(Team &t, hipStream_t s)
+{
+  glsDistMG_ *m0 = t.m[0];
+  const int   ci = m0->desc.coarse_n_iterations;
+  if (ci > 0)
+    {
+      smooth(t, 0, true, ci, s);
+      return;
+    }
+  if (ci == 0)
+    {
+      for (auto *x : t.m)
+        copy_vec(x->X[0], x->B[0], (size_t)x->n_dofs[0] * x->ts(), s);
+      return;
+    }
+  // direct: the owned coarse right-hand side scattered into a zeroed global
+  // vector, all-reduced (every global dof is owned by exactly one rank), the
+  // whole coarse level solved on every rank, the rank's local entries taken
+  std::vector<double *> g;
+  for (auto *x : t.m)
+    {
+      HIP_THROW(hipMemsetAsync(x->g_buf, 0, (size_t)x->ng0 * sizeof(double), s));
+      const int64_t nn = owned_nodes0(x);
+      if (x->prec == GLS_F64)
+        hipLaunchKernelGGL(k_scatter_owned<double>, g1(nn * x->nc), dim3(256), 0, s, x->g_buf,
+                           (const double *)x->B[0], x->d_l2g, nn, x->nc);
+      else
+        hipLaunchKernelGGL(k_scatter_owned<float>, g1(nn * x->nc), dim3(256), 0, s, x->g_buf,
+                           (const float *)x->B[0], x->d_l2g, nn, x->nc);
+      g.push_back(x->g_buf);
+    }
+  HIP_THROW(hipGetLastError());
+  gls::team_allreduce_sum(t.level(0), g.data(), m0->ng0, t.n(), s);
+  for (auto *x : t.m)
+    {
+      const int cp = gls_op_precision(x->coarse_op);
+      if (cp == GLS_F64)
+        copy_vec(x->g_rhs, x->g_buf, (size_t)x->ng0 * 8, s);
+      else
+        hipLaunchKernelGGL((k_cvt<double, float>), g1(x->ng0), dim3(256), 0, s,
+                           (float *)x->g_rhs, (const double *)x->g_buf, x->ng0);
+      check(gls_mg_vcycle(x->coarse_mg, x->g_sol, x->g_rhs, s));
+      const int64_t nn = gls::dist_op(x->lv[0])->n_nodes;
+      if (x->prec == GLS_F64)
+        hipLaunchKernelGGL(k_gather_local<double>, g1(nn * x->nc), dim3(256), 0, s,
+                           (double *)x->X[0], (const double *)x->g_sol, x->d_l2g, nn, x->nc);
+      else
+        hipLaunchKernelGGL(k_gather_local<float>, g1(nn * x->nc), dim3(256), 0, s,
+                           (float *)x->X[0], (const float *)x->g_sol, x->d_l2g, nn, x->nc);
+    }
+  HIP_THROW(hipGetLastError());
+}
+
+// Multigrid::level_v_step: X[l] from B[l]
+void
+v_step(Team &t, int l, hipStream_t s)
+{
+  if (l == 0)
+    {
+      coarse(t, s);
+      return;
+    }
+  const int ns = t.m[0]->desc.smoothing_n_iterations;
+  smooth(t, l, true, ns, s);
+  {
+    auto X = per(t, [&](glsDistMG_ *x) { return x->X[l]; });
+    auto T = per(t, [&](glsDistMG_ *x) { return x->T[l]; });
+    gls::team_vmult(t.level(l), T.data(), X.data(), t.n(), s);
+  }
+  for (auto *x : t.m)
+    {
+      const int64_t n = x->n_dofs[(size_t)l];
+      if (x->prec == GLS_F64)
+        hipLaunchKernelGGL(k_rsub<double>, g1(n), dim3(256), 0, s, (double *)x->T[l],
+                           (const double *)x->B[l], n);
+      else
+        hipLaunchKernelGGL(k_rsub<float>, g1(n), dim3(256), 0, s, (float *)x->T[l],
+                           (const float *)x->B[l], n);
+      HIP_THROW(hipMemsetAsync(x->B[l - 1], 0, (size_t)x->n_dofs[(size_t)l - 1] * x->ts(), s));
+      check(gls_mg_restrict_add(x->tr, l, x->B[l - 1], x->T[l], s));
+    }
+  HIP_THROW(hipGetLastError());
+  {
+    auto Bc = per(t, [&](glsDistMG_ *x) { return x->B[l - 1]; });
+    gls::team_compress_add(t.level(l - 1), Bc.data(), t.n(), s);
+  }
+  v_step(t, l - 1, s);
+  {
+    auto Xc = per(t, [&](glsDistMG_ *x) { return x->X[l - 1]; });
+    gls::team_update_ghosts(t.level(l - 1), Xc.data(), t.n(), s);
+  }
+  for (auto *x : t.m)
+    check(gls_mg_prolongate_add(x->tr, l, x->X[l], x->X[l - 1], s));
+  smooth(t, l, false, ns, s);
+}
+
+// deal.II power_iteration (PreconditionRelaxation::estimate_eigenvalues with
+// EigenvalueAlgorithm::power_iteration): |x . D^-1 A x| after n_eig steps
+double
+power_iteration(Team &t, int l, hipStream_t s)
+{
+  const size_t b = (size_t)t.m[0]->n_dofs[(size_t)l] * t.m[0]->ts();
+  auto         X = per(t, [&](glsDistMG_ *x) { return x->X[l]; });
+  auto         Y = per(t, [&](glsDistMG_ *x) { return x->T[l]; });
+  for (auto *x : t.m)
+    copy_vec(x->X[l], x->start[l], (size_t)x->n_dofs[(size_t)l] * x->ts(), s);
+  (void)b;
+  const double nx = std::sqrt(team_dot(t, l, X, X, s));
+  team_scale(t, l, X, nx > 0 ? 1.0 / nx : 0.0, s);
+  double lam = 0;
+  for (int it = 0; it < t.m[0]->desc.smoothing_eig_n_iterations; ++it)
+    {
+      gls::team_vmult(t.level(l), Y.data(), X.data(), t.n(), s);
+      for (auto *x : t.m)
+        {
+          const int64_t n = x->n_dofs[(size_t)l];
+          if (x->prec == GLS_F64)
+            hipLaunchKernelGGL(k_mul<double>, g1(n), dim3(256), 0, s, (double *)x->T[l],
+                               (const double *)x->invd[l], n);
+          else
+            hipLaunchKernelGGL(k_mul<float>, g1(n), dim3(256), 0, s, (float *)x->T[l],
+                               (const float *)x->invd[l], n);
+        }
+      HIP_THROW(hipGetLastError());
+      lam             = team_dot(t, l, X, Y, s);
+      const double ny = std::sqrt(team_dot(t, l, Y, Y, s));
+      for (auto *x : t.m)
+        copy_vec(x->X[l], x->T[l], (size_t)x->n_dofs[(size_t)l] * x->ts(), s);
+      team_scale(t, l, X, ny > 0 ? 1.0 / ny : 0.0, s);
+    }
+  return std::abs(lam);
+}
+
+} // namespace
+
+extern "C" {
+
+glsStatus
+gls_dist_mg_create(const glsDistMGDesc *d, const glsDist *levels, glsDistMG *out)
+{
+  GLS_TRY
+  if (!d || !levels || !out || d->mg.n_levels < 1)
+    throw std::runtime_error("gls_dist_mg_create: invalid arguments");
+  if (d->mg.coarse_iterate)
+    throw std::runtime_error("gls_dist_mg_create: coarse_iterate is single-domain only");
+  const int nl = d->mg.n_levels;
+  auto     *m  = new glsDistMG_();
+  try
+    {
+      m->desc = d->mg;
+      m->nl   = nl;
+      std::vector<glsOp> ops;
+      for (int l = 0; l < nl; ++l)
+        {
+          if (!levels[l])
+            throw std::runtime_error("gls_dist_mg_create: null level");
+          m->lv.push_back(levels[l]);
+          ops.push_back(gls::dist_op(levels[l]));
+        }
+      m->prec = ops[0]->prec;
+      m->nc   = ops[0]->dim + 1;
+      HIP_THROW(hipSetDevice(ops[0]->device));
+      // transfers / relaxation kernels over the rank-local level operators
+      // (the coarse solve of this glsMG is not used)
+      glsMGDesc td          = d->mg;
+      td.coarse_n_iterations = 0;
+      td.outer_precision     = m->prec;
+      check(gls_mg_create(&td, ops.data(), d->child, &m->tr));
+      for (int l = 0; l < nl; ++l)
+        {
+          glsOp_       *op = ops[l];
+          const size_t  b  = std::max<size_t>(16, (size_t)op->n_dofs * m->ts());
+          void         *p[4];
+          for (auto &q : p)
+            {
+              HIP_THROW(hipMalloc(&q, b));
+              HIP_THROW(hipMemset(q, 0, b));
+            }
+          m->invd.push_back(p[0]);
+          m->X.push_back(p[1]);
+          m->B.push_back(p[2]);
+          m->T.push_back(p[3]);
+          m->n_dofs.push_back(op->n_dofs);
+          m->n_owned.push_back(op->n_owned_dofs);
+          // deal.II's power-iteration start vector on the GLOBAL dof index
+          // (set_initial_guess: x_i = i % 11 minus the mean over all dofs,
+          // constrained entries zeroed by AdditionalData::constraints)
+          std::vector<double> x((size_t)op->n_dofs, 0.0);
+          const int64_t       ng   = d->n_global_nodes[l] * m->nc;
+          const double        mean = ((double)(ng / 11) * 55.0 +
+                               (double)((ng % 11) * ((ng % 11) - 1) / 2)) / (double)ng;
+          for (int64_t nd = 0; nd < op->n_owned_nodes; ++nd)
+            for (int c = 0; c < m->nc; ++c)
+              {
+                const int64_t gi = d->owned_global_nodes[l][nd] * m->nc + c;
+                x[(size_t)(nd * m->nc + c)] =
+                  ((op->h_cmask[(size_t)nd] >> c) & 1) ? 0.0 : (double)(gi % 11) - mean;
+              }
+          void *sv = nullptr;
+          HIP_THROW(hipMalloc(&sv, b));
+          if (m->prec == GLS_F64)
+            HIP_THROW(hipMemcpy(sv, x.data(), x.size() * 8, hipMemcpyHostToDevice));
+          else
+            {
+              std::vector<float> xf(x.begin(), x.end());
+              HIP_THROW(hipMemcpy(sv, xf.data(), xf.size() * 4, hipMemcpyHostToDevice));
+            }
+          m->start.push_back(sv);
+        }
+      m->omega.assign(nl, 1.0);
+      m->lambda.assign(nl, 0.0);
+      HIP_THROW(hipMalloc((void **)&m->red, RED * sizeof(double)));
+      if (d->mg.coarse_n_iterations < 0)
+        {
+          if (!d->coarse_global || !d->coarse_local_global)
+            throw std::runtime_error("gls_dist_mg_create: the direct coarse solver needs the "
+                                     "single-domain coarse operator and the level-0 node map");
+          m->coarse_op = d->coarse_global;
+          m->ng0       = d->coarse_global->n_dofs;
+          glsMGDesc cd = d->mg;
+          cd.n_levels          = 1;
+          cd.outer_precision   = d->coarse_global->prec;
+          check(gls_mg_create(&cd, &m->coarse_op, nullptr, &m->coarse_mg));
+          const int64_t nn = ops[0]->n_nodes;
+          HIP_THROW(hipMalloc((void **)&m->d_l2g, std::max<int64_t>(1, nn) * 8));
+          HIP_THROW(hipMemcpy(m->d_l2g, d->coarse_local_global, nn * 8, hipMemcpyHostToDevice));
+          const size_t cs = d->coarse_global->prec == GLS_F64 ? 8 : 4;
+          HIP_THROW(hipMalloc((void **)&m->g_buf, m->ng0 * 8));
+          HIP_THROW(hipMalloc(&m->g_rhs, m->ng0 * cs));
+          HIP_THROW(hipMalloc(&m->g_sol, m->ng0 * cs));
+        }
+      HIP_THROW(hipMalloc(&m->outer, std::max<size_t>(16, (size_t)ops[nl - 1]->n_dofs * m->ts())));
+    }
+  catch (...)
+    {
+      gls_dist_mg_destroy(m);
+      throw;
+    }
+  *out = m;
+  GLS_CATCH
+}
+
+void
+gls_dist_mg_destroy(glsDistMG m)
+{
+  if (!m)
+    return;
+  if (m->tr)
+    gls_mg_destroy(m->tr);
+  if (m->coarse_mg)
+    gls_mg_destroy(m->coarse_mg);
+  for (auto *v : {&m->invd, &m->X, &m->B, &m->T, &m->start})
+    for (void *p : *v)
+      (void)hipFree(p);
+  for (void *p : {(void *)m->red, (void *)m->d_l2g, (void *)m->g_buf, m->g_rhs, m->g_sol,
+                  m->outer, (void *)m->gm})
+    if (p)
+      (void)hipFree(p);
+  if (m->blas)
+    (void)rocblas_destroy_handle(m->blas);
+  delete m;
+}
+
+glsStatus
+gls_dist_mg_set_linearization_point(glsDistMG const *team, int n, const void *const *u_fine,
+                                    const void *const *const *hist_fine, int n_hist,
+                                    const double *weights, void *stream)
+{
+  GLS_TRY
+  Team        t  = make_team(team, n);
+  hipStream_t s  = (hipStream_t)stream;
+  const int   nl = t.m[0]->nl;
+  // interpolate_to_mg (main.cc:772-803): the finest level's vectors injected
+  // level by level, ghosts updated on both sides; level l's vectors live in
+  // X[l] (linearization point) and a temporary per history vector
+  // hist_fine[r] is a SolutionHistory as gls_op_set_previous_solution takes
+  // it (n_hist entries, entry 0 unused): buffer 0 = the linearization point,
+  // buffers 1 .. n_hist-1 = history entries 1 ..
+  const int                       nv = n_hist > 1 ? n_hist : 1;
+  std::vector<std::vector<void *>> bufs((size_t)n); // [member][level * nv + v]
+  for (int r = 0; r < n; ++r)
+    for (int l = 0; l < nl; ++l)
+      for (int v = 0; v < nv; ++v)
+        {
+          void *p = nullptr;
+          HIP_THROW(hipMallocAsync(&p, std::max<size_t>(16, (size_t)t.m[r]->n_dofs[l] *
+                                                              t.m[r]->ts()), s));
+          bufs[r].push_back(p);
+        }
+  auto buf = [&](int r, int l, int v) { return bufs[r][(size_t)(l * nv + v)]; };
+  try
+    {
+      for (int r = 0; r < n; ++r)
+        for (int v = 0; v < nv; ++v)
+          copy_vec(buf(r, nl - 1, v), v == 0 ? u_fine[r] : hist_fine[r][v],
+                   (size_t)t.m[r]->n_dofs[nl - 1] * t.m[r]->ts(), s);
+      for (int l = nl - 1; l > 0; --l)
+        for (int v = 0; v < nv; ++v)
+          {
+            std::vector<void *> f, c;
+            for (int r = 0; r < n; ++r)
+              {
+                f.push_back(buf(r, l, v));
+                c.push_back(buf(r, l - 1, v));
+              }
+            gls::team_update_ghosts(t.level(l), f.data(), n, s);
+            for (int r = 0; r < n; ++r)
+              check(gls_mg_interpolate(t.m[r]->tr, l, c[r], f[r], s));
+            gls::team_update_ghosts(t.level(l - 1), c.data(), n, s);
+          }
+      for (int l = 0; l < nl; ++l)
+        {
+          std::vector<void *> u;
+          for (int r = 0; r < n; ++r)
+            u.push_back(buf(r, l, 0));
+          gls::team_update_ghosts(t.level(l), u.data(), n, s);
+          for (int v = 1; v < nv; ++v)
+            {
+              std::vector<void *> h;
+              for (int r = 0; r < n; ++r)
+                h.push_back(buf(r, l, v));
+              gls::team_update_ghosts(t.level(l), h.data(), n, s);
+            }
+          for (int r = 0; r < n; ++r)
+            {
+              glsOp_ *op = gls::dist_op(t.m[r]->lv[l]);
+              check(gls_op_set_linearization_point(op, buf(r, l, 0), s));
+              if (nv > 1 && op->prm.order > 0)
+                {
+                  std::vector<const void *> hp(1, nullptr);
+                  for (int v = 1; v < nv; ++v)
+                    hp.push_back(buf(r, l, v));
+                  check(gls_op_set_previous_solution(op, hp.data(), nv, weights, s));
+                }
+            }
+        }
+      // the redundant coarse operator: the level-0 linearization point and
+      // history gathered into global vectors (owned entries scattered, sum
+      // all-reduced), set on the single-domain coarse operator
+      if (t.m[0]->coarse_op)
+        {
+          std::vector<std::vector<void *>> gv((size_t)n);
+          for (int r = 0; r < n; ++r)
+            for (int v = 0; v < nv; ++v)
+              {
+                void *p = nullptr;
+                HIP_THROW(hipMallocAsync(&p, (size_t)t.m[r]->ng0 * t.m[r]->coarse_op->tsize(), s));
+                gv[(size_t)r].push_back(p);
+              }
+          for (int v = 0; v < nv; ++v)
+            {
+              std::vector<double *> g;
+              for (int r = 0; r < n; ++r)
+                {
+                  glsDistMG_ *x = t.m[r];
+                  HIP_THROW(hipMemsetAsync(x->g_buf, 0, (size_t)x->ng0 * 8, s));
+                  const int64_t nn = owned_nodes0(x);
+                  if (x->prec == GLS_F64)
+                    hipLaunchKernelGGL(k_scatter_owned<double>, g1(nn * x->nc), dim3(256), 0, s,
+                                       x->g_buf, (const double *)buf(r, 0, v), x->d_l2g, nn,
+                                       x->nc);
+                  else
+                    hipLaunchKernelGGL(k_scatter_owned<float>, g1(nn * x->nc), dim3(256), 0, s,
+                                       x->g_buf, (const float *)buf(r, 0, v), x->d_l2g, nn,
+                                       x->nc);
+                  g.push_back(x->g_buf);
+                }
+              HIP_THROW(hipGetLastError());
+              gls::team_allreduce_sum(t.level(0), g.data(), t.m[0]->ng0, n, s);
+              for (int r = 0; r < n; ++r)
+                {
+                  glsDistMG_ *x = t.m[r];
+                  if (x->coarse_op->prec == GLS_F64)
+                    copy_vec(gv[(size_t)r][(size_t)v], x->g_buf, (size_t)x->ng0 * 8, s);
+                  else
+                    hipLaunchKernelGGL((k_cvt<double, float>), g1(x->ng0), dim3(256), 0, s,
+                                       (float *)gv[(size_t)r][(size_t)v],
+                                       (const double *)x->g_buf, x->ng0);
+                }
+            }
+          HIP_THROW(hipGetLastError());
+          for (int r = 0; r < n; ++r)
+            {
+              glsOp_ *cop = t.m[r]->coarse_op;
+              check(gls_op_set_linearization_point(cop, gv[(size_t)r][0], s));
+              if (nv > 1 && cop->prm.order > 0)
+                {
+                  std::vector<const void *> hp(1, nullptr);
+                  for (int v = 1; v < nv; ++v)
+                    hp.push_back(gv[(size_t)r][(size_t)v]);
+                  check(gls_op_set_previous_solution(cop, hp.data(), nv, weights, s));
+                }
+              for (void *p : gv[(size_t)r])
+                HIP_THROW(hipFreeAsync(p, s));
+            }
+        }
+    }
+  catch (...)
+    {
+      for (auto &b : bufs)
+        for (void *p : b)
+          (void)hipFreeAsync(p, s);
+      throw;
+    }
+  for (auto &b : bufs)
+    for (void *p : b)
+      HIP_THROW(hipFreeAsync(p, s));
+  for (auto *x : t.m)
+    x->have_lin = true;
+  GLS_CATCH
+}
+
+glsStatus
+gls_dist_mg_setup(glsDistMG const *team, int n, void *stream)
+{
+  GLS_TRY
+  Team        t = make_team(team, n);
+  hipStream_t s = (hipStream_t)stream;
+  for (auto *x : t.m)
+    if (!x->have_lin)
+      throw std::runtime_error("gls_dist_mg_setup before gls_dist_mg_set_linearization_point");
+  const int nl = t.m[0]->nl;
+  for (int l = 0; l < nl; ++l)
+    {
+      // compute_inverse_diagonal of a partitioned operator: the rank-local
+      // assembled diagonal, compress(add), then inverted (operator_ns.cc:
+      // 195-225)
+      auto D = per(t, [&](glsDistMG_ *x) { return x->invd[l]; });
+      for (auto *x : t.m)
+        check(gls_op_compute_diagonal(gls::dist_op(x->lv[l]), x->invd[l], s));
+      gls::team_compress_add(t.level(l), D.data(), n, s);
+      for (auto *x : t.m)
+        check(gls_op_invert_diagonal(gls::dist_op(x->lv[l]), x->invd[l], s));
+      const glsMGDesc &d = t.m[0]->desc;
+      if (l == 0 && nl > 1 && d.coarse_n_iterations <= 0 && d.compute_evs_n_levels <= 0)
+        {
+          for (auto *x : t.m)
+            {
+              x->lambda[l] = 0.0;
+              x->omega[l]  = 1.0;
+            }
+          continue;
+        }
+      // relaxation = 0: omega = 2 / (lambda_max / range + lambda_max) from
+      // the power-iteration estimate times the 1.2 safety factor
+      // (multigrid.cc:294-303, 355-369)
+      const double ev    = 1.2 * power_iteration(t, l, s);
+      const double alpha = d.smoothing_range > 1.0 ? ev / d.smoothing_range : 0.9 * ev;
+      for (auto *x : t.m)
+        {
+          x->lambda[l] = ev;
+          x->omega[l]  = ev > 0 ? 2.0 / (alpha + ev) : 1.0;
+        }
+    }
+  for (auto *x : t.m)
+    if (x->coarse_mg)
+      check(gls_mg_setup(x->coarse_mg, s));
+  HIP_THROW(hipStreamSynchronize(s));
+  for (auto *x : t.m)
+    x->setup_done = true;
+  GLS_CATCH
+}
+
+glsStatus
+gls_dist_mg_get_relaxation(glsDistMG mg, int level, double *omega, double *lambda_max)
+{
+  GLS_TRY
+  if (!mg || level < 0 || level >= mg->nl)
+    throw std::runtime_error("gls_dist_mg_get_relaxation: bad arguments");
+  if (omega)
+    *omega = mg->omega[(size_t)level];
+  if (lambda_max)
+    *lambda_max = mg->lambda[(size_t)level];
+  GLS_CATCH
+}
+
+glsStatus
+gls_dist_mg_vcycle(glsDistMG const *team, int n, void *const *dst, const void *const *src,
+                   void *stream)
+{
+  GLS_TRY
+  Team        t = make_team(team, n);
+  hipStream_t s = (hipStream_t)stream;
+  if (!dst || !src)
+    throw std::runtime_error("gls_dist_mg_vcycle: null vectors");
+  for (auto *x : t.m)
+    if (!x->setup_done)
+      throw std::runtime_error("gls_dist_mg_vcycle before gls_dist_mg_setup");
+  const int top = t.m[0]->nl - 1;
+  // copy_to_mg: FP64 outer vectors into the level precision (PreconditionMG
+  // with MGNumber = float, multigrid.cc:113-135)
+  for (int r = 0; r < n; ++r)
+    {
+      glsDistMG_   *x   = t.m[(size_t)r];
+      const int64_t nd  = x->n_dofs[(size_t)top];
+      const bool    cvt = x->desc.outer_precision == GLS_F64 && x->prec == GLS_F32;
+      if (cvt)
+        hipLaunchKernelGGL((k_cvt<double, float>), g1(nd), dim3(256), 0, s, (float *)x->B[top],
+                           (const double *)src[r], nd);
+      else
+        copy_vec(x->B[top], src[r], (size_t)nd * x->ts(), s);
+    }
+  HIP_THROW(hipGetLastError());
+  v_step(t, top, s);
+  for (int r = 0; r < n; ++r)
+    {
+      glsDistMG_   *x   = t.m[(size_t)r];
+      const int64_t nd  = x->n_dofs[(size_t)top];
+      const bool    cvt = x->desc.outer_precision == GLS_F64 && x->prec == GLS_F32;
+      if (cvt)
+        hipLaunchKernelGGL((k_cvt<float, double>), g1(nd), dim3(256), 0, s, (double *)dst[r],
+                           (const float *)x->X[top], nd);
+      else
+        copy_vec(dst[r], x->X[top], (size_t)nd * x->ts(), s);
+    }
+  HIP_THROW(hipGetLastError());
+  GLS_CATCH
+}
+
+// LinearSolverGMRES::solve (solver_l.cc:45-74) on rank-local vectors:
+// right-preconditioned GMRES(max_n_tmp_vectors - 2) with classical
+// Gram-Schmidt and one re-orthogonalisation; the basis in HBM, the dots over
+// the owned rows all-reduced (the Hessenberg column and |w|^2 cross to the
+// host together, once per iteration); x = 0 on entry.  A: the FP64
+// partitioned operator on the finest level's partition (the multigrid's
+// local vectors); mg NULL = identity preconditioner.
+glsStatus
+gls_dist_gmres_solve(glsDist const *A, glsDistMG const *mg, int n, const glsGMRESDesc *desc,
+                     void *const *x, const void *const *b, glsGMRESResult *result, void *stream)
+{
+  GLS_TRY
+  if (!A || !desc || !x || !b || n < 1 || n > TEAM_MAX)
+    throw std::runtime_error("gls_dist_gmres_solve: bad arguments");
+  if (desc->max_n_tmp_vectors < 3)
+    throw std::runtime_error("gls_dist_gmres_solve: max_n_tmp_vectors must be >= 3");
+  hipStream_t         s = (hipStream_t)stream;
+  const int           m = desc->max_n_tmp_vectors - 2;
+  std::vector<glsOp_ *> ops;
+  for (int r = 0; r < n; ++r)
+    {
+      glsOp_ *op = gls::dist_op(A[r]);
+      if (op->prec != GLS_F64)
+        throw std::runtime_error("gls_dist_gmres_solve: the operator must be FP64");
+      if (mg && (!mg[r] || mg[r]->desc.outer_precision != GLS_F64 ||
+                 mg[r]->n_dofs.back() != op->n_dofs || !mg[r]->setup_done))
+        throw std::runtime_error("gls_dist_gmres_solve: the multigrid must be set up with "
+                                 "FP64 outer vectors on the operator's partition");
+      ops.push_back(op);
+    }
+  gls::DeviceScope dev(ops[0]->device);
+  // per member workspace: V (m+1) n | w n | z n | dots 2 (m+1) + 1, and a
+  // rocBLAS handle (device pointer mode for the dot results)
+  struct WS
+  {
+    double *V, *w, *z, *h;
+    int64_t nloc, nown;
+  };
+  std::vector<WS> ws((size_t)n);
+  std::vector<glsDistMG_ *> owner((size_t)n, nullptr);
+  std::vector<double *>     tmp_alloc;
+  for (int r = 0; r < n; ++r)
+    {
+      const int64_t nloc = ops[r]->n_dofs;
+      const size_t  need = ((size_t)(m + 3) * nloc + 2 * (m + 2)) * sizeof(double);
+      double       *base = nullptr;
+      if (mg)
+        {
+          glsDistMG_ *g = mg[r];
+          if (g->gm_bytes < need)
+            {
+              if (g->gm)
+                {
+                  HIP_THROW(hipStreamSynchronize(s));
+                  HIP_THROW(hipFree(g->gm));
+                }
+              HIP_THROW(hipMalloc((void **)&g->gm, need));
+              g->gm_bytes = need;
+            }
+          base = g->gm;
+        }
+      else
+        {
+          HIP_THROW(hipMalloc((void **)&base, need));
+          tmp_alloc.push_back(base);
+        }
+      ws[(size_t)r] = {base, base + (size_t)(m + 1) * nloc, base + (size_t)(m + 2) * nloc,
+                       base + (size_t)(m + 3) * nloc, nloc, ops[r]->n_owned_dofs};
+    }
+  rocblas_handle h = nullptr;
+  check_blas(rocblas_create_handle(&h), "rocblas_create_handle");
+  struct Cleanup
+  {
+    rocblas_handle         h;
+    std::vector<double *> *a;
+    ~Cleanup()
+    {
+      (void)rocblas_destroy_handle(h);
+      for (double *p : *a)
+        (void)hipFree(p);
+    }
+  } cleanup{h, &tmp_alloc};
+  check_blas(rocblas_set_stream(h, s), "rocblas_set_stream");
+  check_blas(rocblas_set_pointer_mode(h, rocblas_pointer_mode_device), "pointer mode");
+  const double one = 1.0, mone = -1.0, zero = 0.0;
+  double      *d_c = nullptr; // device constants 1, -1, 0 for device pointer mode
+  HIP_THROW(hipMallocAsync((void **)&d_c, 3 * sizeof(double), s));
+  {
+    const double c3[3] = {one, mone, zero};
+    HIP_THROW(hipMemcpyAsync(d_c, c3, sizeof(c3), hipMemcpyHostToDevice, s));
+  }
+  std::vector<double *> hbuf((size_t)n);
+  auto allreduce = [&](int64_t count, int off) {
+    for (int r = 0; r < n; ++r)
+      hbuf[(size_t)r] = ws[(size_t)r].h + off;
+    gls::team_allreduce_sum(A, hbuf.data(), count, n, s);
+  };
+  auto apply_A = [&](const std::vector<double *> &dst, const std::vector<double *> &src) {
+    std::vector<void *> d(dst.begin(), dst.end()), sr(src.begin(), src.end());
+    gls::team_vmult(A, d.data(), sr.data(), n, s);
+  };
+  auto apply_P = [&](const std::vector<double *> &dst, const std::vector<double *> &src) {
+    if (mg)
+      {
+        std::vector<void *>       d(dst.begin(), dst.end());
+        std::vector<const void *> sr(src.begin(), src.end());
+        check(gls_dist_mg_vcycle(mg, n, d.data(), sr.data(), s));
+      }
+    else
+      for (int r = 0; r < n; ++r)
+        copy_vec(dst[(size_t)r], src[(size_t)r], (size_t)ws[(size_t)r].nloc * 8, s);
+  };
+  // |v|^2 over the owned rows, all-reduced, to the host
+  auto norm = [&](const std::vector<double *> &v) {
+    for (int r = 0; r < n; ++r)
+      check_blas(rocblas_ddot(h, (rocblas_int)ws[(size_t)r].nown, v[(size_t)r], 1, v[(size_t)r],
+                              1, ws[(size_t)r].h),
+                 "rocblas_ddot");
+    allreduce(1, 0);
+    double v2 = 0;
+    HIP_THROW(hipMemcpyAsync(&v2, ws[0].h, 8, hipMemcpyDeviceToHost, s));
+    HIP_THROW(hipStreamSynchronize(s));
+    return std::sqrt(v2);
+  };
+  auto vcol = [&](int r, int j) { return ws[(size_t)r].V + (size_t)j * ws[(size_t)r].nloc; };
+  std::vector<double *> Wv, Zv, Xv, Bv, V0;
+  for (int r = 0; r < n; ++r)
+    {
+      Wv.push_back(ws[(size_t)r].w);
+      Zv.push_back(ws[(size_t)r].z);
+      Xv.push_back((double *)x[r]);
+      Bv.push_back((double *)b[r]);
+      V0.push_back(vcol(r, 0));
+    }
+  // solver_l.cc:52-53, 66: tolerance max(rel |b|, abs), dst = 0
+  const double bnorm = norm(Bv);
+  const double tol   = std::max(desc->relative_tolerance * bnorm, desc->absolute_tolerance);
+  for (int r = 0; r < n; ++r)
+    {
+      HIP_THROW(hipMemsetAsync(x[r], 0, (size_t)ws[(size_t)r].nloc * 8, s));
+      copy_vec(vcol(r, 0), b[r], (size_t)ws[(size_t)r].nloc * 8, s);
+    }
+  std::vector<double> H((size_t)(m + 1) * m), g(m + 1), cs(m), sn(m), y(m), col(m + 2);
+  int    it = 0, n_rst = 0;
+  double res = bnorm;
+  while (res > tol && it < desc->max_iterations)
+    {
+      const double sc = 1.0 / res;
+      for (int r = 0; r < n; ++r)
+        {
+          rocblas_set_pointer_mode(h, rocblas_pointer_mode_host);
+          check_blas(rocblas_dscal(h, (rocblas_int)ws[(size_t)r].nloc, &sc, vcol(r, 0), 1),
+                     "rocblas_dscal");
+          rocblas_set_pointer_mode(h, rocblas_pointer_mode_device);
+        }
+      std::fill(H.begin(), H.end(), 0.0);
+      std::fill(g.begin(), g.end(), 0.0);
+      g[0]   = res;
+      int jd = 0;
+      for (int j = 0; j < m && it < desc->max_iterations; ++j)
+        {
+          std::vector<double *> Vj;
+          for (int r = 0; r < n; ++r)
+            Vj.push_back(vcol(r, j));
+          apply_P(Zv, Vj);
+          apply_A(Wv, Zv);
+          // CGS2: h1 = V^T w (owned rows), w -= V h1; h2 likewise; |w|^2
+          for (int pass = 0; pass < 2; ++pass)
+            {
+              for (int r = 0; r < n; ++r)
+                check_blas(rocblas_dgemv(h, rocblas_operation_transpose,
+                                         (rocblas_int)ws[(size_t)r].nown, j + 1, d_c,
+                                         ws[(size_t)r].V, (rocblas_int)ws[(size_t)r].nloc,
+                                         ws[(size_t)r].w, 1, d_c + 2,
+                                         ws[(size_t)r].h + pass * (m + 1), 1),
+                           "rocblas_dgemv");
+              allreduce(j + 1, pass * (m + 1));
+              for (int r = 0; r < n; ++r)
+                check_blas(rocblas_dgemv(h, rocblas_operation_none,
+                                         (rocblas_int)ws[(size_t)r].nloc, j + 1, d_c + 1,
+                                         ws[(size_t)r].V, (rocblas_int)ws[(size_t)r].nloc,
+                                         ws[(size_t)r].h + pass * (m + 1), 1, d_c,
+                                         ws[(size_t)r].w, 1),
+                           "rocblas_dgemv");
+            }
+          for (int r = 0; r < n; ++r)
+            check_blas(rocblas_ddot(h, (rocblas_int)ws[(size_t)r].nown, ws[(size_t)r].w, 1,
+                                    ws[(size_t)r].w, 1, ws[(size_t)r].h + 2 * (m + 1)),
+                       "rocblas_ddot");
+          allreduce(1, 2 * (m + 1));
+          std::vector<double> hc((size_t)(2 * (m + 1) + 1));
+          HIP_THROW(hipMemcpyAsync(hc.data(), ws[0].h, hc.size() * 8, hipMemcpyDeviceToHost, s));
+          HIP_THROW(hipStreamSynchronize(s));
+          double      *Hj = &H[(size_t)j * (m + 1)];
+          for (int i = 0; i <= j; ++i)
+            Hj[i] = hc[(size_t)i] + hc[(size_t)(m + 1 + i)];
+          const double hn = std::sqrt(std::max(0.0, hc[(size_t)(2 * (m + 1))]));
+          Hj[j + 1]       = hn;
+          if (hn > 0)
+            {
+              const double s2 = 1.0 / hn;
+              rocblas_set_pointer_mode(h, rocblas_pointer_mode_host);
+              for (int r = 0; r < n; ++r)
+                {
+                  copy_vec(vcol(r, j + 1), ws[(size_t)r].w, (size_t)ws[(size_t)r].nloc * 8, s);
+                  check_blas(rocblas_dscal(h, (rocblas_int)ws[(size_t)r].nloc, &s2,
+                                           vcol(r, j + 1), 1),
+                             "rocblas_dscal");
+                }
+              rocblas_set_pointer_mode(h, rocblas_pointer_mode_device);
+            }
+          for (int i = 0; i < j; ++i)
+            {
+              const double tt = cs[(size_t)i] * Hj[i] + sn[(size_t)i] * Hj[i + 1];
+              Hj[i + 1]       = -sn[(size_t)i] * Hj[i] + cs[(size_t)i] * Hj[i + 1];
+              Hj[i]           = tt;
+            }
+          const double rr = std::hypot(Hj[j], Hj[j + 1]);
+          cs[(size_t)j]   = rr > 0 ? Hj[j] / rr : 1.0;
+          sn[(size_t)j]   = rr > 0 ? Hj[j + 1] / rr : 0.0;
+          Hj[j]           = rr;
+          Hj[j + 1]       = 0;
+          g[(size_t)j + 1] = -sn[(size_t)j] * g[(size_t)j];
+          g[(size_t)j]     = cs[(size_t)j] * g[(size_t)j];
+          ++it;
+          ++jd;
+          res = std::fabs(g[(size_t)j + 1]);
+          if (res <= tol || hn == 0)
+            break;
+        }
+      for (int i = jd - 1; i >= 0; --i)
+        {
+          double tt = g[(size_t)i];
+          for (int c = i + 1; c < jd; ++c)
+            tt -= H[(size_t)c * (m + 1) + i] * y[(size_t)c];
+          y[(size_t)i] = tt / H[(size_t)i * (m + 1) + i];
+        }
+      // x += P (V y)
+      for (int r = 0; r < n; ++r)
+        {
+          HIP_THROW(hipMemcpyAsync(ws[(size_t)r].h, y.data(), jd * 8, hipMemcpyHostToDevice, s));
+          check_blas(rocblas_dgemv(h, rocblas_operation_none, (rocblas_int)ws[(size_t)r].nloc, jd,
+                                   d_c, ws[(size_t)r].V, (rocblas_int)ws[(size_t)r].nloc,
+                                   ws[(size_t)r].h, 1, d_c + 2, ws[(size_t)r].w, 1),
+                     "rocblas_dgemv");
+        }
+      apply_P(Zv, Wv);
+      rocblas_set_pointer_mode(h, rocblas_pointer_mode_host);
+      for (int r = 0; r < n; ++r)
+        check_blas(rocblas_daxpy(h, (rocblas_int)ws[(size_t)r].nloc, &one, ws[(size_t)r].z, 1,
+                                 (double *)x[r], 1),
+                   "rocblas_daxpy");
+      rocblas_set_pointer_mode(h, rocblas_pointer_mode_device);
+      HIP_THROW(hipStreamSynchronize(s)); // y is reused
+      if (res <= tol || it >= desc->max_iterations)
+        break;
+      // restart: V_0 = b - A x
+      apply_A(V0, Xv);
+      rocblas_set_pointer_mode(h, rocblas_pointer_mode_host);
+      for (int r = 0; r < n; ++r)
+        {
+          const double m1 = -1.0;
+          check_blas(rocblas_dscal(h, (rocblas_int)ws[(size_t)r].nloc, &m1, vcol(r, 0), 1),
+                     "rocblas_dscal");
+          check_blas(rocblas_daxpy(h, (rocblas_int)ws[(size_t)r].nloc, &one, (const double *)b[r],
+                                   1, vcol(r, 0), 1),
+                     "rocblas_daxpy");
+        }
+      rocblas_set_pointer_mode(h, rocblas_pointer_mode_device);
+      res = norm(V0);
+      ++n_rst;
+    }
+  HIP_THROW(hipFreeAsync(d_c, s));
+  HIP_THROW(hipStreamSynchronize(s));
+  if (result)
+    {
+      result->n_iterations     = it;
+      result->n_restarts       = n_rst;
+      result->converged        = res <= tol;
+      result->initial_residual = bnorm;
+      result->final_residual   = res;
+      result->tolerance        = tol;
+    }
+  if (res > tol)
+    {
+      gls::set_error("gls_dist_gmres_solve: no convergence in " + std::to_string(it) +
+                     " iterations (SolverControl::NoConvergence)");
+      return 1;
+    }
+  GLS_CATCH
+}
+
+} // extern "C"

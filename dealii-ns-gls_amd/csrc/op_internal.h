@@ -205,6 +205,19 @@ fused_relax_ok(const glsOp_ *op)
   return op->use_brick && op->n_owned_dofs == op->n_dofs && op->faces.n == 0;
 }
 
+// team primitives of the partitioned multigrid / GMRES (dist.hip): the ranks
+// one process drives in lockstep — one RCCL rank, or all members of an
+// in-process group (rank order)
+glsOp_ *dist_op(glsDist d);
+int     dist_rank(glsDist d);
+int     dist_world(glsDist d);
+void    team_vmult(glsDist const *m, void *const *dst, void *const *src, int n, hipStream_t s);
+void    team_update_ghosts(glsDist const *m, void *const *v, int n, hipStream_t s);
+void    team_compress_add(glsDist const *m, void *const *v, int n, hipStream_t s);
+// buf[r][0 .. count) <- the sum over the team's ranks (ncclAllReduce / member order)
+void    team_allreduce_sum(glsDist const *m, double *const *buf, int64_t count, int n,
+                           hipStream_t s);
+
 // the same operator pieces without staging (GMRES, multigrid)
 void op_vmult_device(glsOp op, void *dst, const void *src, hipStream_t s);
 void op_inverse_diagonal_device(glsOp op, void *diag, hipStream_t s);

@@ -36,7 +36,10 @@ EXPORTS = [
     "gls_op_get_max_u", "gls_mg_set_vector_layout", "gls_dist_update_ghost_values",
     "gls_dist_get_max_u", "gls_op_compute_diagonal", "gls_op_invert_diagonal", "gls_mg_relax",
     "gls_dist_compress_add", "gls_op_brick_shape", "gls_op_cell_permutation",
-    "gls_discover_bricks", "gls_mg_coarse_statistics", "gls_mg_coarse_setup_times", "gls_op_element_matrices",
+    "gls_discover_bricks", "gls_mg_coarse_statistics", "gls_mg_coarse_setup_times",
+    "gls_dist_mg_create", "gls_dist_mg_destroy", "gls_dist_mg_set_linearization_point",
+    "gls_dist_mg_setup", "gls_dist_mg_get_relaxation", "gls_dist_mg_vcycle",
+    "gls_dist_gmres_solve", "gls_op_element_matrices",
     "gls_op_system_matrix", "gls_op_n_outflow_faces", "gls_op_outflow_face_points",
     "gls_op_set_outflow_target",
 ]
@@ -157,6 +160,15 @@ def lib():
         L.gls_op_set_outflow_target.argtypes = [vp, vp, vp]
         L.gls_mg_coarse_statistics.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.gls_mg_coarse_setup_times.argtypes = [vp, vp, C.POINTER(C.c_int)]
+        L.gls_dist_mg_create.argtypes = [vp, vp, vp]
+        L.gls_dist_mg_destroy.argtypes = [vp]
+        L.gls_dist_mg_destroy.restype = None
+        L.gls_dist_mg_set_linearization_point.argtypes = [vp, C.c_int, vp, vp, C.c_int, vp, vp]
+        L.gls_dist_mg_setup.argtypes = [vp, C.c_int, vp]
+        L.gls_dist_mg_get_relaxation.argtypes = [vp, C.c_int, C.POINTER(C.c_double),
+                                                 C.POINTER(C.c_double)]
+        L.gls_dist_mg_vcycle.argtypes = [vp, C.c_int, vp, vp, vp]
+        L.gls_dist_gmres_solve.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp]
         L.gls_discover_bricks.argtypes = [C.c_int, C.c_int, i64, vp, vp, vp]
         L.gls_last_error.restype = C.c_char_p
         _lib = L
@@ -556,6 +568,118 @@ class PartitionedOperator:
         _check(lib().gls_dist_vmult_group(C.cast(hs, C.c_void_p), C.cast(ds, C.c_void_p),
                                           C.cast(ss, C.c_void_p), n, _stream()))
         return dsts
+
+
+class DistMGDesc(C.Structure):
+    _fields_ = [("mg", MGDesc), ("child", C.c_void_p), ("owned_global_nodes", C.c_void_p),
+                ("n_global_nodes", C.c_void_p), ("coarse_global", C.c_void_p),
+                ("coarse_local_global", C.c_void_p)]
+
+
+def _handles(objs):
+    n = len(objs)
+    return (C.c_void_p * n)(*[o.h.value for o in objs]), n
+
+
+def _ptrs(ts):
+    return (C.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
+class PartitionedMultigrid:
+    """The rank-local handle of the native partitioned multigrid
+    (gls_dist_mg_*, csrc/dist_mg.hip): PreconditionerGMG over partitioned
+    level operators (PartitionedOperator handles of one rank, coarse to
+    fine).  child[l] (l >= 1): rank-local child lattice with the global-first
+    NOT_OWNER bits; owned_global_nodes[l]: global ids of the owned nodes;
+    coarse_global (direct coarse solve): a NavierStokesOperator on the whole
+    coarse mesh with coarse_l2g (level-0 local node -> global node).  The
+    team methods take every handle this process drives: [self] for an RCCL
+    rank, all members of an in-process group in rank order (tests)."""
+
+    def __init__(self, levels, child, owned_global_nodes, n_global_nodes,
+                 smoothing_n_iterations=5, smoothing_eig_n_iterations=20, smoothing_range=20.0,
+                 coarse_n_iterations=10, outer_precision="f64", compute_evs_n_levels=0,
+                 coarse_global=None, coarse_l2g=None):
+        n = len(levels)
+        outer = GLS_F64 if outer_precision in ("f64", GLS_F64) else GLS_F32
+        md = MGDesc(n, smoothing_n_iterations, smoothing_eig_n_iterations, smoothing_range,
+                    coarse_n_iterations, outer, compute_evs_n_levels, 0, 1e-4, 10000)
+        self._keep = [None] + [np.ascontiguousarray(c, dtype=np.uint32) for c in child[1:]]
+        self._own = [np.ascontiguousarray(g, dtype=np.int64) for g in owned_global_nodes]
+        self._ng = np.ascontiguousarray(n_global_nodes, dtype=np.int64)
+        chp = (C.c_void_p * n)(*([None] + [c.ctypes.data for c in self._keep[1:]]))
+        ogp = (C.c_void_p * n)(*[g.ctypes.data for g in self._own])
+        self._l2g = None if coarse_l2g is None else np.ascontiguousarray(coarse_l2g, np.int64)
+        self.coarse_global = coarse_global
+        d = DistMGDesc(md, C.cast(chp, C.c_void_p), C.cast(ogp, C.c_void_p),
+                       self._ng.ctypes.data,
+                       None if coarse_global is None else coarse_global.h,
+                       None if self._l2g is None else self._l2g.ctypes.data)
+        lv = (C.c_void_p * n)(*[L.h.value for L in levels])
+        h = C.c_void_p()
+        _check(lib().gls_dist_mg_create(C.byref(d), C.cast(lv, C.c_void_p), C.byref(h)))
+        self.h = h
+        self._ptr_keep = (chp, ogp, lv)
+        self.levels = levels
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().gls_dist_mg_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def relaxation(self, level):
+        w, lam = C.c_double(), C.c_double()
+        _check(lib().gls_dist_mg_get_relaxation(self.h, level, C.byref(w), C.byref(lam)))
+        return w.value, lam.value
+
+    @staticmethod
+    def set_linearization_point(team, u_fine, hist_fine=None, weights=None):
+        hs, n = _handles(team)
+        us = _ptrs(u_fine)
+        nh = 0 if not hist_fine else len(hist_fine[0])
+        hrows = [_ptrs(h) for h in hist_fine] if nh else []
+        hp = (C.c_void_p * n)(*[C.cast(r, C.c_void_p).value for r in hrows]) if nh else None
+        w = None
+        if weights is not None:
+            w = np.ascontiguousarray(weights, dtype=np.float64)
+        _check(lib().gls_dist_mg_set_linearization_point(
+            C.cast(hs, C.c_void_p), n, C.cast(us, C.c_void_p),
+            None if hp is None else C.cast(hp, C.c_void_p), nh,
+            None if w is None else w.ctypes.data, _stream()))
+
+    @staticmethod
+    def setup(team):
+        hs, n = _handles(team)
+        _check(lib().gls_dist_mg_setup(C.cast(hs, C.c_void_p), n, _stream()))
+
+    @staticmethod
+    def vcycle(team, dsts, srcs):
+        hs, n = _handles(team)
+        _check(lib().gls_dist_mg_vcycle(C.cast(hs, C.c_void_p), n, C.cast(_ptrs(dsts), C.c_void_p),
+                                        C.cast(_ptrs(srcs), C.c_void_p), _stream()))
+        return dsts
+
+
+def dist_gmres_solve(ops, mgs, xs, bs, n_max_iterations=10000, absolute_tolerance=1e-12,
+                     relative_tolerance=1e-8, max_n_tmp_vectors=30):
+    """gls_dist_gmres_solve: LinearSolverGMRES::solve on rank-local vectors of
+    the FP64 partitioned operator (PartitionedOperator handles of the team),
+    preconditioned by the native partitioned multigrid (or identity, mgs
+    None).  Returns the result dict; raises GlsError on no convergence."""
+    hs, n = _handles(ops)
+    ms = None if mgs is None else _handles(mgs)[0]
+    desc = GMRESDesc(max_n_tmp_vectors, n_max_iterations, absolute_tolerance, relative_tolerance)
+    res = GMRESResult()
+    rc = lib().gls_dist_gmres_solve(C.cast(hs, C.c_void_p),
+                                    None if ms is None else C.cast(ms, C.c_void_p), n,
+                                    C.byref(desc), C.cast(_ptrs(xs), C.c_void_p),
+                                    C.cast(_ptrs(bs), C.c_void_p), C.byref(res), _stream())
+    out = {f: getattr(res, f) for f, _ in GMRESResult._fields_}
+    _check(rc)
+    return out
 
 
 class Multigrid:

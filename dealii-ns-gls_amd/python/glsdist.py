@@ -737,6 +737,121 @@ class DistributedMultigrid:
         return dst
 
 
+def rank_child_lattices(meshes, parts_per_level, rank):
+    """Rank-local child lattices (local fine node ids) with the global-first
+    NOT_OWNER bits (bit 31) for every level pair, [None, l = 1, ...]."""
+    out = [None]
+    for l in range(1, len(meshes)):
+        G = np.asarray(meshes[l - 1].child_lattice(meshes[l]), dtype=np.int64)
+        own = global_first_owners(G)
+        pc, pf = parts_per_level[l - 1][rank], parts_per_level[l][rank]
+        g2l = np.full(meshes[l].n_nodes, -1, dtype=np.int64)
+        g2l[pf.local_nodes] = np.arange(pf.n_nodes)
+        loc = g2l[G[pc.cell_begin:pc.cell_end]]
+        if (loc < 0).any():
+            raise ValueError("a child lattice node is not local to the fine partition")
+        ch = loc.astype(np.uint32)
+        ch[~own[pc.cell_begin:pc.cell_end]] |= np.uint32(0x80000000)
+        out.append(ch)
+    return out
+
+
+class NativeGroupMultigrid:
+    """Every rank of a partitioned multigrid hierarchy in ONE process on one
+    device (an in-process group), driven through the native team calls of
+    the C-ABI (glsamd.PartitionedMultigrid: gls_dist_mg_* and
+    gls_dist_gmres_solve, csrc/dist_mg.hip) — the single-GPU test of the
+    distributed V-cycle and GMRES that RCCL ranks run one per GPU.  Levels on
+    the same coarse-cell partition (main.cc:398-400); the FP64 outer operator
+    on the finest level's partition."""
+
+    def __init__(self, meshes, cmasks, world, precision="f32", coarse_n_iterations=10,
+                 **mg_kwargs):
+        import glsamd
+        self.world = world
+        n0 = meshes[0].n_cells
+        cb = coarse_bounds(n0, world)
+        self.parts, self.ranks, self.native = [], [], []
+        for m, cm in zip(meshes, cmasks):
+            ratio = m.n_cells // n0
+            parts = build_partitions(m, world, [b * ratio for b in cb])
+            ranks = [RankOperator(m, cm, p, precision) for p in parts]
+            nat = []
+            for r in ranks:
+                nat.append(r.eng.partitioned(r.part, group=nat[0] if nat else None))
+            self.parts.append(parts)
+            self.ranks.append(ranks)
+            self.native.append(nat)
+        fine_parts = build_partitions(meshes[-1], world,
+                                      [b * (meshes[-1].n_cells // n0) for b in cb])
+        self.fine = [RankOperator(meshes[-1], cmasks[-1], p, "f64") for p in fine_parts]
+        self.fine_native = []
+        for r in self.fine:
+            self.fine_native.append(r.eng.partitioned(r.part, group=self.fine_native[0]
+                                                      if self.fine_native else None))
+        self.coarse_ops = [None] * world
+        if coarse_n_iterations < 0:
+            self.coarse_ops = [glsamd.NavierStokesOperator(meshes[0], cmasks[0], precision)
+                               for _ in range(world)]
+        self.mg = []
+        for r in range(world):
+            child = rank_child_lattices(meshes, self.parts, r)
+            self.mg.append(glsamd.PartitionedMultigrid(
+                [self.native[l][r] for l in range(len(meshes))], child,
+                [self.parts[l][r].local_nodes[:self.parts[l][r].n_owned]
+                 for l in range(len(meshes))],
+                [m.n_nodes for m in meshes], coarse_n_iterations=coarse_n_iterations,
+                coarse_global=self.coarse_ops[r],
+                coarse_l2g=self.parts[0][r].local_nodes if coarse_n_iterations < 0 else None,
+                **mg_kwargs))
+
+    def setup(self, params, u_star, hist=None, weights=None):
+        """Parameters on every operator, the finest linearization point and
+        history (replicated global arrays) scattered to the ranks, injected
+        down the levels natively, then gls_dist_mg_setup; the FP64 outer
+        operator gets the fine vectors directly."""
+        import torch
+        for ranks in self.ranks:
+            for r in ranks:
+                r.eng.set_parameters(**params)
+        for op in self.coarse_ops:
+            if op is not None:
+                op.set_parameters(**params)
+        fine = self.ranks[-1]
+        u = [r.local_from_global(u_star) for r in fine]
+        h = None
+        if hist is not None and params.get("order", 0) > 0:
+            h = [[r.local_from_global(x) for x in hist] for r in fine]
+        glsamd_mg = type(self.mg[0])
+        glsamd_mg.set_linearization_point(self.mg, u, h, weights)
+        glsamd_mg.setup(self.mg)
+        for r in self.fine:
+            r.eng.set_parameters(**params)
+            r.eng.set_linearization_point(r.local_from_global(u_star))
+            if h is not None:
+                r.eng.set_previous_solution([r.local_from_global(x) for x in hist], weights)
+        torch.cuda.synchronize()
+
+    def scatter(self, g, ranks=None):
+        return [r.local_from_global(g) for r in (ranks or self.fine)]
+
+    def gather(self, vs, ranks=None):
+        import torch
+        ranks = ranks or self.fine
+        n = sum(r.n_owned_dofs for r in ranks)
+        g = torch.zeros(n, dtype=vs[0].dtype, device=vs[0].device)
+        for r, v in zip(ranks, vs):
+            g.index_copy_(0, r.global_dofs[:r.n_owned_dofs], v[:r.n_owned_dofs])
+        return g
+
+    def vcycle(self, dsts, srcs):
+        return type(self.mg[0]).vcycle(self.mg, dsts, srcs)
+
+    def gmres(self, xs, bs, **kw):
+        import glsamd
+        return glsamd.dist_gmres_solve(self.fine_native, self.mg, xs, bs, **kw)
+
+
 class RedundantCoarseLU:
     """The deck's direct coarse solver for a partitioned hierarchy
     (multigrid.cc:448-455, 477-481): every rank holds the whole coarse level

@@ -411,6 +411,62 @@ typedef struct
 glsStatus gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x,
                           const void *b, glsGMRESResult *result, void *stream);
 
+/* ---- partitioned multigrid preconditioner and GMRES:
+ * PreconditionerGMG::initialize / vmult (multigrid.cc:247-370, 202-220) over
+ * partitioned level operators and LinearSolverGMRES::solve (solver_l.cc:
+ * 45-74) with all-reduced dots, on rank-local [owned | ghost] device vectors.
+ * Every call takes a TEAM: the handles of the ranks this process drives —
+ * n = 1 for a rank of an RCCL communicator (the production case, one process
+ * per GPU), or all members of an in-process group in rank order (tests).
+ * The levels are glsDist handles on the same coarse-cell partition
+ * (main.cc:398-400); parameters are set on every level operator (and the
+ * coarse operator) with gls_op_set_parameters before the linearization
+ * point. */
+typedef struct glsDistMG_ *glsDistMG;
+typedef struct
+{
+  glsMGDesc              mg;   /* as gls_mg_create; coarse_iterate must be 0 */
+  /* child[l] (l >= 1): the rank-local child lattice of the rank's level l-1
+   * cells into level-l local nodes, bit 31 set where the cell is not the
+   * GLOBAL first cell touching the node (the owner-only transfers) */
+  const uint32_t *const *child;
+  const int64_t *const  *owned_global_nodes; /* [n_levels][n_owned_nodes(l)]: global
+                                                node ids (power-iteration start
+                                                vector on the global dof index) */
+  const int64_t         *n_global_nodes;     /* [n_levels] */
+  /* coarse_n_iterations < 0 ("direct"): a single-domain operator on the whole
+   * level-0 mesh (global node numbering, parameters set), solved redundantly
+   * on every rank, and the map of the rank's level-0 local nodes (owned |
+   * ghost) to global nodes; NULL otherwise */
+  glsOp                  coarse_global;
+  const int64_t         *coarse_local_global;
+} glsDistMGDesc;
+glsStatus gls_dist_mg_create(const glsDistMGDesc *desc, const glsDist *levels, glsDistMG *out);
+void      gls_dist_mg_destroy(glsDistMG mg);
+/* interpolate_to_mg (main.cc:772-803) of the finest level's linearization
+ * point and history (level precision, rank-local) down the hierarchy, set on
+ * every level operator (and the redundant coarse operator); hist_fine[r] is
+ * rank r's SolutionHistory as gls_op_set_previous_solution takes it (n_hist
+ * entries, entry 0 unused; n_hist 0: none) */
+glsStatus gls_dist_mg_set_linearization_point(glsDistMG const *team, int n,
+                                              const void *const *u_fine,
+                                              const void *const *const *hist_fine, int n_hist,
+                                              const double *weights, void *stream);
+/* diagonals (compress(add) + inversion) and power-iteration relaxation
+ * factors with all-reduced dots; the redundant coarse LU */
+glsStatus gls_dist_mg_setup(glsDistMG const *team, int n, void *stream);
+glsStatus gls_dist_mg_get_relaxation(glsDistMG mg, int level, double *omega, double *lambda_max);
+/* one V-cycle on the finest level's rank-local vectors (outer precision) */
+glsStatus gls_dist_mg_vcycle(glsDistMG const *team, int n, void *const *dst,
+                             const void *const *src, void *stream);
+/* GMRES on the FP64 partitioned operator A (the finest level's partition),
+ * preconditioned by one V-cycle per application (mg NULL: identity);
+ * x = 0 on entry; status 1 on no convergence with *result filled */
+glsStatus gls_dist_gmres_solve(glsDist const *A, glsDistMG const *mg, int n,
+                               const glsGMRESDesc *desc, void *const *x, const void *const *b,
+                               glsGMRESResult *result, void *stream);
+
+
 const char *gls_last_error(void);
 
 #ifdef __cplusplus

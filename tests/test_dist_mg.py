@@ -286,3 +286,33 @@ def test_rccl_world1_direct_coarse():
         assert rel_err(top.gather_global(x1).cpu().numpy(), x2.cpu().numpy()) < 1e-3
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_native_mg_plan(world):
+    """The per-rank plan of the native partitioned multigrid
+    (glsdist.rank_child_lattices -> gls_dist_mg_create): on every level pair
+    each global fine node is claimed (NOT_OWNER bit clear) by exactly one
+    (rank, coarse cell) lattice entry, and that rank owns the node in the
+    fine partition — the invariant the owner-only restriction and
+    prolongation rely on (every owned fine row is written / read by its own
+    rank only)."""
+    from helpers import deck
+    d = deck("input_hoffmann_3D_Re3900.json")
+    meshes = [d.mesh(r) for r in range(2)]
+    n0 = meshes[0].n_cells
+    cb = glsdist.coarse_bounds(n0, world)
+    parts = [glsdist.build_partitions(m, world, [b * (m.n_cells // n0) for b in cb])
+             for m in meshes]
+    claims = np.zeros(meshes[1].n_nodes, dtype=np.int64)
+    for r in range(world):
+        ch = glsdist.rank_child_lattices(meshes, parts, r)[1]
+        pf = parts[1][r]
+        own = (ch & np.uint32(0x80000000)) == 0
+        loc = (ch & np.uint32(0x7FFFFFFF)).astype(np.int64)
+        assert (loc < pf.n_nodes).all()
+        gl = pf.local_nodes[loc[own]]
+        np.add.at(claims, gl, 1)
+        # the claiming rank owns the node (local index in the owned prefix)
+        assert (loc[own] < pf.n_owned).all()
+    assert (claims == 1).all()
