@@ -54,8 +54,5 @@ clean:
 
 .PHONY: all mesh amd oracle cpptest clean
 
-# diagnostic ablation builds (timing only, wrong results by design)
-abl:
-	@mkdir -p $(LIBDIR)/abl
-	for v in 1 2 4 8 14; do $(HIPCC) $(HIPFLAGS) -DGLS_ABL=$$v -shared -o $(LIBDIR)/abl/libglsamd_abl$$v.so $(AMD_SRC) $(AMD_LIBS) & done; wait
-.PHONY: abl
+# diagnostic variant builds (timing experiments; wrong results by design for
+# the GLS_BABL ablations): scripts/build_variants.sh < "<name> <-D flags>" lines

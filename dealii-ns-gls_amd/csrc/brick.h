@@ -300,6 +300,13 @@ struct BrickLDS
 #ifndef GLS_INV_ZERO
 #define GLS_INV_ZERO 1
 #endif
+// GLS_BABL: diagnostic-only ablation builds of k_brick (timing only, wrong
+// results by design; never the product library): 1 no cell rounds (prologue
+// + write-out), 2 no table / geometry loads, 4 no LDS sweeps, 8 no q-point
+// physics
+#ifndef GLS_BABL
+#define GLS_BABL 0
+#endif
 // Experimental table formulations (measured round 2), off by
 // default so that the brick kernel streams the reference's per-q tables
 // (operator_ns.h:120-132, SURVEY §8d B_tab):
@@ -411,6 +418,28 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
   // quadrature weight, the inactive-lane mask) would make the compiler wait
   // for the loads at the prefetch point (an s_waitcnt vmcnt(0) in the middle
   // of the round); jxw() applies both at the point of use
+  if (GLS_BABL & 2)
+    {
+#pragma unroll
+      for (int i = 0; i < dim; ++i)
+#pragma unroll
+        for (int e = 0; e < dim; ++e)
+          r.inv[i][e] = i == e ? T(1) + T(0.01) * p : T(0);
+      r.JxW = T(1) + T(0.001) * lcell;
+#pragma unroll
+      for (int d = 0; d < dim; ++d)
+        {
+          r.U[d] = T(0.1) * d + T(0.01) * p, r.T1[d] = T(0.2), r.UT[d] = T(0.3);
+#pragma unroll
+          for (int e = 0; e < dim; ++e)
+            r.GU[d][e] = T(0.05) * (d + e);
+        }
+#pragma unroll
+      for (int i = 0; i < LaneData<dim, T, MODE>::NOLD; ++i)
+        r.oldg[i] = 0;
+      r.d1 = T(0.5), r.d2 = T(0.25), r.h = T(1);
+      return;
+    }
   if (general)
     {
       const int64_t gq = qindex<dim, n>(cell, p, a.n_cells);
@@ -639,7 +668,10 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       tg[it]      = i < L ? bt[i] : 0u;
     }
   uint32_t binfo   = a.brick_geo[brick];
-  bool     general = (binfo & 1u) != 0;
+#ifndef GLS_FORCE_CART
+#define GLS_FORCE_CART 0
+#endif
+  bool     general = !GLS_FORCE_CART && (binfo & 1u) != 0;
   int      ncell   = (int)(binfo >> 8);
   uint32_t cell0   = a.brick_cell0[brick];
   uint32_t chunk0  = a.brick_chunk0[brick];
@@ -761,7 +793,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       cell0_n  = a.brick_cell0[next];
       chunk0_n = a.brick_chunk0[next];
     }
-  for (int base = 0; base < ncell; base += step)
+  for (int base = 0; base < ((GLS_BABL & 1) ? 0 : ncell); base += step)
     {
       // GLS_LATE_PREFETCH: a round's geometry and tables are issued at the
       // start of that round (in flight during its evaluate sweeps) instead
@@ -772,6 +804,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
                                    in_wave, p, pa, cur);
 
       // ---- evaluate: x sweep straight from the src lattice, then y (, z)
+      if (!(GLS_BABL & 4))
       {
         const int lb = cur.li - pa[0];
         if (in_wave)
@@ -782,7 +815,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       wave_sync();
       V *in = A, *out = B;
 #pragma unroll
-      for (int ax = 1; ax < dim; ++ax)
+      for (int ax = 1; ax < ((GLS_BABL & 4) ? 1 : dim); ++ax)
         {
           if (in_wave)
 #pragma unroll
@@ -806,7 +839,24 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
         }
       // left-over lanes stay out of the reads (they would only add bank
       // conflicts in their ds_read_b128 lane groups)
-      if (in_wave)
+      if (GLS_BABL & 4)
+        {
+#pragma unroll
+          for (int kp = 0; kp < NP; ++kp)
+            {
+              const V v = s_src[kp * LP + cur.li];
+#pragma unroll
+              for (int w = 0; w < W; ++w)
+                if (kp * W + w < nc)
+                  {
+                    val[kp * W + w] = v[w];
+#pragma unroll
+                    for (int ax = 0; ax < dim; ++ax)
+                      gref[kp * W + w][ax] = v[w] * sS[ax];
+                  }
+            }
+        }
+      else if (in_wave)
 #pragma unroll
       for (int kp = 0; kp < NP; ++kp)
         {
@@ -873,7 +923,18 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
             u2 += cur.U[d] * cur.U[d];
           delta_qwise(u2, cur.h, a.nu, a.stau, d1, d2);
         }
-      if constexpr (MODE == MODE_NEWTON && GLS_NEWTON_T1)
+      if constexpr ((GLS_BABL & 8) != 0)
+        {
+#pragma unroll
+          for (int c = 0; c < nc; ++c)
+            {
+              vr[c] = val[c] * cur.U[c % dim] + cur.d1;
+#pragma unroll
+              for (int e = 0; e < dim; ++e)
+                gr[c][e] = (c < dim ? gu[c][e] : gp[e]) * cur.GU[c % dim][e] + cur.d2 * cur.T1[e] + cur.UT[e];
+            }
+        }
+      else if constexpr (MODE == MODE_NEWTON && GLS_NEWTON_T1)
         qpoint_newton_t1<dim, T>(val, val[dim], gu, gp, cur.U, cur.GU, cur.T1, d1, d2, a.nu,
                                  a.w0, a.td, vr, gr);
       else
@@ -922,8 +983,20 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       // fused with the accumulation into the brick lattice
       V wv[NP];
       to_packs<V, T, nc, NP, W>(wq, wv);
+      if (GLS_BABL & 4)
+        {
 #pragma unroll
-      for (int ax0 = 0; ax0 < dim; ax0 += 2)
+          for (int kp = 0; kp < NP; ++kp)
+#pragma unroll
+            for (int ax = 0; ax < dim; ++ax)
+              {
+                V g0[NP];
+                to_packs<V, T, nc, NP, W>(ghat[ax], g0);
+                wv[kp] += g0[kp];
+              }
+        }
+#pragma unroll
+      for (int ax0 = 0; ax0 < ((GLS_BABL & 4) ? 0 : dim); ax0 += 2)
         {
           if (in_wave)
             {
@@ -993,7 +1066,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       in  = A;
       out = B;
 #pragma unroll
-      for (int ax = dim - 1; ax >= 1; --ax)
+      for (int ax = dim - 1; ax >= ((GLS_BABL & 4) ? dim : 1); --ax)
         {
           if (in_wave)
 #pragma unroll
@@ -1011,7 +1084,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
 #pragma unroll
         for (int kp = 0; kp < NP; ++kp)
           {
-            const V r = contract_c<n>(in + kp * BL::KS, cx, q - pa[0], 1);
+            const V r = (GLS_BABL & 4) ? wv[kp] : contract_c<n>(in + kp * BL::KS, cx, q - pa[0], 1);
 #pragma unroll
             for (int w = 0; w < W; ++w)
               if (kp * W + w < nc)

@@ -456,12 +456,15 @@ void
 cell_jacobians(int dim, const Basis1D &b, const double *X /* [nloc][dim] */,
                std::vector<double> &J /* [nq][dim][dim] */)
 {
-  const int n = b.n, nq = dim == 3 ? n * n * n : n * n;
+  // b.S / b.D are [q][i] with qp.size() quadrature points and n support
+  // points (a mapping basis may differ in degree from the element's)
+  const int n = b.n, m = (int)b.qp.size();
+  const int nq = dim == 3 ? m * m * m : m * m, nl = dim == 3 ? n * n * n : n * n;
   J.assign((size_t)nq * dim * dim, 0.0);
   for (int q = 0; q < nq; ++q)
     {
-      const int qa[3] = {q % n, (q / n) % n, dim == 3 ? q / (n * n) : 0};
-      for (int i = 0; i < nq; ++i)
+      const int qa[3] = {q % m, (q / m) % m, dim == 3 ? q / (m * m) : 0};
+      for (int i = 0; i < nl; ++i)
         {
           const int ia[3] = {i % n, (i / n) % n, dim == 3 ? i / (n * n) : 0};
           double    sv[3], dv[3];
@@ -482,6 +485,37 @@ cell_jacobians(int dim, const Basis1D &b, const double *X /* [nloc][dim] */,
             }
         }
     }
+}
+
+// the Lagrange basis of MappingQ(m) (Gauss-Lobatto support points, as
+// Basis1D(m)) and its derivative at the given quadrature points:
+// S[q*n+i], D[q*n+i] with n = m + 1 and qp.size() points
+Basis1D
+mapping_basis(int m, const std::vector<double> &qp)
+{
+  Basis1D b(m);
+  const int n = b.n, nq = (int)qp.size();
+  b.qp = qp;
+  b.S.assign((size_t)nq * n, 0.0);
+  b.D.assign((size_t)nq * n, 0.0);
+  for (int q = 0; q < nq; ++q)
+    for (int i = 0; i < n; ++i)
+      {
+        double v = 1, dv = 0;
+        for (int j = 0; j < n; ++j)
+          if (j != i)
+            {
+              double prod = 1.0 / (b.nodes[i] - b.nodes[j]);
+              for (int l = 0; l < n; ++l)
+                if (l != i && l != j)
+                  prod *= (qp[q] - b.nodes[l]) / (b.nodes[i] - b.nodes[l]);
+              dv += prod;
+              v *= (qp[q] - b.nodes[j]) / (b.nodes[i] - b.nodes[j]);
+            }
+        b.S[(size_t)q * n + i] = v;
+        b.D[(size_t)q * n + i] = dv;
+      }
+  return b;
 }
 
 void
@@ -1310,8 +1344,11 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
   if ((d->dim != 2 && d->dim != 3) || d->degree < 1 || d->degree > 3 ||
       (d->precision != GLS_F64 && d->precision != GLS_F32) || d->n_cells < 0 || d->n_nodes < 0 ||
       d->n_owned_nodes < 0 || d->n_owned_nodes > d->n_nodes || !d->cell_nodes ||
-      !d->node_coords || !d->node_cmask || !d->cell_measure || !d->cell_hmin)
+      !d->node_coords || !d->node_cmask || !d->cell_measure || !d->cell_hmin ||
+      (d->mapping_points && (d->mapping_degree < 1 || d->mapping_degree > 3)))
     throw std::runtime_error("gls_op_create: invalid descriptor");
+  if (d->mapping_points && d->n_outflow_faces > 0)
+    throw std::runtime_error("gls_op_create: outflow faces with mapping_points are not supported");
   if (d->n_nodes >= (int64_t)NODE_MASK)
     throw std::runtime_error("gls_op_create: too many local nodes for 28-bit node indices");
   // an arbitrary cell order (brick[0] < 0, e.g. deal.II's MatrixFree cell
@@ -1322,7 +1359,7 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
   glsOpDesc             dd     = *d;
   gls::BrickPlan        plan;
   std::vector<uint32_t> p_nodes;
-  std::vector<double>   p_meas, p_hmin;
+  std::vector<double>   p_meas, p_hmin, p_map;
   if (d->brick[0] < 0)
     {
       dd.brick[0] = dd.brick[1] = dd.brick[2] = 0;
@@ -1345,6 +1382,19 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
                         p_nodes.begin() + c * nqc);
               p_meas[c] = d->cell_measure[e];
               p_hmin[c] = d->cell_hmin[e];
+            }
+          if (d->mapping_points)
+            {
+              const int nm  = d->mapping_degree + 1;
+              const int nmq = (d->dim == 3 ? nm * nm * nm : nm * nm) * d->dim;
+              p_map.resize((size_t)d->n_cells * nmq);
+              for (int64_t c = 0; c < d->n_cells; ++c)
+                {
+                  const int64_t e = plan.perm[(size_t)c];
+                  std::copy(d->mapping_points + e * nmq, d->mapping_points + (e + 1) * nmq,
+                            p_map.begin() + c * nmq);
+                }
+              dd.mapping_points = p_map.data();
             }
           dd.cell_nodes   = p_nodes.data();
           dd.cell_measure = p_meas.data();
@@ -1417,12 +1467,23 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
   std::vector<double>   cart_rows, gen_rows;
   std::vector<double>   X((size_t)nq * dim), J;
   int64_t               n_cart = 0, n_gen = 0;
+  // a mapping of its own degree (glsOpDesc.mapping_points): its basis at the
+  // element's quadrature points
+  Basis1D mb(d->mapping_points ? d->mapping_degree : op->degree);
+  if (d->mapping_points)
+    mb = mapping_basis(d->mapping_degree, op->basis.qp);
+  const int nmq = d->mapping_points ? (dim == 3 ? mb.n * mb.n * mb.n : mb.n * mb.n) : nq;
   for (int64_t c = 0; c < d->n_cells; ++c)
     {
-      for (int i = 0; i < nq; ++i)
-        for (int e = 0; e < dim; ++e)
-          X[i * dim + e] = d->node_coords[(size_t)d->cell_nodes[c * nq + i] * dim + e];
-      cell_jacobians(dim, op->basis, X.data(), J);
+      if (d->mapping_points)
+        cell_jacobians(dim, mb, d->mapping_points + (size_t)c * nmq * dim, J);
+      else
+        {
+          for (int i = 0; i < nq; ++i)
+            for (int e = 0; e < dim; ++e)
+              X[i * dim + e] = d->node_coords[(size_t)d->cell_nodes[c * nq + i] * dim + e];
+          cell_jacobians(dim, op->basis, X.data(), J);
+        }
       double scale = 0;
       for (int e = 0; e < dim; ++e)
         scale = std::max(scale, std::abs(J[e * dim + e]));

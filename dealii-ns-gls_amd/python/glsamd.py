@@ -54,7 +54,8 @@ class OpDesc(C.Structure):
                 ("node_cmask", C.c_void_p), ("cell_measure", C.c_void_p),
                 ("cell_hmin", C.c_void_p), ("brick", C.c_int * 3),
                 ("n_outflow_faces", C.c_int64), ("outflow_cells", C.c_void_p),
-                ("outflow_face_no", C.c_void_p), ("outflow_kind", C.c_void_p)]
+                ("outflow_face_no", C.c_void_p), ("outflow_kind", C.c_void_p),
+                ("mapping_degree", C.c_int), ("mapping_points", C.c_void_p)]
 
 OUTFLOW_KIND = {"cut": 1, "nitsche": 2}
 
@@ -263,6 +264,14 @@ class NavierStokesOperator:
             d.n_outflow_faces = len(fc)
             d.outflow_cells, d.outflow_face_no, d.outflow_kind = (
                 fc.ctypes.data, fn.ctypes.data, kind.ctypes.data)
+        mp = getattr(mesh, "mapping_points", None)
+        mapping = mp() if callable(mp) else None
+        if mapping is not None:
+            # MappingQ of the parent (FE_Q_iso_Q1 level): per-cell support points
+            mdeg, pts = mapping
+            pts = np.ascontiguousarray(pts if cells is None else pts[cells], dtype=np.float64)
+            self._keep.append(pts)
+            d.mapping_degree, d.mapping_points = int(mdeg), pts.ctypes.data
         h = C.c_void_p()
         _check(lib().gls_op_create(C.byref(d), C.byref(h)))
         self.h = h

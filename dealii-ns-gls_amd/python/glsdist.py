@@ -160,6 +160,14 @@ class LocalMesh:
         self._meas = np.ascontiguousarray(meas[part.cell_begin:part.cell_end])
         self._hmin = np.ascontiguousarray(hmin[part.cell_begin:part.cell_end])
         self._brick = _local_brick(mesh.brick(), self.n_cells)
+        mp = getattr(mesh, "mapping_points", None)
+        self._mapping = None
+        if callable(mp):
+            m, pts = mp()
+            self._mapping = (m, np.ascontiguousarray(pts[part.cell_begin:part.cell_end]))
+
+    def mapping_points(self):
+        return self._mapping
 
     @property
     def n_dofs(self):

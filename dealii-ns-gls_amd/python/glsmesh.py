@@ -566,6 +566,26 @@ class ShuffledMesh:
 
 
 # ------------------------------------------------------------ FE_Q_iso_Q1
+def _gll_nodes(k):
+    """Support points of FE_Q(k) / MappingQ(k) on [0, 1] (QGaussLobatto(k+1))."""
+    if k == 1:
+        return np.array([0.0, 1.0])
+    if k == 2:
+        return np.array([0.0, 0.5, 1.0])
+    if k == 3:
+        r = np.sqrt(5.0) / 10.0
+        return np.array([0.0, 0.5 - r, 0.5 + r, 1.0])
+    raise ValueError("degree > 3 not supported")
+
+
+def _lagrange(nodes, i, x):
+    v = np.ones_like(np.asarray(x, dtype=np.float64))
+    for j, xj in enumerate(nodes):
+        if j != i:
+            v = v * (x - xj) / (nodes[i] - xj)
+    return v
+
+
 class IsoQ1Mesh:
     """The multigrid's coarsest level with FE_Q_iso_Q1 (main.cc:436-446,
     "gmg coarse grid use fe q iso q1"): the same support points as FE_Q(k)
@@ -580,10 +600,10 @@ class IsoQ1Mesh:
     next level is the Q1 one: every sub-cell is one child of the next level,
     whose Q_k nodes sit at the sub-cell's 3^dim refined lattice points
     (child_lattice), and the linear embedding is the iso-Q1 prolongation.
-    Geometry: the sub-cells are mapped multilinearly through their corner
-    support points — exact for multilinear coarse cells (the sphere mesh);
-    on MappingQ_k-curved cells this differs from the parent mapping at the
-    iterated points."""
+    Geometry: the parent cell's MappingQ(k) at the iterated quadrature
+    points (mapping_points: per sub-cell the parent map at its Q_k lattice,
+    passed to the operator as glsOpDesc.mapping_points), as the reference
+    maps every level with MappingQ(mapping_degree) (main.cc:413-414)."""
 
     def __init__(self, mesh):
         k, dim = mesh.degree, mesh.dim
@@ -621,6 +641,40 @@ class IsoQ1Mesh:
 
     def brick(self):
         return (self.k, self.k, self.k if self.dim == 3 else 1)
+
+    def mapping_points(self):
+        """The level's MappingQ(k) (main.cc:413-414: one mapping of the
+        level's degree for every level, the FE_Q_iso_Q1 coarse level too)
+        restricted to each sub-cell: the parent's Q_k map evaluated at the
+        sub-cell's (k+1)^dim GLL lattice points.  A Q_k map restricted to a
+        sub-box is again a Q_k map of the sub-cell's own coordinates, so these
+        points reproduce the parent mapping at the iterated quadrature points
+        exactly (curved cells included).  Returns (k, [n_cells][(k+1)^dim][dim])."""
+        k, dim = self.k, self.dim
+        n = k + 1
+        g = _gll_nodes(k)                      # parent and sub-cell lattices
+        # E[c][j][i]: parent basis i at sub-cell c's lattice point j (1D)
+        E = np.zeros((k, n, n))
+        for c in range(k):
+            xi = g[c] + (g[c + 1] - g[c]) * g
+            for i in range(n):
+                E[c, :, i] = _lagrange(g, i, xi)
+        X = np.asarray(self.coords, dtype=np.float64)[
+            np.asarray(self.base.cell_nodes, dtype=np.int64)].reshape((-1,) + (n,) * dim + (dim,))
+        out = []
+        if dim == 3:
+            for a in range(k):
+                for b in range(k):
+                    for c in range(k):
+                        out.append(np.einsum("pz,qy,rx,nzyxd->npqrd", E[a], E[b], E[c], X)
+                                   .reshape(X.shape[0], -1, dim))
+        else:
+            for b in range(k):
+                for c in range(k):
+                    out.append(np.einsum("qy,rx,nyxd->nqrd", E[b], E[c], X)
+                               .reshape(X.shape[0], -1, dim))
+        pts = np.stack(out, axis=1).reshape(-1, n ** dim, dim)  # [coarse][sub] order
+        return k, np.ascontiguousarray(pts)
 
     def cell_measure(self):
         meas, hmin = self.base.cell_measure()

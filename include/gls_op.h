@@ -124,6 +124,15 @@ typedef struct
   const int64_t  *outflow_cells;   /* host [n_outflow_faces]                 */
   const int32_t  *outflow_face_no; /* host [n_outflow_faces] 0 .. 2*dim-1    */
   const int32_t  *outflow_kind;    /* host [n_outflow_faces] glsOutflow      */
+  /* optional cell mapping of its own degree (the level's
+   * MappingQ(mapping_degree), main.cc:413-414, which maps the FE_Q_iso_Q1
+   * coarse level too, where the element is Q1 on sub-cells, :437-446):
+   * per cell the (m+1)^dim support points of its MappingQ_m, lexicographic
+   * on the Gauss-Lobatto lattice.  NULL (zero-initialised descriptor): the
+   * element's own support points node_coords.  Cell integrals only (no
+   * outflow faces with it).                                                 */
+  int             mapping_degree;  /* m, 1..3                                */
+  const double   *mapping_points;  /* host [n_cells][(m+1)^dim][dim] or NULL */
 } glsOpDesc;
 
 enum glsOutflow

@@ -239,6 +239,46 @@ nfields(int dim)
 #define F_GP(dim) (2 + (dim) + (dim) * (dim))
 #define F_UT(dim) (2 + 2 * (dim) + (dim) * (dim))
 
+static void lagrange1d(const basis1d *b, int i, double x, double *v, double *d);
+
+/* reference-space gradient of the MappingQ_m map of cell c at the element's
+ * quadrature points (QGauss(k+1)^dim): g[d][a][q] = dx_d / dxi_a, from the
+ * cell's (m+1)^dim mapping support points (mapping_points) */
+static void
+mapping_gradients(const orc_op *op, int64_t c, double g[3][3][MAXNQ])
+{
+  const int dim = op->m.dim, n = op->b.n, nq = op->nq;
+  const int m = op->m.mapping_degree, nm = m + 1;
+  const int nmq = dim == 3 ? nm * nm * nm : nm * nm;
+  basis1d   bm;
+  make_basis(m, &bm);
+  double S[MAXN][MAXN], D[MAXN][MAXN]; /* [q][i]: mapping basis at the FE points */
+  for (int q = 0; q < n; ++q)
+    for (int i = 0; i < nm; ++i)
+      lagrange1d(&bm, i, op->b.qp[q], &S[q][i], &D[q][i]);
+  const double *X = op->m.mapping_points + (size_t)c * nmq * dim;
+  for (int d = 0; d < dim; ++d)
+    for (int a = 0; a < dim; ++a)
+      for (int q = 0; q < nq; ++q)
+        g[d][a][q] = 0;
+  for (int q = 0; q < nq; ++q)
+    {
+      const int qa[3] = {q % n, (q / n) % n, dim == 3 ? q / (n * n) : 0};
+      for (int i = 0; i < nmq; ++i)
+        {
+          const int ia[3] = {i % nm, (i / nm) % nm, dim == 3 ? i / (nm * nm) : 0};
+          for (int a = 0; a < dim; ++a)
+            {
+              double w = 1;
+              for (int e = 0; e < dim; ++e)
+                w *= e == a ? D[qa[e]][ia[e]] : S[qa[e]][ia[e]];
+              for (int d = 0; d < dim; ++d)
+                g[d][a][q] += X[i * dim + d] * w;
+            }
+        }
+    }
+}
+
 static void
 compute_geometry(orc_op *op)
 {
@@ -248,11 +288,16 @@ compute_geometry(orc_op *op)
   for (int64_t c = 0; c < op->m.n_cells; ++c)
     {
       double X[3][MAXNQ], val[MAXNQ], g[3][3][MAXNQ];
-      for (int d = 0; d < dim; ++d)
-        for (int i = 0; i < nloc; ++i)
-          X[d][i] = op->m.coords[(size_t)op->m.cell_nodes[c * nloc + i] * dim + d];
-      for (int d = 0; d < dim; ++d)
-        eval_scalar(dim, &op->b, X[d], val, &g[d][0][0]);
+      if (op->m.mapping_points)
+        mapping_gradients(op, c, g);
+      else
+        {
+          for (int d = 0; d < dim; ++d)
+            for (int i = 0; i < nloc; ++i)
+              X[d][i] = op->m.coords[(size_t)op->m.cell_nodes[c * nloc + i] * dim + d];
+          for (int d = 0; d < dim; ++d)
+            eval_scalar(dim, &op->b, X[d], val, &g[d][0][0]);
+        }
       for (int q = 0; q < nq; ++q)
         {
           double J[3][3] = {{0}}, inv[3][3] = {{0}}, det;
@@ -296,7 +341,8 @@ orc_op *
 orc_create(const orc_mesh *mesh, const orc_params *prm)
 {
   if (!mesh || !prm || mesh->degree < 1 || mesh->degree > MAXK ||
-      (mesh->dim != 2 && mesh->dim != 3))
+      (mesh->dim != 2 && mesh->dim != 3) ||
+      (mesh->mapping_points && (mesh->mapping_degree < 1 || mesh->mapping_degree > MAXK)))
     return NULL;
   orc_op *op = (orc_op *)calloc(1, sizeof(orc_op));
   op->m      = *mesh;
@@ -664,6 +710,8 @@ orc_set_outflow_faces(orc_op *op, int64_t n, const int64_t *cells, const int32_t
 {
   const int dim = op->m.dim, nq = op->nq, n1 = op->b.n, k = op->m.degree;
   const int nqf = dim == 3 ? n1 * n1 : n1;
+  if (op->m.mapping_points && n > 0)
+    return 1; /* face geometry from the element's support points only */
   for (int64_t f = 0; f < n; ++f)
     if (cells[f] < 0 || cells[f] >= op->m.n_cells || face_no[f] < 0 || face_no[f] >= 2 * dim ||
         (kind[f] != ORC_OUTFLOW_CUT && kind[f] != ORC_OUTFLOW_NITSCHE))

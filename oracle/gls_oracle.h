@@ -47,6 +47,13 @@ typedef struct
   const uint8_t  *cmask;        /* [n_nodes] constrained component bits      */
   const double   *cell_measure; /* [n_cells] vertex-based measure (|K|)     */
   const double   *cell_hmin;    /* [n_cells] minimum vertex distance        */
+  /* optional cell mapping of another degree (main.cc:413-414: the level's
+   * MappingQ(mapping_degree) on every level, also on the FE_Q_iso_Q1 coarse
+   * level where the element is Q1 on sub-cells): per cell the
+   * (m+1)^dim support points of its MappingQ_m, lexicographic on the GLL
+   * lattice.  NULL: the element's own support points (coords).           */
+  int             mapping_degree;
+  const double   *mapping_points; /* [n_cells][(m+1)^dim][dim] or NULL     */
 } orc_mesh;
 
 typedef struct

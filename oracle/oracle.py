@@ -19,7 +19,8 @@ _lib = None
 class _Mesh(C.Structure):
     _fields_ = [("dim", C.c_int), ("degree", C.c_int), ("n_cells", C.c_int64),
                 ("n_nodes", C.c_int64), ("cell_nodes", C.c_void_p), ("coords", C.c_void_p),
-                ("cmask", C.c_void_p), ("cell_measure", C.c_void_p), ("cell_hmin", C.c_void_p)]
+                ("cmask", C.c_void_p), ("cell_measure", C.c_void_p), ("cell_hmin", C.c_void_p),
+                ("mapping_degree", C.c_int), ("mapping_points", C.c_void_p)]
 
 
 class _Params(C.Structure):
@@ -87,8 +88,17 @@ class OracleMesh:
         meas, hmin = mesh.cell_measure()
         self.measure = np.ascontiguousarray(meas)
         self.hmin = np.ascontiguousarray(hmin)
+        # MappingQ_m of another degree (the FE_Q_iso_Q1 level's parent mapping)
+        mp = getattr(mesh, "mapping_points", None)
+        self.mapping = mp() if callable(mp) else None
+        mdeg, mptr = 0, None
+        if self.mapping is not None:
+            mdeg, pts = self.mapping
+            self.mapping_pts = np.ascontiguousarray(pts, dtype=np.float64)
+            mptr = _p(self.mapping_pts)
         self.s = _Mesh(self.dim, self.degree, self.n_cells, self.n_nodes, _p(self.cell_nodes),
-                       _p(self.coords), _p(self.cmask), _p(self.measure), _p(self.hmin))
+                       _p(self.coords), _p(self.cmask), _p(self.measure), _p(self.hmin),
+                       mdeg, mptr)
 
     @property
     def n_dofs(self):
