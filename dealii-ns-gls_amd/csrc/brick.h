@@ -61,13 +61,17 @@ struct BrickMax
   static constexpr int cells = dim == 3 ? 4 : 8; // cells per direction
 };
 
+#ifndef GLS_BRICK_MAXZ
+#define GLS_BRICK_MAXZ 1
+#endif
 template <int dim, int k>
 struct BrickLattice
 {
   // largest lattice the brick kernel takes: 3D bricks of up to 4x4x1 cells
-  // (build_bricks runs 3D bricks as one-cell layers), 2D up to 8x8 cells
+  // (build_bricks runs 3D bricks as one-cell layers; GLS_BRICK_MAXZ layers in
+  // variant builds), 2D up to 8x8 cells
   static constexpr int side = k * BrickMax<dim>::cells + 1;
-  static constexpr int L    = dim == 3 ? side * side * (k + 1) : side * side;
+  static constexpr int L    = dim == 3 ? side * side * (k * GLS_BRICK_MAXZ + 1) : side * side;
   static constexpr bool fits = L <= 729;
 };
 

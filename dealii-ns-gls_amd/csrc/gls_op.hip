@@ -147,6 +147,10 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
       int z = 1;
       while (bx * by * z * 2 <= 8 && bz % (z * 2) == 0)
         z *= 2;
+      // variant builds (GLS_BRICK_MAXZ > 1): GLS_BRICK_BZ layers per brick
+      if (const char *e = getenv("GLS_BRICK_BZ"))
+        while (z * 2 <= std::min(std::atoi(e), GLS_BRICK_MAXZ) && bz % (z * 2) == 0)
+          z *= 2;
       bz = z;
     }
   const int64_t cpb = (int64_t)bx * by * bz;
@@ -155,8 +159,8 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
   const int Lx = k * bx + 1, Ly = k * by + 1, Lz = dim == 3 ? k * bz + 1 : 1;
   const int L  = Lx * Ly * Lz;
   const int side_max = k * (dim == 3 ? 4 : 8) + 1;
-  const int lmax     = dim == 3 ? side_max * side_max * (k + 1) : side_max * side_max;
-  if (L > lmax || lmax > 729 || (dim == 3 && (bx > 4 || by > 4 || bx * by * bz > 16)) ||
+  const int lmax     = dim == 3 ? side_max * side_max * (k * GLS_BRICK_MAXZ + 1) : side_max * side_max;
+  if (L > lmax || lmax > 729 || (dim == 3 && (bx > 4 || by > 4 || bx * by * bz > 16 * GLS_BRICK_MAXZ)) ||
       (dim == 2 && (bx > 8 || by > 8)))
     return; // lattice does not fit the brick kernel's LDS: per-cell path
   const int64_t nb_full = d->n_cells / cpb;
@@ -742,7 +746,7 @@ struct Impl
         // padded LDS lattice: 3D Q2 bricks of 4x4 cells in x, y use strides
         // 11, 12 (ds_read_b128 conflict-free x sweep, exhaustive search)
         static const bool pad32 = !getenv("GLS_PAD32") || std::atoi(getenv("GLS_PAD32")) != 0;
-        const bool pad  = dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9 &&
+        const bool pad  = dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9 && op->L == 243 &&
                          (sizeof(T) == 8 || pad32);
         a.PLx           = pad ? 11 : op->Lx;
         a.PLy           = pad ? 12 : op->Ly;
