@@ -206,6 +206,8 @@ def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src,
     out.update(mg_companions(d, params, weights, n_ref))
     del scratch
     torch.cuda.empty_cache()
+    out.update(amg_companions())
+    torch.cuda.empty_cache()
     return out
 
 
@@ -349,6 +351,61 @@ def mg_companions(d, params, weights, n_ref, reps=20):
             f"r{n_ref}_gmres_iteration": {"ms": float(np.median(times)) * 1e3,
                                           "note": "V-cycle + FP64 vmult + CGS2 + host "
                                                   "Hessenberg step, wall clock"}}
+
+
+def amg_companions(reps=5):
+    """The AMG decks' coarse solver (multigrid.cc:372-433,
+    491-530): FE_Q_iso_Q1 coarse level, "gmg coarse grid iterate" (GMRES to
+    1e-4) preconditioned by the smoothed-aggregation AMG (gls_amg_*, the
+    substitute for Trilinos ML) against the same coarse GMRES preconditioned
+    by 10 relaxation sweeps: coarse GMRES iterations, wall ms per V-cycle,
+    AMG setup and hierarchy, on the sphere (r3, its configured size) and the
+    stationary Re20 deck (r2).  The Re20 deck's saddle-point coarse level
+    diverges under Jacobi sweeps: no relaxation line there."""
+    import torch
+    import glsamd
+    out = {}
+    for name, n_ref, relax in (("input_sphere_amg.json", 3, True),
+                               ("input_turek_2D_Re20_stat.json", 2, False)):
+        d = gm.read_deck(os.path.join(gm.DECK_DIR, name))
+        params, w = d.operator_parameters(2.5e-4)
+        meshes = [d.mesh(r) for r in range(n_ref + 1)]
+        vel, p, slip = d.boundary_descriptor()
+        cm = [m.constraint_mask(vel, p, slip) for m in meshes]
+        u = gi.linearization_point(meshes[-1].n_nodes, meshes[-1].dim, d.u_max)
+        hist = gi.history(u, params["order"])
+        b = torch.from_numpy(gi.src_vector(meshes[-1].n_dofs)).cuda()
+        x = torch.zeros_like(b)
+        line = {"finest_dofs": meshes[-1].n_dofs, "levels": n_ref + 1}
+        variants = [("amg", dict(coarse_amg=d.amg_parameters()))]
+        if relax:
+            variants.append(("relax10", dict(coarse_n_iterations=10)))
+        for key, kw in variants:
+            try:
+                mg, _ = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f32",
+                                         coarse_iso_q1=True, coarse_iterate=True,
+                                         coarse_reltol=1e-4, coarse_maxiter=2000, **kw)
+                mg.vcycle(x, b)
+                torch.cuda.synchronize()
+                t = []
+                for _ in range(reps):
+                    t0 = time.perf_counter()
+                    mg.vcycle(x, b)
+                    torch.cuda.synchronize()
+                    t.append((time.perf_counter() - t0) * 1e3)
+                it, conv = mg.coarse_statistics()
+                r = {"vcycle_ms": float(np.median(t)), "coarse_gmres_iterations": it,
+                     "converged": conv, "coarse_dofs": meshes[0].n_dofs}
+                if key == "amg":
+                    info, setup_ms = mg.coarse_amg()
+                    r.update(amg_setup_ms=setup_ms, amg_sizes=info["sizes"],
+                             amg_nnz=info["nnz"])
+                line[key] = r
+                del mg
+            except Exception as e:  # reported, never fatal
+                line[key] = {"error": str(e)}
+        out[f"{d.simulation}_{'2d' if d.dim == 2 else '3d'}_r{n_ref}_coarse_gmres"] = line
+    return out
 
 
 def dist_size_companion(d, params, weights, n_ref, dist, rank, world, reps=30):

@@ -466,8 +466,8 @@ gls_dist_mg_create(const glsDistMGDesc *d, const glsDist *levels, glsDistMG *out
   GLS_TRY
   if (!d || !levels || !out || d->mg.n_levels < 1)
     throw std::runtime_error("gls_dist_mg_create: invalid arguments");
-  if (d->mg.coarse_iterate)
-    throw std::runtime_error("gls_dist_mg_create: coarse_iterate is single-domain only");
+  if (d->mg.coarse_iterate || d->mg.coarse_amg)
+    throw std::runtime_error("gls_dist_mg_create: coarse_iterate / coarse_amg are single-domain only");
   const int nl = d->mg.n_levels;
   auto     *m  = new glsDistMG_();
   try

@@ -490,6 +490,12 @@ struct glsMG_
   double *cg_ws    = nullptr;
   void   *cg_lvl   = nullptr;
   int     cg_iters = 0, cg_conv = 0;
+  // "gmg coarse grid solver": "AMG" (desc.coarse_amg): the smoothed-
+  // aggregation AMG on the coarse level's system matrix (amg.hip), rebuilt by
+  // every gls_mg_setup (PreconditionerGMG::initialize, multigrid.cc:372-433)
+  glsAMG  amg      = nullptr;
+  double *amg_io   = nullptr; // [2 n0] FP64 in / out of a direct AMG coarse solve
+  double  amg_setup_ms = 0;
 
   size_t
   ts() const
@@ -1179,13 +1185,36 @@ coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
 
 void v_step(glsMG_ *mg, int l, hipStream_t s);
 
+void
+check_amg(glsStatus st)
+{
+  if (st != 0)
+    throw std::runtime_error(std::string("coarse AMG: ") + gls_last_error());
+}
+
 // the coarse "preconditioner" once: sol[0] from def[0] (multigrid.cc:465-489):
 // dense LU (< 0), identity (0) or relaxation sweeps (> 0)
 void
 coarse_apply(glsMG_ *mg, hipStream_t s)
 {
   const size_t bytes = (size_t)mg->ops[0]->n_dofs * mg->ts();
-  if (mg->desc.coarse_n_iterations < 0)
+  if (mg->desc.coarse_amg)
+    {
+      // one AMG V-cycle as the coarse solver (coarse_iterate = 0): in FP64
+      const int64_t n = mg->ops[0]->n_dofs;
+      if (mg->prec == GLS_F64)
+        check_amg(gls_amg_vmult(mg->amg, (double *)mg->sol[0], (const double *)mg->def[0], s));
+      else
+        {
+          hipLaunchKernelGGL((k_convert<float, double>), g1(n), dim3(256), 0, s, mg->amg_io,
+                             (const float *)mg->def[0], n);
+          check_amg(gls_amg_vmult(mg->amg, mg->amg_io + n, mg->amg_io, s));
+          hipLaunchKernelGGL((k_convert<double, float>), g1(n), dim3(256), 0, s,
+                             (float *)mg->sol[0], mg->amg_io + n, n);
+        }
+      HIP_THROW(hipGetLastError());
+    }
+  else if (mg->desc.coarse_n_iterations < 0)
     {
       if (mg->prec == GLS_F64)
         coarse_lu_solve_t<double>(mg, s);
@@ -1249,8 +1278,14 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
   auto cvt_out = [&](double *dst, const T *src) {
     hipLaunchKernelGGL((k_convert<T, double>), g1(n), dim3(256), 0, s, dst, src, n);
   };
-  // dst = P^{-1} src (through def[0] -> sol[0])
+  // dst = P^{-1} src (through def[0] -> sol[0]); AMG: its V-cycle on the
+  // FP64 vectors directly (the reference's Trilinos AMG on the FP64 matrix)
   auto prec = [&](double *dst, const double *src) {
+    if (mg->desc.coarse_amg)
+      {
+        check_amg(gls_amg_vmult(mg->amg, dst, src, s));
+        return;
+      }
     cvt_in((T *)mg->def[0], src);
     coarse_apply(mg, s);
     cvt_out(dst, (const T *)mg->sol[0]);
@@ -1594,6 +1629,8 @@ gls_mg_create(const glsMGDesc *desc, const glsOp *levels, const uint32_t *const 
       mg->partitioned = mg->partitioned || op->n_owned_nodes != op->n_nodes;
       mg->ops.push_back(op);
     }
+  if (desc->coarse_amg && mg->partitioned)
+    throw std::runtime_error("gls_mg_create: the AMG coarse solver is single-domain");
   if (nl_levels > 1 && (!child || mg->degree > 2))
     throw std::runtime_error("gls_mg_create: child lattices required (degree <= 2)");
   // 1D prolongation per coarse degree: parent GLL basis at the child
@@ -1720,6 +1757,10 @@ gls_mg_destroy(glsMG mg)
       (void)hipFree(p);
   if (mg->blas)
     rocblas_destroy_handle(mg->blas);
+  if (mg->amg)
+    gls_amg_destroy(mg->amg);
+  if (mg->amg_io)
+    (void)hipFree(mg->amg_io);
   if (mg->graph_exec)
     (void)hipGraphExecDestroy(mg->graph_exec);
   if (mg->graph)
@@ -1822,7 +1863,30 @@ gls_mg_setup(glsMG mg, void *stream)
         else
           mg->omega[l] = 1.0;
       }
-  if (mg->desc.coarse_n_iterations < 0)
+  if (mg->desc.coarse_amg)
+    {
+      // the coarse level's system matrix (FP64, constrained rows / columns
+      // identity) and the AMG hierarchy on it
+      HIP_THROW(hipStreamSynchronize(s));
+      const auto t0   = std::chrono::steady_clock::now();
+      glsOp      op0  = mg->ops[0];
+      int64_t    nnz  = 0;
+      if (gls_op_system_matrix(op0, &nnz, nullptr, nullptr, nullptr) != 0)
+        throw std::runtime_error(std::string("coarse AMG: ") + gls_last_error());
+      std::vector<int64_t> rp((size_t)op0->n_dofs + 1), ci((size_t)nnz);
+      std::vector<double>  va((size_t)nnz);
+      if (gls_op_system_matrix(op0, &nnz, rp.data(), ci.data(), va.data()) != 0)
+        throw std::runtime_error(std::string("coarse AMG: ") + gls_last_error());
+      if (mg->amg)
+        gls_amg_destroy(mg->amg), mg->amg = nullptr;
+      check_amg(gls_amg_create(op0->n_dofs, rp.data(), ci.data(), va.data(), &mg->desc.amg,
+                               &mg->amg));
+      if (!mg->amg_io)
+        HIP_THROW(hipMalloc((void **)&mg->amg_io, (size_t)2 * op0->n_dofs * 8));
+      mg->amg_setup_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+  else if (mg->desc.coarse_n_iterations < 0)
     {
       if (mg->prec == GLS_F64)
         coarse_lu_setup_t<double>(mg, s);
@@ -1966,6 +2030,18 @@ gls_mg_coarse_statistics(glsMG mg, int *n_iterations, int *converged)
     throw std::runtime_error("gls_mg_coarse_statistics: null argument");
   *n_iterations = mg->cg_iters;
   *converged    = mg->cg_conv;
+  GLS_CATCH
+}
+
+glsStatus
+gls_mg_coarse_amg(glsMG mg, glsAMG *amg, double *setup_ms)
+{
+  GLS_TRY
+  if (!mg || !amg)
+    throw std::runtime_error("gls_mg_coarse_amg: null argument");
+  *amg = mg->amg;
+  if (setup_ms)
+    *setup_ms = mg->amg_setup_ms;
   GLS_CATCH
 }
 

@@ -37,6 +37,8 @@ EXPORTS = [
     "gls_dist_get_max_u", "gls_op_compute_diagonal", "gls_op_invert_diagonal", "gls_mg_relax",
     "gls_dist_compress_add", "gls_op_brick_shape", "gls_op_cell_permutation",
     "gls_discover_bricks", "gls_mg_coarse_statistics", "gls_mg_coarse_setup_times",
+    "gls_amg_create", "gls_amg_destroy", "gls_amg_vmult", "gls_amg_info", "gls_mg_coarse_amg",
+    "gls_amg_level_matrix",
     "gls_dist_mg_create", "gls_dist_mg_destroy", "gls_dist_mg_set_linearization_point",
     "gls_dist_mg_setup", "gls_dist_mg_get_relaxation", "gls_dist_mg_vcycle",
     "gls_dist_gmres_solve", "gls_op_element_matrices",
@@ -66,12 +68,28 @@ class OpParams(C.Structure):
                 ("order", C.c_int), ("flags", C.c_int)]
 
 
+class AMGParams(C.Structure):
+    _fields_ = [("block_size", C.c_int), ("threshold", C.c_double),
+                ("smoother_sweeps", C.c_int), ("coarse_max_size", C.c_int),
+                ("elliptic", C.c_int), ("max_levels", C.c_int)]
+
+
+def amg_params(block_size=1, threshold=1e-4, smoother_sweeps=2, coarse_max_size=2000,
+               elliptic=True, max_levels=10):
+    """glsAMGParams; the defaults are TrilinosWrappers::PreconditionAMG::
+    AdditionalData()'s (one constant mode, threshold 1e-4, 2 smoother sweeps,
+    elliptic) with deal.II's "coarse: max size" 2000."""
+    return AMGParams(int(block_size), float(threshold), int(smoother_sweeps),
+                     int(coarse_max_size), int(bool(elliptic)), int(max_levels))
+
+
 class MGDesc(C.Structure):
     _fields_ = [("n_levels", C.c_int), ("smoothing_n_iterations", C.c_int),
                 ("smoothing_eig_n_iterations", C.c_int), ("smoothing_range", C.c_double),
                 ("coarse_n_iterations", C.c_int), ("outer_precision", C.c_int),
                 ("compute_evs_n_levels", C.c_int), ("coarse_iterate", C.c_int),
-                ("coarse_reltol", C.c_double), ("coarse_maxiter", C.c_int)]
+                ("coarse_reltol", C.c_double), ("coarse_maxiter", C.c_int),
+                ("coarse_amg", C.c_int), ("amg", AMGParams)]
 
 
 class DistDesc(C.Structure):
@@ -161,6 +179,14 @@ def lib():
         L.gls_op_set_outflow_target.argtypes = [vp, vp, vp]
         L.gls_mg_coarse_statistics.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.gls_mg_coarse_setup_times.argtypes = [vp, vp, C.POINTER(C.c_int)]
+        L.gls_amg_create.argtypes = [i64, vp, vp, vp, C.POINTER(AMGParams), C.POINTER(vp)]
+        L.gls_amg_destroy.argtypes = [vp]
+        L.gls_amg_destroy.restype = None
+        L.gls_amg_vmult.argtypes = [vp, vp, vp, vp]
+        L.gls_amg_info.argtypes = [vp, C.POINTER(C.c_int), vp, vp, vp]
+        L.gls_amg_level_matrix.argtypes = [vp, C.c_int, C.c_int, C.POINTER(i64), C.POINTER(i64),
+                                           vp, vp, vp]
+        L.gls_mg_coarse_amg.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_double)]
         L.gls_dist_mg_create.argtypes = [vp, vp, vp]
         L.gls_dist_mg_destroy.argtypes = [vp]
         L.gls_dist_mg_destroy.restype = None
@@ -639,6 +665,15 @@ class PartitionedMultigrid:
         except Exception:
             pass
 
+    def coarse_amg(self):
+        """(AMG info dict, setup ms) of the coarse AMG (coarse_amg given), or
+        None before setup."""
+        h, ms = C.c_void_p(), C.c_double()
+        _check(lib().gls_mg_coarse_amg(self.h, C.byref(h), C.byref(ms)))
+        if not h.value:
+            return None
+        return AMG._info_of(h), ms.value
+
     def relaxation(self, level):
         w, lam = C.c_double(), C.c_double()
         _check(lib().gls_dist_mg_get_relaxation(self.h, level, C.byref(w), C.byref(lam)))
@@ -691,6 +726,70 @@ def dist_gmres_solve(ops, mgs, xs, bs, n_max_iterations=10000, absolute_toleranc
     return out
 
 
+class AMG:
+    """TrilinosWrappers::PreconditionAMG over the C-ABI (gls_amg_*): built
+    from a scipy CSR matrix (initialize), vmult = one V-cycle on device FP64
+    vectors.  The substitute for Trilinos ML (csrc/amg.hip)."""
+
+    def __init__(self, matrix, **params):
+        import torch
+        if not torch.cuda.is_available():
+            raise GlsError("AMG needs a GPU (no CPU fallback by design)")
+        A = matrix.tocsr()
+        A.sort_indices()
+        rp = np.ascontiguousarray(A.indptr, dtype=np.int64)
+        ci = np.ascontiguousarray(A.indices, dtype=np.int64)
+        va = np.ascontiguousarray(A.data, dtype=np.float64)
+        self.prm = amg_params(**params)
+        h = C.c_void_p()
+        _check(lib().gls_amg_create(A.shape[0], rp.ctypes.data, ci.ctypes.data, va.ctypes.data,
+                                    C.byref(self.prm), C.byref(h)))
+        self.h = h
+        self.n = A.shape[0]
+
+    @staticmethod
+    def _info_of(h):
+        nl = C.c_int()
+        _check(lib().gls_amg_info(h, C.byref(nl), None, None, None))
+        sizes = np.zeros(nl.value, dtype=np.int64)
+        nnz = np.zeros(nl.value, dtype=np.int64)
+        lam = np.zeros(nl.value)
+        _check(lib().gls_amg_info(h, C.byref(nl), sizes.ctypes.data, nnz.ctypes.data,
+                                  lam.ctypes.data))
+        return {"levels": nl.value, "sizes": sizes.tolist(), "nnz": nnz.tolist(),
+                "lambda": lam.tolist()}
+
+    def info(self):
+        return self._info_of(self.h)
+
+    def level_matrix(self, level, which="A"):
+        """the device hierarchy's A / P / R of a level as scipy CSR"""
+        import scipy.sparse as sp
+        w = {"A": 0, "P": 1, "R": 2}[which]
+        n, nnz = C.c_int64(), C.c_int64()
+        _check(lib().gls_amg_level_matrix(self.h, level, w, C.byref(n), C.byref(nnz), None, None,
+                                          None))
+        rp = np.zeros(n.value + 1, dtype=np.int32)
+        ci = np.zeros(nnz.value, dtype=np.int32)
+        va = np.zeros(nnz.value)
+        _check(lib().gls_amg_level_matrix(self.h, level, w, C.byref(n), C.byref(nnz),
+                                          rp.ctypes.data, ci.ctypes.data, va.ctypes.data))
+        m = int(ci.max()) + 1 if nnz.value else 0
+        return sp.csr_matrix((va, ci, rp), shape=(n.value, max(m, 1)))
+
+    def vmult(self, dst, src):
+        _check(lib().gls_amg_vmult(self.h, _vptr(dst), _vptr(src), _stream()))
+        return dst
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().gls_amg_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
 class Multigrid:
     """PreconditionerGMG (multigrid.h:61-141) over the C-ABI: level operators
     (MGNumber = float by default), damped-Jacobi relaxation smoother with a
@@ -699,7 +798,7 @@ class Multigrid:
     def __init__(self, level_ops, child_lattices, smoothing_n_iterations=5,
                  smoothing_eig_n_iterations=20, smoothing_range=20.0, coarse_n_iterations=20,
                  outer_precision="f64", compute_evs_n_levels=0, coarse_iterate=False,
-                 coarse_reltol=1e-4, coarse_maxiter=10000):
+                 coarse_reltol=1e-4, coarse_maxiter=10000, coarse_amg=None):
         self.ops = list(level_ops)
         self._child = [None] + [np.ascontiguousarray(c, dtype=np.uint32)
                                 for c in child_lattices]
@@ -710,6 +809,12 @@ class Multigrid:
         self.desc = MGDesc(n, smoothing_n_iterations, smoothing_eig_n_iterations,
                            smoothing_range, coarse_n_iterations, outer, compute_evs_n_levels,
                            int(bool(coarse_iterate)), coarse_reltol, coarse_maxiter)
+        if coarse_amg is not None:
+            # "gmg coarse grid solver": "AMG": a dict of amg_params() keywords
+            # or an AMGParams
+            self.desc.coarse_amg = 1
+            self.desc.amg = (coarse_amg if isinstance(coarse_amg, AMGParams)
+                             else amg_params(**coarse_amg))
         self.outer_dtype = None
         h = C.c_void_p()
         _check(lib().gls_mg_create(C.byref(self.desc), C.cast(arr, C.c_void_p),
@@ -742,6 +847,15 @@ class Multigrid:
         _check(lib().gls_mg_coarse_setup_times(self.h, ms, C.byref(nc)))
         return {"assembly_ms": ms[0], "getrf_ms": ms[1], "getri_ms": ms[2],
                 "colors": nc.value}
+
+    def coarse_amg(self):
+        """(AMG info dict, setup ms) of the coarse AMG (coarse_amg given), or
+        None before setup."""
+        h, ms = C.c_void_p(), C.c_double()
+        _check(lib().gls_mg_coarse_amg(self.h, C.byref(h), C.byref(ms)))
+        if not h.value:
+            return None
+        return AMG._info_of(h), ms.value
 
     def relaxation(self, level):
         w, lam = C.c_double(), C.c_double()

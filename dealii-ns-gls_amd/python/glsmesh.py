@@ -358,6 +358,26 @@ class Deck:
         return v
 
     @property
+    def coarse_solver(self):
+        # "gmg coarse grid solver" (multigrid.cc:164-166; default "AMG",
+        # multigrid.h:35)
+        return self.raw.get("gmg coarse grid solver", "AMG")
+
+    def amg_parameters(self):
+        """glsAMGParams keywords of the deck's coarse AMG (multigrid.cc:
+        372-433): "gmg coarse grid amg use default parameters" true ->
+        PreconditionAMG::AdditionalData() (one constant mode, threshold 1e-4,
+        elliptic, Chebyshev smoother, Amesos-KLU coarse); false -> the
+        multigrid.h:44-53 values (constant modes per component, threshold
+        1e-14, non-elliptic, 2 sweeps; the ILU smoother / coarse solver are
+        substituted by Chebyshev / a dense direct solve)."""
+        if self.raw.get("gmg coarse grid amg use default parameters", True):
+            return dict(block_size=1, threshold=1e-4, smoother_sweeps=2, coarse_max_size=2000,
+                        elliptic=True, max_levels=10)
+        return dict(block_size=self.dim + 1, threshold=1e-14, smoother_sweeps=2,
+                    coarse_max_size=2000, elliptic=False, max_levels=10)
+
+    @property
     def use_fe_q_iso_q1(self):
         # "gmg coarse grid use fe q iso q1" (main.cc:136, 436-446)
         return bool(self.raw.get("gmg coarse grid use fe q iso q1", False))

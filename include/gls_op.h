@@ -70,6 +70,7 @@ extern "C" {
 
 typedef struct glsOp_ *glsOp;
 typedef struct glsMG_ *glsMG;
+typedef struct glsAMG_ *glsAMG;
 typedef int            glsStatus;
 
 enum glsPrecision
@@ -279,6 +280,42 @@ glsStatus gls_op_element_matrices(glsOp op, double *out);
 glsStatus gls_op_system_matrix(glsOp op, int64_t *nnz, int64_t *row_ptr, int64_t *cols,
                                double *vals);
 
+/* ------------------------------------------------- algebraic multigrid
+ * Smoothed-aggregation AMG on an assembled CSR matrix: the substitute for
+ * TrilinosWrappers::PreconditionAMG (Trilinos ML) of the coarse solver
+ * "AMG" (multigrid.cc:372-433).  Algorithm: csrc/amg.hip, DESIGN.md §7. */
+typedef struct
+{
+  int    block_size;      /* dofs per node ("PDE equations"): dim + 1 with
+                             constant modes per component (deal.II's
+                             extract_constant_modes, the decks' custom
+                             parameters), 1 with the default parameters   */
+  double threshold;       /* aggregation_threshold (1e-4 deal.II default)   */
+  int    smoother_sweeps; /* smoother_sweeps: Chebyshev degree (2)           */
+  int    coarse_max_size; /* "coarse: max size": dense direct solve below
+                             (2000, deal.II's ML parameter)                */
+  int    elliptic;        /* 1: smoothed prolongator (omega 4/3 / lambda);
+                             0: tentative prolongator (non-elliptic)       */
+  int    max_levels;      /* ML "max levels" (10)                            */
+} glsAMGParams;
+/* PreconditionAMG::initialize(matrix, data): n x n CSR (host, int64
+ * row_ptr[n + 1], cols / vals [nnz]); setup on the host, the hierarchy and
+ * the V-cycle on the current device */
+glsStatus gls_amg_create(int64_t n, const int64_t *row_ptr, const int64_t *cols,
+                         const double *vals, const glsAMGParams *prm, glsAMG *out);
+void      gls_amg_destroy(glsAMG amg);
+/* PreconditionAMG::vmult: dst = one V-cycle on src (device FP64 vectors) */
+glsStatus gls_amg_vmult(glsAMG amg, double *dst, const double *src, void *stream);
+/* levels, per level its size, nonzeros and the D^-1 A spectral-radius
+ * estimate (arrays of at least n_levels entries, or NULL) */
+glsStatus gls_amg_info(glsAMG amg, int *n_levels, int64_t *sizes, int64_t *nnz,
+                       double *lambda);
+/* the device hierarchy of level `level` as built (which: 0 A, 1 P, 2 R;
+ * none on the coarsest for P / R): rows, nonzeros, and with non-NULL
+ * arrays the CSR (int32 row_ptr [rows + 1], cols / vals [nnz]) */
+glsStatus gls_amg_level_matrix(glsAMG amg, int level, int which, int64_t *n_rows, int64_t *nnz,
+                               int32_t *row_ptr, int32_t *cols, double *vals);
+
 /* ------------------------------------------------------------ multigrid */
 typedef struct
 {
@@ -303,6 +340,14 @@ typedef struct
                                   solver above; 0 = apply it once            */
   double coarse_reltol;        /* 1e-4  multigrid.h:41 (ReductionControl)    */
   int    coarse_maxiter;       /* 10000 multigrid.h:39                       */
+  /* "gmg coarse grid solver": "AMG" (multigrid.cc:372-433): 1 = the coarse
+   * preconditioner is one V-cycle of a smoothed-aggregation AMG built by
+   * gls_mg_setup on the coarse level's assembled system matrix
+   * (gls_op_system_matrix, as op[min_level]->get_system_matrix()), applied
+   * to the FP64 coarse GMRES vectors (coarse_iterate = 1 needed);
+   * coarse_n_iterations is then ignored.  0 = as above.                     */
+  int    coarse_amg;
+  glsAMGParams amg;            /* its parameters (gls_amg_create)            */
 } glsMGDesc;
 
 /* levels[l] are level operators (same precision); child[l] for l >= 1 is the
@@ -319,6 +364,9 @@ glsStatus gls_mg_get_relaxation(glsMG mg, int level, double *omega,
 /* GMRES iterations of the last coarse solve (coarse_iterate = 1), and
  * whether it reached the tolerance */
 glsStatus gls_mg_coarse_statistics(glsMG mg, int *n_iterations, int *converged);
+/* the AMG of the coarse solver (desc.coarse_amg; NULL before gls_mg_setup)
+ * and the wall ms of its last setup (system matrix + hierarchy) */
+glsStatus gls_mg_coarse_amg(glsMG mg, glsAMG *amg, double *setup_ms);
 /* the last dense-coarse setup (coarse_n_iterations < 0): wall ms of the
  * free-block assembly (element matrices of the coarse level scattered per
  * cell colour), of getrf and of getri, and the number of cell colours */
