@@ -665,15 +665,6 @@ class PartitionedMultigrid:
         except Exception:
             pass
 
-    def coarse_amg(self):
-        """(AMG info dict, setup ms) of the coarse AMG (coarse_amg given), or
-        None before setup."""
-        h, ms = C.c_void_p(), C.c_double()
-        _check(lib().gls_mg_coarse_amg(self.h, C.byref(h), C.byref(ms)))
-        if not h.value:
-            return None
-        return AMG._info_of(h), ms.value
-
     def relaxation(self, level):
         w, lam = C.c_double(), C.c_double()
         _check(lib().gls_dist_mg_get_relaxation(self.h, level, C.byref(w), C.byref(lam)))

@@ -536,6 +536,8 @@ class DistributedMultigrid:
         cb = coarse_bounds(n0, world)
         self.fine_bounds = [b * (meshes[-1].n_cells // n0) for b in cb]
         self._fine = (meshes[-1], cmasks[-1], engine, native)
+        self._n_global_nodes = [m.n_nodes for m in meshes]
+        self._coarse_mesh = (meshes[0], cmasks[0], precision)
         self.levels = []
         for m, cm in zip(meshes, cmasks):
             if m.n_cells % n0:
@@ -577,6 +579,41 @@ class DistributedMultigrid:
         for D in self.levels:
             gd = torch.from_numpy(_dofs(D.r.part.local_nodes[:D.r.part.n_owned], D.r.nc))
             self._global_dof.append(gd.to(D.r.device))
+
+    def native(self, params, u_star, hist=None, weights=None):
+        """This rank's native partitioned multigrid over the same level
+        operators (glsamd.PartitionedMultigrid, gls_dist_mg_*: the V-cycle
+        with its halo exchanges, relaxation and coarse solve inside the
+        library, one team call per rank) with its linearization point and
+        setup done; the GMRES over it is glsamd.dist_gmres_solve([fine
+        operator's native handle], [mg], ...).  Needs the native level
+        operators (engine "gpu")."""
+        import glsamd
+        hs = [D.native for D in self.levels]
+        if any(h is None for h in hs):
+            raise ValueError("native(): the level operators have no native handles")
+        coarse, l2g = None, None
+        if self._coarse_direct:
+            m0, cm0, prec = self._coarse_mesh
+            coarse = glsamd.NavierStokesOperator(m0, cm0, prec)
+            coarse.set_parameters(**params)
+            l2g = self.levels[0].r.part.local_nodes
+        mg = glsamd.PartitionedMultigrid(
+            hs, self.child, [D.r.part.local_nodes[:D.r.part.n_owned] for D in self.levels],
+            self._n_global_nodes, smoothing_n_iterations=self.n_smooth,
+            smoothing_eig_n_iterations=self.n_eig, smoothing_range=self.range,
+            coarse_n_iterations=self.coarse_iters, compute_evs_n_levels=self.evs_levels,
+            coarse_global=coarse, coarse_l2g=l2g)
+        for D in self.levels:
+            D.r.eng.set_parameters(**params)
+        top = self.levels[-1].r
+        u = [top.local_from_global(u_star)]
+        h = None
+        if hist is not None and params.get("order", 0) > 0:
+            h = [[top.local_from_global(x) for x in hist]]
+        glsamd.PartitionedMultigrid.set_linearization_point([mg], u, h, weights)
+        glsamd.PartitionedMultigrid.setup([mg])
+        return mg
 
     def fine_operator(self, precision="f64"):
         """The outer (system) operator on the finest level's partition: its
