@@ -118,6 +118,24 @@ def _timed_vmults(op, dst, src, reps, flush=None):
     return float(np.median(t))
 
 
+def survey_bytes(op, td=True, cell_wise=False):
+    """SURVEY §8d's algorithmic bytes of one vmult, the roofline's numerator:
+    s 2N + s C nq n_tab + s [n_gen nq (dim^2+1) + n_cart (dim+1)] + 4 C nq,
+    n_tab = the reference's per-q table values of the Newton vmult
+    (operator_ns.h:120-132: delta_1, delta_2, U, grad U, grad P, and U_t with
+    the time derivative; 20 in 3D).  The brick kernel streams fewer (T1 and h
+    instead of grad P, U_t, delta_1/2: op.vmult_bytes()), so the bytes it
+    moves are below this figure."""
+    s = float(op.dtype.itemsize)
+    dim, nq = op.dim, (op.degree + 1) ** op.dim
+    n_tab = 2 + dim + dim * dim + dim + (dim if td else 0) - (2 if cell_wise else 0)
+    n_gen, n_cart = op.geometry_counts()
+    C = float(op.n_cells)
+    b = s * 2.0 * op.m() + s * C * nq * n_tab + s * (n_gen * nq * (dim * dim + 1) +
+                                                    n_cart * (dim + 1)) + 4.0 * C * nq
+    return b + (s * 2.0 * C if cell_wise else 0.0)
+
+
 def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src, reps=50):
     """The rest of SURVEY §8d's timing protocol, beside the headline line:
     cold (MALL flushed by a 1 GiB scratch write between reps) vs warm FP64
@@ -135,8 +153,9 @@ def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src,
         for _ in range(5):
             op.vmult(dst, src)
         ms = _timed_vmults(op, dst, src, reps, fl)
-        b = op.vmult_bytes()
+        b = survey_bytes(op)
         r = {"ms": ms, "dofs_per_s": op.m() / (ms * 1e-3), "algorithmic_bytes": b,
+             "streamed_bytes": op.vmult_bytes(),
              "roofline_frac": b / (ms * 1e-3) / HBM_PEAK, "dtype": prec}
         if fl is None:
             # the same vmults back to back between two events (how the
@@ -437,7 +456,7 @@ def dist_size_companion(d, params, weights, n_ref, dist, rank, world, reps=30):
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ms = float(t.item()) / reps * 1e3
-    b = torch.tensor([A.op.vmult_bytes()], dtype=torch.float64, device="cuda")
+    b = torch.tensor([survey_bytes(A.op)], dtype=torch.float64, device="cuda")
     dist.all_reduce(b)  # the ranks' local algorithmic bytes (ghost cells counted once each)
     return {f"r{n_ref + 1}_f64_dist": {
         "ms": ms, "dofs": m.n_dofs, "cells": m.n_cells, "dofs_per_s": m.n_dofs / (ms * 1e-3),
@@ -777,7 +796,7 @@ def main():
         g = dist_gmres_companion(d, params, weights, n_ref, dist, rank, world)
         dist_comp = dict(dist_comp or {}, **g)
         log(f"[bench] distributed GMRES iteration: {g}")
-    bytes_per_vmult = op.vmult_bytes()
+    bytes_per_vmult = survey_bytes(op)
     n_gen, n_cart = op.geometry_counts()
     # parity of the timed result: the headline dst (FP64) against the oracle
     # on the same inputs (and the FP32 level operator at N = 1); a result
@@ -862,7 +881,8 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
                          "kernel": "vmult = gls::k_brick<3,2,double,MODE_NEWTON> + "
                                    "gls::k_shared_reduce_cls (both inside the events)",
-                         "kernel_ms": kernel_ms, "algorithmic_bytes": bytes_per_vmult},
+                         "kernel_ms": kernel_ms, "algorithmic_bytes": bytes_per_vmult,
+                         "streamed_bytes": op.vmult_bytes()},
             "cpu_baseline": cpu,
             "parity": parity,
             "companions": comp if dist_comp is None else dict(comp or {}, **dist_comp),

@@ -288,11 +288,12 @@ struct BrickLDS
   static constexpr int CPW = 64 / nq > 0 ? 64 / nq : 1;
   static constexpr int WB  = BufLayout<dim, n, NP>::WB; // per-cell sweep buffer (packs)
   static constexpr int WPB = BLOCK / 64;
+  static constexpr int ORG = 64; // cell-origin table entries (cells per brick)
   static size_t
-  bytes(int L) // L: padded LDS lattice size
+  bytes(int L, bool pipe = false) // L: padded LDS lattice size; pipe: two src lattices
   {
-    return 16 * ((size_t)NP * L + (size_t)WPB * CPW * WB) + tab_offset(L) +
-           sizeof(T) * 4 * n * CoefRow<T, n>::RP;
+    return 16 * ((size_t)(pipe ? 2 : 1) * NP * L + (size_t)WPB * CPW * WB) + tab_offset(L) +
+           sizeof(T) * 4 * n * CoefRow<T, n>::RP + sizeof(int) * ORG;
   }
   __host__ __device__ static size_t
   tab_offset(int L) // accumulator bytes (FP64 for both precisions) rounded up to 16
@@ -311,25 +312,39 @@ struct BrickLDS
 #ifndef GLS_BABL
 #define GLS_BABL 0
 #endif
-// Experimental table formulations (measured round 2), off by
-// default so that the brick kernel streams the reference's per-q tables
-// (operator_ns.h:120-132, SURVEY §8d B_tab):
+// Table formulation of the brick kernel (the tables hold
+// the reference's per-q fields, operator_ns.h:120-132, plus T1 and h):
 //   GLS_NEWTON_T1: the Newton vmult streams T1 (Fields::T1, the
-//     linearization-point part of R1) instead of grad P* and Ut_old;
+//     linearization-point part of R1, formed once per linearization point
+//     and time weights by k_finalize_t1) instead of grad P* and Ut_old;
 //   GLS_DELTA_OTF: q-wise delta_1 / delta_2 recomputed from U and h at the
 //     q point (delta_qwise, the producer's expression) instead of streamed.
-// Together: 16 instead of 20 values per q; Re3900 r3 283 -> 272 us, r2
-// unchanged (the kernel is latency-bound, not bandwidth-bound, there).
+// Together: 16 instead of the reference's 20 values per q (round 2: r3
+// 283 -> 272 us), and the register budget that lets the Cartesian kernel
+// run 4 waves per SIMD (round 3).
 #ifndef GLS_NEWTON_T1
-#define GLS_NEWTON_T1 0
+#define GLS_NEWTON_T1 1
 #endif
 #ifndef GLS_DELTA_OTF
-#define GLS_DELTA_OTF 0
+#define GLS_DELTA_OTF 1
 #endif
+#ifndef GLS_LATE_PREFETCH
+#define GLS_LATE_PREFETCH 0
+#endif
+// q-wise delta_1 / delta_2 recomputed in the kernel: the Q2 Newton vmult
+// only (its sqrt / division temporaries push other instantiations over their
+// register budget)
+template <int k, int MODE>
+__host__ __device__ constexpr bool
+delta_otf()
+{
+  return GLS_DELTA_OTF && MODE == MODE_NEWTON && k == 2;
+}
+
 // the table fields a brick vmult / residual of MODE streams: Newton U, grad U,
-// T1 and h (or delta_1/2); fixed-point U and h (delta_1/2); residual also
+// T1 and h (or delta_1/2); fixed-point U and delta_1/2; residual also
 // Ut_old.  Groups of 16 bytes with none of these are not loaded.
-template <int dim, int MODE>
+template <int dim, int MODE, int k = 2>
 __host__ __device__ constexpr bool
 field_read(int f)
 {
@@ -342,13 +357,13 @@ field_read(int f)
   const bool gp   = f >= F::GP && f < F::GP + dim;
   const bool t1   = f >= F::T1 && f < F::T1 + dim;
   const bool newt = GLS_NEWTON_T1 ? (gu || t1) : (gu || gp || ut);
-  return (GLS_DELTA_OTF ? h : d12) || u || (MODE == MODE_NEWTON && newt) ||
+  return (delta_otf<k, MODE>() ? h : d12) || u || (MODE == MODE_NEWTON && newt) ||
          (MODE == MODE_RESIDUAL && ut);
 }
 
 // a 16-byte group whose only Newton fields are U_t (read when the time
 // derivative is considered): loaded only when the runtime flag td says so
-template <int dim, int MODE>
+template <int dim, int MODE, int k = 2>
 __host__ __device__ constexpr bool
 group_ut_only(int g, int W)
 {
@@ -357,7 +372,7 @@ group_ut_only(int g, int W)
   for (int w = 0; w < W; ++w)
     {
       const int f = g * W + w;
-      if (!field_read<dim, MODE>(f))
+      if (!field_read<dim, MODE, k>(f))
         continue;
       any = true;
       other = other || !(f >= F::UT && f < F::UT + dim);
@@ -374,7 +389,6 @@ struct LaneData
   T    JxW; // as loaded: JxW (curved) or det J (Cartesian); see jxw()
   T    U[dim], GU[dim][dim], T1[dim], UT[dim], oldg[NOLD];
   T    h, d1, d2; // h: q-wise delta from U on the fly (GLS_DELTA_OTF)
-  int  li;
   bool active;
 };
 
@@ -397,10 +411,6 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
   using F            = Fields<dim>;
   constexpr int NG   = (F::N + W - 1) / W;
   r.active           = in_wave && lcell < ncell;
-  const int cx       = r.active ? lcell % a.bx : 0;
-  const int cy       = r.active ? (lcell / a.bx) % a.by : 0;
-  const int cz       = r.active ? lcell / (a.bx * a.by) : 0;
-  r.li = (cx * k + pa[0]) + a.PLx * ((cy * k + pa[1]) + a.PLy * (cz * k + pa[2]));
   // inactive lanes (the 64 % nq left-over lanes, cells past the brick's
   // end) load the brick's first cell instead of zero-filling ~30 registers
   // per round: finite values, and JxW = 0 below keeps them out of the sums
@@ -475,9 +485,9 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
       bool any = false;
 #pragma unroll
       for (int w = 0; w < W; ++w)
-        any = any || field_read<dim, MODE>(g * W + w);
+        any = any || field_read<dim, MODE, k>(g * W + w);
       V v = {};
-      if (any && (!group_ut_only<dim, MODE>(g, W) || a.td))
+      if (any && (!group_ut_only<dim, MODE, k>(g, W) || a.td))
         v = tv[g * GS];
 #pragma unroll
       for (int w = 0; w < W; ++w)
@@ -569,30 +579,61 @@ finish_shared(const Args &a, uint32_t packed, T (&r)[nc])
 #ifndef GLS_BRICK_OCC32
 #define GLS_BRICK_OCC32 3
 #endif
+#ifndef GLS_BRICK_OCC_CART
+#define GLS_BRICK_OCC_CART 4
+#endif
+
+// Geometry of a launch's bricks (build_bricks orders the Cartesian and the
+// curved bricks of each segment into separate runs): GEO_CART bricks hold
+// one diagonal J^{-1} and det J per cell, GEO_GEN bricks J^{-1} and JxW per
+// q point, GEO_ANY reads the type per brick (brick_geo bit 0).
+enum
+{
+  GEO_ANY  = 0,
+  GEO_CART = 1,
+  GEO_GEN  = 2
+};
+// The Cartesian FP64 3D Q2 vmult kernel (Newton, fixed point) fits 128
+// VGPRs (4 waves/SIMD) with its tables issued at the start of each round (in
+// flight during the evaluate sweeps) and an unpadded lattice (4 workgroups
+// per CU in LDS); the per-q geometry of curved bricks keeps 3 waves/SIMD and
+// the earlier prefetch (issued behind the previous round's Dq^T sweeps), as
+// do the other instantiations.
+// (A GEO_ANY kernel whose curved bricks load J^{-1} at its two points of
+// use instead of with the tables still needs 162 VGPRs: measured round 3.)
+template <int dim, int k, typename T, int MODE, int GEO>
+struct BrickOcc
+{
+  static constexpr bool cart4 = GEO == GEO_CART && sizeof(T) == 8 && dim == 3 && k == 2 &&
+                                MODE != MODE_RESIDUAL;
+  static constexpr int  waves = cart4 ? GLS_BRICK_OCC_CART :
+                                sizeof(T) == 4 ? GLS_BRICK_OCC32 :
+                                                 GLS_BRICK_OCC;
+  static constexpr bool late  = GLS_LATE_PREFETCH || cart4;
+};
 // PIPE: persistent pipelined variant.  The grid is at most the resident
 // workgroup slots; workgroup g runs the work units brick_begin + g + j *
 // gridDim.x (gridDim.x a multiple of 8 keeps every unit of a workgroup on
 // its XCD's run of bricks, build_bricks).  While a brick's cells run, the
 // next brick's lattice node ids and write targets (issued with the brick's
-// first round), its src gather (issued in the brick's last round, behind the
-// Dq^T sweeps, when the q-point tables are dead) and its first round's
-// tables (the usual next-round prefetch) are in flight, so a brick switch
-// costs the write-out and one LDS staging pass instead of the dependent
-// id -> gather round trips of a workgroup's prologue.
+// first round), its src gather and its first round's tables (both issued in
+// the brick's last round, behind the Dq^T sweeps, when the q-point tables
+// are dead) are in flight, so a brick switch costs the write-out and one
+// barrier instead of the dependent id -> gather round trips of a
+// workgroup's prologue.  The gather is an LDS-DMA
+// (global_load_lds_dwordx4, one 16-byte pack per lane) straight into a
+// second, unpadded src lattice: lattice node i of the next brick lands at
+// pack i, lane-linear, and occupies no registers while in flight.
 #ifndef GLS_FUSED_BUILD
 #define GLS_FUSED_BUILD 0
 #endif
-#ifndef GLS_PIPE_LATE_GATHER
-#define GLS_PIPE_LATE_GATHER 0
-#endif
+// GLS_PIPE_TAB: the next brick's first-round tables are prefetched in the
+// last round (1) or issued at the brick switch (0)
 #ifndef GLS_PIPE_TAB
 #define GLS_PIPE_TAB 1
 #endif
-#ifndef GLS_PIPE_SYNC
-#define GLS_PIPE_SYNC 0
-#endif
-template <int dim, int k, typename T, int MODE, bool PIPE = false>
-__global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_BRICK_OCC)
+template <int dim, int k, typename T, int MODE, bool PIPE = false, int GEO = GEO_ANY>
+__global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves))
   k_brick(BrickArgs<T, dim, k + 1> a)
 {
   using LDS          = BrickLDS<dim, k, T>;
@@ -612,7 +653,9 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
   const int L      = a.L;  // lattice nodes (global order of brick_nodes)
   const int LP     = a.LP; // padded LDS lattice (bank-conflict-free x sweep)
   V        *s_src  = reinterpret_cast<V *>(smem);   // [NP][LP] brick src values
-  V        *s_work = s_src + NP * LP;                // [WPB*CPW][WB]
+  // PIPE: the next brick's lattice (LDS-DMA target; LP == L, unpadded)
+  V        *s_alt  = s_src + NP * LP;
+  V        *s_work = s_src + (PIPE ? 2 : 1) * NP * LP; // [WPB*CPW][WB]
   // the accumulator lattice is FP64 for both precisions: ds_add_f32 costs
   // ~10 us per FP32 vmult on gfx950 (ablation GLS_ABL_NOATOMIC: 38.1 -> 28.2
   // us), ds_add_f64 next to nothing (40.1 -> 39.7 us)
@@ -624,6 +667,10 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
   const T  *sST    = s_tab + TAB_ST * n * RP;
   const T  *sD     = s_tab + TAB_D * n * RP;
   const T  *sDT    = s_tab + TAB_DT * n * RP;
+  // lattice position of each brick cell's first node (cell-major order
+  // x, y, z): one LDS read per round instead of per-lane divisions by the
+  // runtime brick shape, which the compiler would hoist into registers
+  int      *s_org  = reinterpret_cast<int *>(s_tab + 4 * n * RP); // [ORG]
 
   // 32-bit brick indices and cell / chunk offsets (uniform values: fewer
   // SGPRs live across the persistent variant's brick loop)
@@ -643,6 +690,11 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       s_tab[TAB_D * n * RP + t]  = v ? a.sh.Dq[r][j] : T(0);
       s_tab[TAB_DT * n * RP + t] = v ? a.sh.Dq[j][r] : T(0);
     }
+  if (t < a.bx * a.by * a.bz && t < LDS::ORG)
+    {
+      const int cx = t % a.bx, cy = (t / a.bx) % a.by, cz = t / (a.bx * a.by);
+      s_org[t]     = cx * k + a.PLx * (cy * k + a.PLy * cz * k);
+    }
   const int  wave    = t >> 6, lane = t & 63;
   const int  slot    = lane / nq;
   const int  p       = lane - slot * nq;
@@ -655,6 +707,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
   const int  pa[3]   = {p % n, (p / n) % n, dim == 3 ? p / (n * n) : 0};
   const int  st[3]   = {1, BL::PY, BL::PZ};               // buffer strides
   const int  q       = pa[0] + BL::PY * pa[1] + BL::PZ * pa[2]; // own slot
+  const int  lpa     = pa[0] + a.PLx * (pa[1] + a.PLy * pa[2]);  // lattice offset in a cell
   const int  step    = CPW * WPB;
 
   // ---- prologue: every load that does not depend on another is issued
@@ -675,7 +728,8 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
 #ifndef GLS_FORCE_CART
 #define GLS_FORCE_CART 0
 #endif
-  bool     general = !GLS_FORCE_CART && (binfo & 1u) != 0;
+  constexpr bool LATE = BrickOcc<dim, k, T, MODE, GEO>::late;
+  bool     general = GEO == GEO_GEN || (GEO == GEO_ANY && !GLS_FORCE_CART && (binfo & 1u) != 0);
   int      ncell   = (int)(binfo >> 8);
   uint32_t cell0   = a.brick_cell0[brick];
   uint32_t chunk0  = a.brick_chunk0[brick];
@@ -738,8 +792,9 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       const int i = t + it * BLOCK;
       if (i >= L)
         break;
-      const int      iz = i / Lxy, iy = (i - iz * Lxy) / a.Lx;
-      const int      ip = (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
+      // PIPE runs the unpadded lattice (the LDS-DMA lands lane-linearly)
+      const int      iz = PIPE ? 0 : i / Lxy, iy = PIPE ? 0 : (i - iz * Lxy) / a.Lx;
+      const int      ip = PIPE ? i : (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
       const uint32_t cm = pk[it] >> 28;
 #pragma unroll
       for (int c = 0; c < nc; ++c)
@@ -757,9 +812,6 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
   __syncthreads();
   GLS_STAMP(brick, 1);
 
-#ifndef GLS_LATE_PREFETCH
-#define GLS_LATE_PREFETCH 0
-#endif
   // the lane's tensor quadrature weight (Cartesian bricks: JxW = det J w_q)
   T wq_lane = a.sh.w[pa[0]] * a.sh.w[pa[1]];
   if (dim == 3)
@@ -777,10 +829,9 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
   const bool    has_next = PIPE && next < brick_end;
   constexpr int NIP      = PIPE ? NI : 1;
   uint32_t      pk_n[NIP], tg_n[NIP];
-  T             u_n[NIP][nc];
   uint32_t      binfo_n  = 0;
   uint32_t      cell0_n = 0, chunk0_n = 0;
-  if (PIPE && has_next && !GLS_PIPE_SYNC)
+  if (PIPE && has_next)
     {
       // the next brick's ids and write targets: in flight during this
       // brick's rounds (the next brick's gather depends on them)
@@ -803,14 +854,16 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       // start of that round (in flight during its evaluate sweeps) instead
       // of before the previous round's integrate sweeps: fewer registers
       // live across the integrate sweeps
-      if (GLS_LATE_PREFETCH && base > 0)
+      if (LATE && base > 0)
         load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, base + wave * CPW + slot,
                                    in_wave, p, pa, cur);
 
+      // the lane's lattice node this round (inactive lanes: the first cell's)
+      const int li = (cur.active ? s_org[base + wave * CPW + slot] : 0) + lpa;
       // ---- evaluate: x sweep straight from the src lattice, then y (, z)
       if (!(GLS_BABL & 4))
       {
-        const int lb = cur.li - pa[0];
+        const int lb = li - pa[0];
         if (in_wave)
 #pragma unroll
           for (int kp = 0; kp < NP; ++kp)
@@ -848,7 +901,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
 #pragma unroll
           for (int kp = 0; kp < NP; ++kp)
             {
-              const V v = s_src[kp * LP + cur.li];
+              const V v = s_src[kp * LP + li];
 #pragma unroll
               for (int w = 0; w < W; ++w)
                 if (kp * W + w < nc)
@@ -919,7 +972,7 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
         }
       T vr[nc], gr[nc][dim];
       T d1 = cur.d1, d2 = cur.d2;
-      if (GLS_DELTA_OTF && !a.cw)
+      if (delta_otf<k, MODE>() && !a.cw)
         {
           T u2 = 0;
 #pragma unroll
@@ -1042,30 +1095,41 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       // live), in flight during the S^T sweeps and the next evaluate (this
       // round's lattice position is kept: the prefetch overwrites cur)
       GLS_STAMP(brick, base == 0 ? 3 : 5);
-      const int  li_now     = cur.li;
+      const int  li_now     = li;
       const bool active_now = cur.active;
-      if (PIPE && !GLS_PIPE_LATE_GATHER && !GLS_PIPE_SYNC && has_next && base + step >= ncell)
+      if (!LATE && base + step < ncell)
+        load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, base + step + wave * CPW + slot,
+                                   in_wave, p, pa, cur);
+      else if (!LATE && PIPE && GLS_PIPE_TAB && has_next)
+        load_lane<dim, k, T, MODE>(a, cell0_n, chunk0_n, (int)(binfo_n >> 8), (binfo_n & 1u) != 0,
+                                   wave * CPW + slot, in_wave, p, pa, cur);
+      if constexpr (PIPE && nc * sizeof(T) % 16 == 0)
+      if (has_next && base + step >= ncell)
         {
           // last round: the next brick's src gather (read_dof_values of its
-          // lattice), landing in registers; staged after the write-out
+          // lattice) by LDS-DMA into the other lattice, one 16-byte pack per
+          // lane and instruction; lattice positions outside the next brick's
+          // cells (UNUSED_NODE) read node 0 (never read back)
 #pragma unroll
           for (int it = 0; it < NIP; ++it)
             {
               const int i = tl + it * BLOCK;
-              if (i < L && (pk_n[it] & NODE_MASK) != UNUSED_NODE)
-                load_node<T, nc>(a.src, pk_n[it] & NODE_MASK, u_n[it]);
-              else
+              if (i < L)
+                {
+                  uint32_t node = pk_n[it] & NODE_MASK;
+                  if (node == UNUSED_NODE)
+                    node = 0;
+                  const V *g = reinterpret_cast<const V *>(a.src) + (size_t)node * NP;
 #pragma unroll
-                for (int c = 0; c < nc; ++c)
-                  u_n[it][c] = T(0);
+                  for (int kp = 0; kp < NP; ++kp)
+                    __builtin_amdgcn_global_load_lds(
+                      (const void *)(g + kp),
+                      (__attribute__((address_space(3))) void *)(s_alt + kp * LP + it * BLOCK +
+                                                                 wave * 64),
+                      16, 0, 0);
+                }
             }
         }
-      if (!GLS_LATE_PREFETCH && base + step < ncell)
-        load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, base + step + wave * CPW + slot,
-                                   in_wave, p, pa, cur);
-      else if (!GLS_LATE_PREFETCH && PIPE && GLS_PIPE_TAB && has_next)
-        load_lane<dim, k, T, MODE>(a, cell0_n, chunk0_n, (int)(binfo_n >> 8), (binfo_n & 1u) != 0,
-                                   wave * CPW + slot, in_wave, p, pa, cur);
       wave_sync();
       in  = A;
       out = B;
@@ -1100,19 +1164,12 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
           }
       wave_sync();
     }
-  if (PIPE && GLS_PIPE_LATE_GATHER && !GLS_PIPE_SYNC && has_next)
-#pragma unroll
-    for (int it = 0; it < NIP; ++it)
-      {
-        const int i = tl + it * BLOCK;
-        if (i < L && (pk_n[it] & NODE_MASK) != UNUSED_NODE)
-          load_node<T, nc>(a.src, pk_n[it] & NODE_MASK, u_n[it]);
-        else
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-            u_n[it][c] = T(0);
-      }
-  __syncthreads();
+  if constexpr (PIPE)
+    // a bare barrier: __syncthreads() would also wait for the next brick's
+    // LDS-DMA gather (a pending LDS write on the VM counter)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else
+    __syncthreads();
   GLS_STAMP(brick, 6);
 
   if (PIPE)
@@ -1129,8 +1186,9 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       const int i = tl + it * BLOCK;
       if (i >= L)
         break;
-      const int      iz = i / Lxy, iy = (i - iz * Lxy) / a.Lx;
-      const int      ip = (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
+      // PIPE runs the unpadded lattice (the LDS-DMA lands lane-linearly)
+      const int      iz = PIPE ? 0 : i / Lxy, iy = PIPE ? 0 : (i - iz * Lxy) / a.Lx;
+      const int      ip = PIPE ? i : (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
       const uint32_t tgt = tg[it];
       double         acc[nc];
 #pragma unroll
@@ -1262,39 +1320,12 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
   GLS_STAMP(brick, 7);
   if (!has_next)
     break;
-  // ---- switch to the next brick: its lattice staged from the registers
-  // the last round's gather filled (the accumulator was zeroed by the
-  // write-out), its ids / targets / scalars from this brick's prefetch
-  if (GLS_PIPE_SYNC)
-    {
-      // diagnostic: the next brick's ids and gather after the write-out
-      const uint32_t *bnn = a.brick_nodes + next * (int64_t)L;
-      const uint32_t *btn = a.brick_target + next * (int64_t)L;
-#pragma unroll
-      for (int it = 0; it < NIP; ++it)
-        {
-          const int i = tl + it * BLOCK;
-          pk_n[it]    = i < L ? bnn[i] : 0u;
-          tg_n[it]    = i < L ? btn[i] : 0u;
-        }
-      binfo_n  = a.brick_geo[next];
-      cell0_n  = a.brick_cell0[next];
-      chunk0_n = a.brick_chunk0[next];
-#pragma unroll
-      for (int it = 0; it < NIP; ++it)
-        {
-          const int i = tl + it * BLOCK;
-          if (i < L && (pk_n[it] & NODE_MASK) != UNUSED_NODE)
-            load_node<T, nc>(a.src, pk_n[it] & NODE_MASK, u_n[it]);
-          else
-#pragma unroll
-            for (int c = 0; c < nc; ++c)
-              u_n[it][c] = T(0);
-        }
-    }
+  // ---- switch to the next brick: its lattice has landed in s_alt (the
+  // accumulator was zeroed by the write-out), its ids / targets / scalars
+  // come from this brick's prefetch
   brick   = next;
   binfo   = binfo_n;
-  general = (binfo & 1u) != 0;
+  general = GEO == GEO_GEN || (GEO == GEO_ANY && !GLS_FORCE_CART && (binfo & 1u) != 0);
   ncell   = (int)(binfo >> 8);
   cell0   = cell0_n;
   chunk0  = chunk0_n;
@@ -1304,17 +1335,37 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
       pk[it] = pk_n[it];
       tg[it] = tg_n[it];
     }
-  if constexpr (PRE)
-    {
+  // the DMA (and the next round's tables issued before it) complete
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  {
+    V *tmp = s_src;
+    s_src  = s_alt;
+    s_alt  = tmp;
+  }
 #pragma unroll
-      for (int it = 0; it < NI; ++it)
+  for (int it = 0; it < NIP; ++it)
+    {
+      const int i = tl + it * BLOCK;
+      if (i >= L)
+        break;
+      const uint32_t cm = pk[it] >> 28;
+      if constexpr (PRE)
         {
-          const int  i    = tl + it * BLOCK;
-          const bool excl = i < L && tg[it] != UNUSED_NODE && !(tg[it] & SHARED_BIT);
+          // the fused relaxation's operands of the exclusive nodes: the raw
+          // src values from the landed lattice, b and d from memory
+          const bool excl = tg[it] != UNUSED_NODE && !(tg[it] & SHARED_BIT);
+#pragma unroll
+          for (int kp = 0; kp < NP; ++kp)
+            {
+              const V v = s_src[kp * LP + i];
+#pragma unroll
+              for (int w = 0; w < W; ++w)
+                if (kp * W + w < nc)
+                  xs[it][kp * W + w] = v[w];
+            }
 #pragma unroll
           for (int c = 0; c < nc; ++c)
             {
-              xs[it][c] = u_n[PIPE ? it : 0][c];
               xb[it][c] = T(0);
               xd[it][c] = T(1);
             }
@@ -1325,28 +1376,17 @@ __global__ void __launch_bounds__(BLOCK, sizeof(T) == 4 ? GLS_BRICK_OCC32 : GLS_
                 load_node<T, nc>(a.rd, tg[it], xd[it]);
             }
         }
+      // homogeneous constraints read as 0 (read_dof_values)
+      if (!R && cm)
+        {
+          T *sv = reinterpret_cast<T *>(s_src);
+#pragma unroll
+          for (int c = 0; c < nc; ++c)
+            if ((cm >> c) & 1)
+              sv[((c / W) * LP + i) * W + c % W] = T(0);
+        }
     }
-#pragma unroll
-  for (int it = 0; it < NIP; ++it)
-    {
-      const int i = tl + it * BLOCK;
-      if (i >= L)
-        break;
-      const int      iz = i / Lxy, iy = (i - iz * Lxy) / a.Lx;
-      const int      ip = (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
-      const uint32_t cm = pk[it] >> 28;
-      if (!R)
-#pragma unroll
-        for (int c = 0; c < nc; ++c)
-          if ((cm >> c) & 1)
-            u_n[it][c] = T(0);
-      V v[NP];
-      to_packs<V, T, nc, NP, W>(u_n[it], v);
-#pragma unroll
-      for (int kp = 0; kp < NP; ++kp)
-        s_src[kp * LP + ip] = v[kp];
-    }
-  if (PIPE && !GLS_PIPE_TAB)
+  if (LATE || !GLS_PIPE_TAB)
     load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, wave * CPW + slot, in_wave, p,
                                pa, cur);
   __syncthreads();

@@ -208,6 +208,7 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
   int64_t n_interior = 0;
   while (n_interior < nb_full - n_split && !ghosted[order[n_interior]])
     ++n_interior;
+
   // XCD-aware launch order: workgroup i of a launch is dispatched to XCD
   // i % 8, each XCD with its own L2.  Consecutive bricks of the mesh order
   // (the z layers of one refined coarse cell) share a lattice plane of src
@@ -663,6 +664,9 @@ struct Impl
 #ifndef GLS_BRICK_PIPE_DEFAULT
 #define GLS_BRICK_PIPE_DEFAULT 0
 #endif
+#ifndef GLS_PIPE_BUILD
+#define GLS_PIPE_BUILD 0
+#endif
   // resident workgroup slots of a kernel on the current device (occupancy x
   // CUs), queried once per (kernel, LDS bytes): the query costs several
   // microseconds of host time, which short coarse-level launches cannot hide
@@ -685,14 +689,16 @@ struct Impl
     return slots;
   }
 
-  // the brick kernel over n_units work units: one workgroup per unit, or
-  // (GLS_BRICK_PIPE=1, more units than resident slots) the persistent
+  // the brick kernel over n_units work units of one geometry type: one
+  // workgroup per unit, or (GLS_PIPE_BUILD diagnostic builds with
+  // GLS_BRICK_PIPE=1, more units than resident slots) the persistent
   // pipelined variant on the resident slots rounded down to a multiple of 8
   template <int M>
   static void
-  launch_brick(int64_t n_units, size_t lds, bool pipe, hipStream_t s,
+  launch_brick(int64_t n_units, size_t lds, bool pipe, int geo, hipStream_t s,
                const BrickArgs<T, dim, n> &a)
   {
+#if GLS_PIPE_BUILD
     if (pipe)
       {
         const int64_t slots = resident_slots(k_brick<dim, k, T, M, true>, lds) / 8 * 8;
@@ -703,8 +709,16 @@ struct Impl
             return;
           }
       }
-    hipLaunchKernelGGL((k_brick<dim, k, T, M, false>), dim3((unsigned)n_units), dim3(BLOCK), lds,
-                       s, a);
+#endif
+    if (geo == GEO_GEN)
+      hipLaunchKernelGGL((k_brick<dim, k, T, M, false, GEO_GEN>), dim3((unsigned)n_units),
+                         dim3(BLOCK), lds, s, a);
+    else if (geo == GEO_CART)
+      hipLaunchKernelGGL((k_brick<dim, k, T, M, false, GEO_CART>), dim3((unsigned)n_units),
+                         dim3(BLOCK), lds, s, a);
+    else
+      hipLaunchKernelGGL((k_brick<dim, k, T, M, false, GEO_ANY>), dim3((unsigned)n_units),
+                         dim3(BLOCK), lds, s, a);
   }
 
   // brick kernel over work units [b0, b1) (what & BRICK_RUN) and the
@@ -744,13 +758,28 @@ struct Impl
         a.Lx            = op->Lx;
         a.Ly            = op->Ly;
         // padded LDS lattice: 3D Q2 bricks of 4x4 cells in x, y use strides
-        // 11, 12 (ds_read_b128 conflict-free x sweep, exhaustive search)
+        // 11, 12 (ds_read_b128 conflict-free x sweep, exhaustive search);
+        // the FP64 Cartesian kernel takes the unpadded lattice (4 workgroups
+        // per CU in LDS), and so does the persistent variant (its LDS-DMA
+        // lands lane-linearly, two lattices in LDS)
         static const bool pad32 = !getenv("GLS_PAD32") || std::atoi(getenv("GLS_PAD32")) != 0;
-        const bool pad  = dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9 && op->L == 243 &&
-                         (sizeof(T) == 8 || pad32);
-        a.PLx           = pad ? 11 : op->Lx;
-        a.PLy           = pad ? 12 : op->Ly;
-        a.LP            = a.PLx * a.PLy * (op->L / (op->Lx * op->Ly));
+        static const bool pad64 = getenv("GLS_PAD64") && std::atoi(getenv("GLS_PAD64")) != 0;
+        static const int pipe_env = getenv("GLS_BRICK_PIPE") ?
+                                      std::atoi(getenv("GLS_BRICK_PIPE")) :
+                                      GLS_BRICK_PIPE_DEFAULT;
+        const bool pipe = GLS_PIPE_BUILD && pipe_env != 0 && (dim + 1) * sizeof(T) % 16 == 0 &&
+                          b1 - b0 > 0 && (what & BRICK_RUN);
+        auto set_lattice = [&](bool general) {
+          // (the 4-wave Cartesian FP64 kernels: BrickOcc<...>::cart4)
+          const bool cart4 = !general && sizeof(T) == 8 && mode != MODE_RESIDUAL && dim == 3 &&
+                             k == 2;
+          const bool pad   = !pipe && dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9 &&
+                           op->L == 243 && (sizeof(T) == 8 ? (!cart4 || pad64) : pad32);
+          a.PLx = pad ? 11 : op->Lx;
+          a.PLy = pad ? 12 : op->Ly;
+          a.LP  = a.PLx * a.PLy * (op->L / (op->Lx * op->Ly));
+        };
+        set_lattice(false);
         a.nu            = (T)op->prm.nu;
         a.w0            = (T)op->prm.w0;
         a.theta         = (T)op->prm.theta;
@@ -777,7 +806,6 @@ struct Impl
         a.rc            = rc0;
         if (fused)
           what = BRICK_RUN;
-        const size_t lds = BrickLDS<dim, k, T>::bytes(a.LP);
         if ((what & BRICK_RUN) && b1 > b0 && mode == MODE_NEWTON && GLS_NEWTON_T1)
           {
             // T1 (Fields::T1) from the current tables and time weights
@@ -796,16 +824,18 @@ struct Impl
           }
         if ((what & BRICK_RUN) && b1 > b0)
           {
-            const int pipe_env = getenv("GLS_BRICK_PIPE") ?
-                                          std::atoi(getenv("GLS_BRICK_PIPE")) :
-                                          GLS_BRICK_PIPE_DEFAULT;
-            const bool pipe = pipe_env != 0 && !fused;
+            const bool pl  = pipe && !fused;
+            const int  geo = op->n_curved_bricks == 0            ? GEO_CART :
+                             op->n_curved_bricks == op->n_bricks ? GEO_GEN :
+                                                                   GEO_ANY;
+            set_lattice(geo != GEO_CART);
+            const size_t lds = BrickLDS<dim, k, T>::bytes(a.LP, pl);
             if (mode == MODE_NEWTON)
-              launch_brick<MODE_NEWTON>(b1 - b0, lds, pipe, s, a);
+              launch_brick<MODE_NEWTON>(b1 - b0, lds, pl, geo, s, a);
             else if (mode == MODE_FIXED)
-              launch_brick<MODE_FIXED>(b1 - b0, lds, pipe, s, a);
+              launch_brick<MODE_FIXED>(b1 - b0, lds, pl, geo, s, a);
             else
-              launch_brick<MODE_RESIDUAL>(b1 - b0, lds, pipe, s, a);
+              launch_brick<MODE_RESIDUAL>(b1 - b0, lds, pl, geo, s, a);
             HIP_THROW(hipGetLastError());
           }
         if ((what & BRICK_REDUCE) && op->n_shared > 0)
@@ -1579,8 +1609,12 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
       for (int64_t c = 0; c < C; ++c)
         if (cell_geo[c] & GEO_GENERAL)
           bgeo[brick_of[c]] |= 1u;
+      op->n_curved_bricks = 0;
       for (int64_t b = 0; b < op->n_bricks; ++b)
-        bgeo[b] |= op->brick_ncell[b] << 8;
+        {
+          op->n_curved_bricks += bgeo[b] & 1u;
+          bgeo[b] |= op->brick_ncell[b] << 8;
+        }
       for (int64_t c = 0; c < C; ++c)
         {
           const uint32_t cg = cell_geo[c];
@@ -2463,8 +2497,13 @@ gls_op_vmult_bytes(glsOp op)
           for (int w = 0; w < W; ++w)
             {
               const int f = g * W + w;
-              any = any || (dim == 3 ? (nt ? field_read<3, MODE_NEWTON>(f) : field_read<3, MODE_FIXED>(f))
-                                     : (nt ? field_read<2, MODE_NEWTON>(f) : field_read<2, MODE_FIXED>(f)));
+              const bool q2 = op->degree == 2;
+              any = any || (dim == 3 ? (nt ? (q2 ? field_read<3, MODE_NEWTON, 2>(f)
+                                                 : field_read<3, MODE_NEWTON, 1>(f))
+                                            : field_read<3, MODE_FIXED>(f))
+                                     : (nt ? (q2 ? field_read<2, MODE_NEWTON, 2>(f)
+                                                 : field_read<2, MODE_NEWTON, 1>(f))
+                                            : field_read<2, MODE_FIXED>(f)));
             }
           const bool ut_only = nt && (dim == 3 ? group_ut_only<3, MODE_NEWTON>(g, W)
                                                : group_ut_only<2, MODE_NEWTON>(g, W));

@@ -132,6 +132,9 @@ struct glsOp_
   uint32_t *d_brick_geo    = nullptr; // per brick: curved (bit 0) | cells << 8
   uint32_t *d_brick_cell0  = nullptr; // per brick: first cell
   uint32_t *d_brick_chunk0 = nullptr; // per brick: first table chunk
+  // bricks with per-q geometry (any curved cell): none -> the launches run
+  // k_brick<GEO_CART>, all -> <GEO_GEN>, some -> <GEO_ANY>
+  int64_t   n_curved_bricks = 0;
 
   // per-q table layout (kernels.h tab_index): 16-byte field groups, one
   // chunk per wavefront round of the brick kernel
