@@ -25,6 +25,7 @@
 // in-process group on one device (tests: the same data movement as device
 // copies), as gls_dist_vmult / gls_dist_vmult_group.
 #include "../../include/gls_op.h"
+#include "cgs.h"
 #include "common.h"
 #include "op_internal.h"
 
@@ -846,7 +847,11 @@ gls_dist_mg_vcycle(glsDistMG const *team, int n, void *const *dst, const void *c
 // right-preconditioned GMRES(max_n_tmp_vectors - 2) with classical
 // Gram-Schmidt and one re-orthogonalisation; the basis in HBM, the dots over
 // the owned rows all-reduced (the Hessenberg column and |w|^2 cross to the
-// host together, once per iteration); x = 0 on entry.  A: the FP64
+// host together, once per iteration); x = 0 on entry.  As the single-domain
+// gls_gmres_solve: for up to 32 basis columns the orthogonalisation is the
+// fused CGS2 passes of cgs.h (all-reduces between them), v_{j+1} = w / |w|
+// is formed on the device, and Arnoldi step j + 1 is enqueued before the
+// host waits for step j's column (a converged solve runs one discarded step).  A: the FP64
 // partitioned operator on the finest level's partition (the multigrid's
 // local vectors); mg NULL = identity preconditioner.
 glsStatus
@@ -877,7 +882,7 @@ gls_dist_gmres_solve(glsDist const *A, glsDistMG const *mg, int n, const glsGMRE
   // rocBLAS handle (device pointer mode for the dot results)
   struct WS
   {
-    double *V, *w, *z, *h;
+    double *V, *w, *z, *h, *part;
     int64_t nloc, nown;
   };
   std::vector<WS> ws((size_t)n);
@@ -886,7 +891,7 @@ gls_dist_gmres_solve(glsDist const *A, glsDistMG const *mg, int n, const glsGMRE
   for (int r = 0; r < n; ++r)
     {
       const int64_t nloc = ops[r]->n_dofs;
-      const size_t  need = ((size_t)(m + 3) * nloc + 2 * (m + 2)) * sizeof(double);
+      const size_t  need = ((size_t)(m + 3) * nloc + 2 * (m + 2) + CGS_PART) * sizeof(double);
       double       *base = nullptr;
       if (mg)
         {
@@ -908,8 +913,13 @@ gls_dist_gmres_solve(glsDist const *A, glsDistMG const *mg, int n, const glsGMRE
           HIP_THROW(hipMalloc((void **)&base, need));
           tmp_alloc.push_back(base);
         }
-      ws[(size_t)r] = {base, base + (size_t)(m + 1) * nloc, base + (size_t)(m + 2) * nloc,
-                       base + (size_t)(m + 3) * nloc, nloc, ops[r]->n_owned_dofs};
+      ws[(size_t)r] = {base,
+                       base + (size_t)(m + 1) * nloc,
+                       base + (size_t)(m + 2) * nloc,
+                       base + (size_t)(m + 3) * nloc,
+                       base + (size_t)(m + 3) * nloc + 2 * (m + 2),
+                       nloc,
+                       ops[r]->n_owned_dofs};
     }
   rocblas_handle h = nullptr;
   check_blas(rocblas_create_handle(&h), "rocblas_create_handle");
@@ -984,7 +994,99 @@ gls_dist_gmres_solve(glsDist const *A, glsDistMG const *mg, int n, const glsGMRE
       HIP_THROW(hipMemsetAsync(x[r], 0, (size_t)ws[(size_t)r].nloc * 8, s));
       copy_vec(vcol(r, 0), b[r], (size_t)ws[(size_t)r].nloc * 8, s);
     }
-  std::vector<double> H((size_t)(m + 1) * m), g(m + 1), cs(m), sn(m), y(m), col(m + 2);
+  std::vector<double> H((size_t)(m + 1) * m), g(m + 1), cs(m), sn(m), y(m);
+  // the Hessenberg column h1 | h2 | |w|^2 of member 0 (all-reduced) to
+  // pinned host memory, double-buffered by step parity
+  const int64_t HC = 2 * (m + 1) + 1;
+  struct Pinned
+  {
+    double    *p = nullptr;
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ~Pinned()
+    {
+      if (p)
+        (void)hipHostFree(p);
+      for (hipEvent_t x : e)
+        if (x)
+          (void)hipEventDestroy(x);
+    }
+  } pin;
+  HIP_THROW(hipHostMalloc((void **)&pin.p, 2 * HC * sizeof(double)));
+  for (int i = 0; i < 2; ++i)
+    HIP_THROW(hipEventCreateWithFlags(&pin.e[i], hipEventDisableTiming));
+  static const bool force_rocblas = getenv("GLS_GMRES_ROCBLAS") && getenv("GLS_GMRES_ROCBLAS")[0] == '1';
+  auto grid = [](int64_t k) { return dim3((unsigned)((k + 255) / 256)); };
+  // Arnoldi step j, enqueued only
+  auto arnoldi = [&](int j) {
+    std::vector<double *> Vj;
+    for (int r = 0; r < n; ++r)
+      Vj.push_back(vcol(r, j));
+    apply_P(Zv, Vj);
+    apply_A(Wv, Zv);
+    const int J = j + 1;
+    if (J <= CGS_MAXJ && !force_rocblas)
+      {
+        // h1 = V^T w; w -= V h1, h2 = V^T w; w -= V h2, |w|^2 (owned-row
+        // dots, all-reduced between the passes)
+        for (int r = 0; r < n; ++r)
+          {
+            const WS &q = ws[(size_t)r];
+            hipLaunchKernelGGL(k_cgs_dots, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)q.V,
+                               J, (const double *)q.w, q.part, q.nown, q.nloc);
+            hipLaunchKernelGGL(k_cgs_finish, dim3(J), dim3(256), 0, s, (const double *)q.part, q.h,
+                               0);
+          }
+        allreduce(J, 0);
+        for (int pass = 1; pass <= 2; ++pass)
+          {
+            for (int r = 0; r < n; ++r)
+              {
+                const WS &q = ws[(size_t)r];
+                hipLaunchKernelGGL(k_cgs_update, dim3(CGS_BLOCKS), dim3(256), 0, s,
+                                   (const double *)q.V, J, (const double *)(q.h + (pass - 1) * (m + 1)),
+                                   q.w, q.part, q.nloc, q.nown, q.nloc, pass == 2 ? 1 : 0);
+                hipLaunchKernelGGL(k_cgs_finish, dim3(pass == 2 ? 1 : J), dim3(256), 0, s,
+                                   (const double *)q.part, q.h + pass * (m + 1), 0);
+              }
+            allreduce(pass == 2 ? 1 : J, pass * (m + 1));
+          }
+        HIP_THROW(hipGetLastError());
+      }
+    else
+      {
+        for (int pass = 0; pass < 2; ++pass)
+          {
+            for (int r = 0; r < n; ++r)
+              check_blas(rocblas_dgemv(h, rocblas_operation_transpose,
+                                       (rocblas_int)ws[(size_t)r].nown, J, d_c,
+                                       ws[(size_t)r].V, (rocblas_int)ws[(size_t)r].nloc,
+                                       ws[(size_t)r].w, 1, d_c + 2,
+                                       ws[(size_t)r].h + pass * (m + 1), 1),
+                         "rocblas_dgemv");
+            allreduce(J, pass * (m + 1));
+            for (int r = 0; r < n; ++r)
+              check_blas(rocblas_dgemv(h, rocblas_operation_none,
+                                       (rocblas_int)ws[(size_t)r].nloc, J, d_c + 1,
+                                       ws[(size_t)r].V, (rocblas_int)ws[(size_t)r].nloc,
+                                       ws[(size_t)r].h + pass * (m + 1), 1, d_c,
+                                       ws[(size_t)r].w, 1),
+                         "rocblas_dgemv");
+          }
+        for (int r = 0; r < n; ++r)
+          check_blas(rocblas_ddot(h, (rocblas_int)ws[(size_t)r].nown, ws[(size_t)r].w, 1,
+                                  ws[(size_t)r].w, 1, ws[(size_t)r].h + 2 * (m + 1)),
+                     "rocblas_ddot");
+        allreduce(1, 2 * (m + 1));
+      }
+    HIP_THROW(hipMemcpyAsync(pin.p + (j % 2) * HC, ws[0].h, HC * sizeof(double),
+                             hipMemcpyDeviceToHost, s));
+    HIP_THROW(hipEventRecord(pin.e[j % 2], s));
+    for (int r = 0; r < n; ++r)
+      hipLaunchKernelGGL(k_unit_col_sq, grid(ws[(size_t)r].nloc), dim3(256), 0, s,
+                         vcol(r, j + 1), (const double *)ws[(size_t)r].w,
+                         (const double *)(ws[(size_t)r].h + 2 * (m + 1)), ws[(size_t)r].nloc);
+    HIP_THROW(hipGetLastError());
+  };
   int    it = 0, n_rst = 0;
   double res = bnorm;
   while (res > tol && it < desc->max_iterations)
@@ -1001,58 +1103,20 @@ gls_dist_gmres_solve(glsDist const *A, glsDistMG const *mg, int n, const glsGMRE
       std::fill(g.begin(), g.end(), 0.0);
       g[0]   = res;
       int jd = 0;
+      if (m > 0)
+        arnoldi(0);
       for (int j = 0; j < m && it < desc->max_iterations; ++j)
         {
-          std::vector<double *> Vj;
-          for (int r = 0; r < n; ++r)
-            Vj.push_back(vcol(r, j));
-          apply_P(Zv, Vj);
-          apply_A(Wv, Zv);
-          // CGS2: h1 = V^T w (owned rows), w -= V h1; h2 likewise; |w|^2
-          for (int pass = 0; pass < 2; ++pass)
-            {
-              for (int r = 0; r < n; ++r)
-                check_blas(rocblas_dgemv(h, rocblas_operation_transpose,
-                                         (rocblas_int)ws[(size_t)r].nown, j + 1, d_c,
-                                         ws[(size_t)r].V, (rocblas_int)ws[(size_t)r].nloc,
-                                         ws[(size_t)r].w, 1, d_c + 2,
-                                         ws[(size_t)r].h + pass * (m + 1), 1),
-                           "rocblas_dgemv");
-              allreduce(j + 1, pass * (m + 1));
-              for (int r = 0; r < n; ++r)
-                check_blas(rocblas_dgemv(h, rocblas_operation_none,
-                                         (rocblas_int)ws[(size_t)r].nloc, j + 1, d_c + 1,
-                                         ws[(size_t)r].V, (rocblas_int)ws[(size_t)r].nloc,
-                                         ws[(size_t)r].h + pass * (m + 1), 1, d_c,
-                                         ws[(size_t)r].w, 1),
-                           "rocblas_dgemv");
-            }
-          for (int r = 0; r < n; ++r)
-            check_blas(rocblas_ddot(h, (rocblas_int)ws[(size_t)r].nown, ws[(size_t)r].w, 1,
-                                    ws[(size_t)r].w, 1, ws[(size_t)r].h + 2 * (m + 1)),
-                       "rocblas_ddot");
-          allreduce(1, 2 * (m + 1));
-          std::vector<double> hc((size_t)(2 * (m + 1) + 1));
-          HIP_THROW(hipMemcpyAsync(hc.data(), ws[0].h, hc.size() * 8, hipMemcpyDeviceToHost, s));
-          HIP_THROW(hipStreamSynchronize(s));
-          double      *Hj = &H[(size_t)j * (m + 1)];
+          // step j + 1 in flight while the host handles step j
+          if (j + 1 < m && it + 1 < desc->max_iterations)
+            arnoldi(j + 1);
+          HIP_THROW(hipEventSynchronize(pin.e[j % 2]));
+          const double *hc = pin.p + (j % 2) * HC;
+          double       *Hj = &H[(size_t)j * (m + 1)];
           for (int i = 0; i <= j; ++i)
             Hj[i] = hc[(size_t)i] + hc[(size_t)(m + 1 + i)];
           const double hn = std::sqrt(std::max(0.0, hc[(size_t)(2 * (m + 1))]));
           Hj[j + 1]       = hn;
-          if (hn > 0)
-            {
-              const double s2 = 1.0 / hn;
-              rocblas_set_pointer_mode(h, rocblas_pointer_mode_host);
-              for (int r = 0; r < n; ++r)
-                {
-                  copy_vec(vcol(r, j + 1), ws[(size_t)r].w, (size_t)ws[(size_t)r].nloc * 8, s);
-                  check_blas(rocblas_dscal(h, (rocblas_int)ws[(size_t)r].nloc, &s2,
-                                           vcol(r, j + 1), 1),
-                             "rocblas_dscal");
-                }
-              rocblas_set_pointer_mode(h, rocblas_pointer_mode_device);
-            }
           for (int i = 0; i < j; ++i)
             {
               const double tt = cs[(size_t)i] * Hj[i] + sn[(size_t)i] * Hj[i + 1];
@@ -1072,6 +1136,8 @@ gls_dist_gmres_solve(glsDist const *A, glsDistMG const *mg, int n, const glsGMRE
           if (res <= tol || hn == 0)
             break;
         }
+      // the discarded step (if any) has finished before its columns are reused
+      HIP_THROW(hipStreamSynchronize(s));
       for (int i = jd - 1; i >= 0; --i)
         {
           double tt = g[(size_t)i];

@@ -13,6 +13,7 @@
 // for a streaming device.  The basis GEMVs are plain library GEMVs (rocBLAS);
 // the operator apply and the V-cycle are this library's own kernels.
 #include "../../include/gls_op.h"
+#include "cgs.h"
 #include "common.h"
 #include "op_internal.h"
 
@@ -69,138 +70,6 @@ k_residual(double *__restrict__ r, const double *__restrict__ b, int64_t n)
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < n)
     r[i] = b[i] - r[i];
-}
-
-// v = w / |w| with the norm read on the device (|w| = 0, the lucky
-// breakdown: v = 0, never used); the same 1/hn multiply as a host dscal
-__global__ void
-k_unit_col(double *__restrict__ v, const double *__restrict__ w, const double *__restrict__ hn,
-           int64_t n)
-{
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const double  h = *hn;
-  if (i < n)
-    v[i] = h > 0 ? w[i] * (1.0 / h) : 0.0;
-}
-
-// Fused CGS2 for the restart lengths GMRES runs by default (j + 1 <= 32
-// basis columns): three streaming passes over the basis instead of four
-// rocBLAS GEMVs plus a norm, each thread holding its rows' basis entries in
-// registers between the update and the next dots.
-//   k_cgs_dots:   part = V^T w                         (pass 1)
-//   k_cgs_update: w -= V h; part = V^T w  (or |w|^2)   (passes 2, 3)
-// Per-block partials (fixed row ranges) are summed in a fixed order by
-// k_cgs_finish: the result does not depend on scheduling.
-constexpr int CGS_MAXJ   = 32;
-constexpr int CGS_BLOCKS = 512; // 1024 measured slower (update 24.1 -> 27.4 us)
-
-__device__ __forceinline__ void
-cgs_block_store(double (&acc)[CGS_MAXJ], int J, double *__restrict__ part)
-{
-  __shared__ double red[4][CGS_MAXJ];
-  const int         lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-  for (int c = 0; c < CGS_MAXJ; ++c)
-    if (c < J) // uniform: a skipped column costs a branch, not its shuffles
-      {
-        double v = acc[c];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1)
-          v += __shfl_down(v, off);
-        if (lane == 0)
-          red[wv][c] = v;
-      }
-  __syncthreads();
-  if (threadIdx.x < J)
-    {
-      const int c = threadIdx.x;
-      part[(size_t)blockIdx.x * CGS_MAXJ + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
-    }
-}
-
-__global__ void __launch_bounds__(256)
-  k_cgs_dots(const double *__restrict__ V, int J, const double *__restrict__ w,
-             double *__restrict__ part, int64_t n)
-{
-  double acc[CGS_MAXJ];
-#pragma unroll
-  for (int c = 0; c < CGS_MAXJ; ++c)
-    acc[c] = 0;
-  const int64_t per = (n + CGS_BLOCKS - 1) / CGS_BLOCKS;
-  const int64_t r0 = blockIdx.x * per, r1 = r0 + per < n ? r0 + per : n;
-  for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x)
-    {
-      // all of the row's basis loads issued before the first FMA
-      double v[CGS_MAXJ];
-#pragma unroll
-      for (int c = 0; c < CGS_MAXJ; ++c)
-        v[c] = c < J ? V[(size_t)c * n + i] : 0.0;
-      const double wi = w[i];
-#pragma unroll
-      for (int c = 0; c < CGS_MAXJ; ++c)
-        acc[c] += v[c] * wi;
-    }
-  cgs_block_store(acc, J, part);
-}
-
-// w -= V h (h on the device); then the dots of the updated w with the basis
-// (norm = 0) or its squared norm into partial 0 (norm = 1)
-__global__ void __launch_bounds__(256)
-  k_cgs_update(const double *__restrict__ V, int J, const double *__restrict__ h,
-               double *__restrict__ w, double *__restrict__ part, int64_t n, int norm)
-{
-  double acc[CGS_MAXJ], hc[CGS_MAXJ];
-#pragma unroll
-  for (int c = 0; c < CGS_MAXJ; ++c)
-    {
-      acc[c] = 0;
-      hc[c]  = c < J ? h[c] : 0.0;
-    }
-  const int64_t per = (n + CGS_BLOCKS - 1) / CGS_BLOCKS;
-  const int64_t r0 = blockIdx.x * per, r1 = r0 + per < n ? r0 + per : n;
-  for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x)
-    {
-      double v[CGS_MAXJ];
-#pragma unroll
-      for (int c = 0; c < CGS_MAXJ; ++c)
-        v[c] = c < J ? V[(size_t)c * n + i] : 0.0;
-      double wi = w[i], t = 0;
-#pragma unroll
-      for (int c = 0; c < CGS_MAXJ; ++c)
-        t += v[c] * hc[c];
-      wi -= t;
-      w[i] = wi;
-      if (norm)
-        acc[0] += wi * wi;
-      else
-#pragma unroll
-        for (int c = 0; c < CGS_MAXJ; ++c)
-          acc[c] += v[c] * wi;
-    }
-  cgs_block_store(acc, norm ? 1 : J, part);
-}
-
-// out[c] = sum over blocks of part[b][c] in a fixed order: one workgroup
-// per column c = blockIdx.x (two partials per thread, fixed shuffle tree);
-// sqrt_out: out[0] = sqrt(sum) (the norm)
-__global__ void __launch_bounds__(256)
-  k_cgs_finish(const double *__restrict__ part, double *__restrict__ out, int sqrt_out)
-{
-  static_assert(CGS_BLOCKS == 512, "two partials per thread");
-  __shared__ double red[4];
-  const int    c = blockIdx.x, t = threadIdx.x;
-  double       s = part[(size_t)t * CGS_MAXJ + c] + part[(size_t)(t + 256) * CGS_MAXJ + c];
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1)
-    s += __shfl_down(s, off);
-  if ((t & 63) == 0)
-    red[t >> 6] = s;
-  __syncthreads();
-  if (t == 0)
-    {
-      const double v = (red[0] + red[1]) + (red[2] + red[3]);
-      out[c]         = sqrt_out ? sqrt(v) : v;
-    }
 }
 
 dim3
@@ -347,15 +216,15 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
         // fused CGS2: dots, update + dots, update + norm (three basis passes)
         const int J = j + 1;
         hipLaunchKernelGGL(k_cgs_dots, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(), J,
-                           (const double *)w.d(), cpart.d(), n);
+                           (const double *)w.d(), cpart.d(), n, n);
         hipLaunchKernelGGL(k_cgs_finish, dim3(J), dim3(256), 0, s, (const double *)cpart.d(),
                            dh.d(), 0);
         hipLaunchKernelGGL(k_cgs_update, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(),
-                           J, (const double *)dh.d(), w.d(), cpart.d(), n, 0);
+                           J, (const double *)dh.d(), w.d(), cpart.d(), n, n, n, 0);
         hipLaunchKernelGGL(k_cgs_finish, dim3(J), dim3(256), 0, s, (const double *)cpart.d(),
                            dh.d() + (m + 1), 0);
         hipLaunchKernelGGL(k_cgs_update, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(),
-                           J, (const double *)(dh.d() + (m + 1)), w.d(), cpart.d(), n, 1);
+                           J, (const double *)(dh.d() + (m + 1)), w.d(), cpart.d(), n, n, n, 1);
         hipLaunchKernelGGL(k_cgs_finish, dim3(1), dim3(256), 0, s, (const double *)cpart.d(), hn, 1);
         HIP_THROW(hipGetLastError());
       }
