@@ -12,7 +12,10 @@
 //     index order: a node whose strong neighbours are all free seeds an
 //     aggregate with them; a remaining node joins the aggregate of its first
 //     aggregated strong neighbour; the rest seed aggregates with their free
-//     strong neighbours;
+//     strong neighbours.  A node with no off-diagonal entry at all (the
+//     identity rows / columns of constrained dofs: Dirichlet points) is left
+//     out of every aggregate, its prolongator row zero, as ML and MueLu treat
+//     Dirichlet rows, so the coarse levels carry only the coupled dofs;
 //   * tentative prolongator from the near-null space (constant modes) by a
 //     QR per aggregate and mode (per-mode disjoint supports: a scaling);
 //   * prolongator smoothing P = (I - omega / lambda D^-1 A) P_tent, omega =
@@ -208,10 +211,14 @@ aggregate(const HostCSR &A, int b, double theta, int32_t &n_agg)
         S[(size_t)I].push_back(e.first);
   std::vector<int32_t> agg((size_t)N, -1);
   n_agg = 0;
+  // Dirichlet points: no off-diagonal entry (never aggregated; -2)
+  for (int64_t I = 0; I < N; ++I)
+    if (g[(size_t)I].empty())
+      agg[(size_t)I] = -2;
   // pass 1: nodes whose strong neighbourhood is entirely free
   for (int64_t I = 0; I < N; ++I)
     {
-      if (agg[(size_t)I] >= 0)
+      if (agg[(size_t)I] != -1)
         continue;
       bool free_nb = true;
       for (int32_t J : S[(size_t)I])
@@ -240,7 +247,7 @@ aggregate(const HostCSR &A, int b, double theta, int32_t &n_agg)
   // pass 3: the rest seed aggregates with their free strong neighbours
   for (int64_t I = 0; I < N; ++I)
     {
-      if (agg[(size_t)I] >= 0)
+      if (agg[(size_t)I] != -1)
         continue;
       agg[(size_t)I] = n_agg;
       for (int32_t J : S[(size_t)I])
@@ -585,9 +592,12 @@ gls_amg_create(int64_t n, const int64_t *row_ptr, const int64_t *cols, const dou
               break; // no coarsening: this level is the coarsest
             }
           // tentative prolongator: P[i, agg(i) b + comp(i)] = beta_i / |beta_(agg, comp)|
+          // (rows of Dirichlet points empty)
           std::vector<double> nrm((size_t)nc, 0.0);
           for (int64_t i = 0; i < Al.n; ++i)
-            nrm[(size_t)(agg[(size_t)(i / b)] * (int64_t)b + i % b)] += beta[(size_t)i] * beta[(size_t)i];
+            if (agg[(size_t)(i / b)] >= 0)
+              nrm[(size_t)(agg[(size_t)(i / b)] * (int64_t)b + i % b)] +=
+                beta[(size_t)i] * beta[(size_t)i];
           for (auto &v : nrm)
             v = std::sqrt(v);
           HostCSR Pt;
@@ -595,12 +605,14 @@ gls_amg_create(int64_t n, const int64_t *row_ptr, const int64_t *cols, const dou
           Pt.rp.resize((size_t)Al.n + 1);
           for (int64_t i = 0; i < Al.n; ++i)
             {
+              Pt.rp[(size_t)i] = (int64_t)Pt.ci.size();
+              if (agg[(size_t)(i / b)] < 0)
+                continue;
               const int64_t c = agg[(size_t)(i / b)] * (int64_t)b + i % b;
-              Pt.rp[(size_t)i] = i;
               Pt.ci.push_back((int32_t)c);
               Pt.v.push_back(nrm[(size_t)c] > 0 ? beta[(size_t)i] / nrm[(size_t)c] : 0.0);
             }
-          Pt.rp[(size_t)Al.n] = Al.n;
+          Pt.rp[(size_t)Al.n] = (int64_t)Pt.ci.size();
           // P = P_t - omega / lambda D^-1 A P_t (omega 4/3; elliptic = 0: P_t)
           HostCSR P = Pt;
           if (prm->elliptic && L.lambda > 0)
@@ -612,27 +624,29 @@ gls_amg_create(int64_t n, const int64_t *row_ptr, const int64_t *cols, const dou
               S.rp.assign((size_t)Al.n + 1, 0);
               for (int64_t i = 0; i < Al.n; ++i)
                 {
-                  // merge row i of P_t (one entry) with -w dinv_i (A P_t)_i
-                  const int32_t ct = Pt.ci[(size_t)i];
-                  bool          put = false;
+                  // merge row i of P_t (one entry, or none) with -w dinv_i (A P_t)_i
+                  const bool    has = Pt.rp[(size_t)i + 1] > Pt.rp[(size_t)i];
+                  const int32_t ct  = has ? Pt.ci[(size_t)Pt.rp[(size_t)i]] : -1;
+                  const double  pv  = has ? Pt.v[(size_t)Pt.rp[(size_t)i]] : 0.0;
+                  bool          put = !has;
                   for (int64_t k = AP.rp[(size_t)i]; k < AP.rp[(size_t)i + 1]; ++k)
                     {
                       const int32_t c = AP.ci[(size_t)k];
                       if (!put && ct < c)
                         {
-                          S.ci.push_back(ct), S.v.push_back(Pt.v[(size_t)i]);
+                          S.ci.push_back(ct), S.v.push_back(pv);
                           put = true;
                         }
                       double v = -w * dinv[(size_t)i] * AP.v[(size_t)k];
                       if (c == ct)
                         {
-                          v += Pt.v[(size_t)i];
+                          v += pv;
                           put = true;
                         }
                       S.ci.push_back(c), S.v.push_back(v);
                     }
                   if (!put)
-                    S.ci.push_back(ct), S.v.push_back(Pt.v[(size_t)i]);
+                    S.ci.push_back(ct), S.v.push_back(pv);
                   S.rp[(size_t)i + 1] = (int64_t)S.ci.size();
                 }
               P = std::move(S);

@@ -44,9 +44,14 @@ def aggregate(A, b, theta):
         keep = (cols != I) & (vals > 0) & (vals >= theta * np.sqrt(self_[I] * self_[cols]))
         S.append(cols[keep])
     agg = np.full(N, -1, dtype=np.int64)
+    # Dirichlet points (no off-diagonal entry): never aggregated (-2)
+    for I in range(N):
+        cols = B.indices[B.indptr[I]:B.indptr[I + 1]]
+        if not np.any(cols != I):
+            agg[I] = -2
     n_agg = 0
     for I in range(N):
-        if agg[I] >= 0:
+        if agg[I] != -1:
             continue
         if np.any(agg[S[I]] >= 0):
             continue
@@ -61,7 +66,7 @@ def aggregate(A, b, theta):
                     agg[I] = agg1[J]
                     break
     for I in range(N):
-        if agg[I] >= 0:
+        if agg[I] != -1:
             continue
         agg[I] = n_agg
         for J in S[I]:
@@ -93,9 +98,10 @@ class AMGRef:
                     self.levels.append(L)
                     break
                 i = np.arange(A.shape[0])
+                i = i[agg[i // b] >= 0]  # Dirichlet points: empty prolongator rows
                 col = agg[i // b] * b + i % b
-                nrm = np.sqrt(np.bincount(col, weights=beta ** 2, minlength=nc))
-                Pt = sp.csr_matrix((np.where(nrm[col] > 0, beta / np.where(nrm[col] > 0, nrm[col], 1), 0),
+                nrm = np.sqrt(np.bincount(col, weights=beta[i] ** 2, minlength=nc))
+                Pt = sp.csr_matrix((np.where(nrm[col] > 0, beta[i] / np.where(nrm[col] > 0, nrm[col], 1), 0),
                                     (i, col)), shape=(A.shape[0], nc))
                 P = Pt
                 if elliptic and lam > 0:

@@ -42,6 +42,38 @@ def test_ref_poisson_converges():
     assert res[-1] < 1e-3 and res[-1] / res[-2] < 0.5
 
 
+def _with_dirichlet(A, every=7):
+    """A with every `every`-th dof constrained the way the level operators
+    constrain dofs: identity row and column."""
+    A = sp.lil_matrix(A)
+    idx = np.arange(0, A.shape[0], every)
+    for i in idx:
+        A.rows[i], A.data[i] = [int(i)], [1.0]
+    A = A.tocsc()
+    keep = np.ones(A.shape[0], dtype=bool)
+    keep[idx] = False
+    D = sp.diags(keep.astype(float))
+    A = (A @ D).tolil()
+    for i in idx:
+        A[i, i] = 1.0
+    return A.tocsr(), idx
+
+
+def test_ref_dirichlet_points_not_aggregated():
+    """Identity rows / columns (constrained dofs) join no aggregate: the
+    coarse levels hold the coupled dofs only, and the cycle still converges
+    on the free dofs (Dirichlet rows are solved exactly by the smoother)."""
+    A0 = _poisson(40)
+    A, idx = _with_dirichlet(A0)
+    M = AMGRef(A, block_size=1, threshold=0.0, coarse_max_size=100)
+    Mfree = AMGRef(A0, block_size=1, threshold=0.0, coarse_max_size=100)
+    P = M.levels[0]["P"]
+    assert np.all(np.diff(P.indptr)[idx] == 0)  # empty prolongator rows
+    assert M.info()["sizes"][1] <= Mfree.info()["sizes"][1]
+    res = _stationary_iteration(A, M, gi.rnd(4, A.shape[0]), 10)
+    assert res[-1] < 1e-3
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("params", [dict(block_size=1, threshold=0.0, coarse_max_size=300),
                                     dict(block_size=1, threshold=0.0, coarse_max_size=300,
