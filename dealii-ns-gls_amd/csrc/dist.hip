@@ -642,6 +642,12 @@ dist_op(glsDist d)
   return d->op;
 }
 
+bool
+dist_has_peers(glsDist d)
+{
+  return !d->peers.empty();
+}
+
 int
 dist_rank(glsDist d)
 {

@@ -294,6 +294,18 @@ team_scale(Team &t, int l, const std::vector<void *> &x, double a, hipStream_t s
   HIP_THROW(hipGetLastError());
 }
 
+// true when a partitioned apply on level l exchanges halos (some member has
+// peers); false at world 1, where the fused single-domain kernels apply
+bool
+exchanges(Team &t, int l)
+{
+  for (auto *x : t.m)
+    if (gls::dist_has_peers(x->lv[(size_t)l]) || !gls::dist_op(x->lv[(size_t)l])->use_brick ||
+        gls::dist_op(x->lv[(size_t)l])->faces.n > 0)
+      return true;
+  return false;
+}
+
 // PreconditionRelaxation::vmult (zero start) / step, `iters` damped-Jacobi
 // iterations x <- x + omega D^-1 (b - A x) on level l (multigrid.cc:347-351)
 void
@@ -306,8 +318,27 @@ smooth(Team &t, int l, bool zero, int iters, hipStream_t s)
         check(gls_mg_relax(x->tr, l, x->X[l], x->B[l], nullptr, x->invd[l], x->omega[l], 1, s));
       it = 1;
     }
+  const bool alone = !exchanges(t, l);
   for (; it < iters; ++it)
     {
+      if (alone)
+        {
+          // no exchange: the single-domain smoother, the damped-Jacobi step
+          // fused into the brick write-out and the shared-node reduce, into
+          // T; then X and T swap roles
+          for (auto *x : t.m)
+            {
+              glsOp_        *op = gls::dist_op(x->lv[(size_t)l]);
+              gls::RelaxStep rx;
+              rx.b     = x->B[l];
+              rx.d     = x->invd[l];
+              rx.omega = x->omega[l];
+              gls::brick_launch(op, gls::op_vmult_mode(op), x->T[l], x->X[l], 0, op->n_bricks,
+                                gls::BRICK_RUN | gls::BRICK_REDUCE, s, &rx);
+              std::swap(x->X[l], x->T[l]);
+            }
+          continue;
+        }
       auto X = per(t, [&](glsDistMG_ *x) { return x->X[l]; });
       auto T = per(t, [&](glsDistMG_ *x) { return x->T[l]; });
       gls::team_vmult(t.level(l), T.data(), X.data(), t.n(), s);
@@ -388,15 +419,32 @@ v_step(Team &t, int l, hipStream_t s)
     }
   const int ns = t.m[0]->desc.smoothing_n_iterations;
   smooth(t, l, true, ns, s);
-  {
-    auto X = per(t, [&](glsDistMG_ *x) { return x->X[l]; });
-    auto T = per(t, [&](glsDistMG_ *x) { return x->T[l]; });
-    gls::team_vmult(t.level(l), T.data(), X.data(), t.n(), s);
-  }
+  const bool alone = !exchanges(t, l);
+  if (alone)
+    // no exchange: the residual b - A x fused into the brick write-out and
+    // the shared-node reduce (RelaxStep with d = 1, omega = 1, keep = false)
+    for (auto *x : t.m)
+      {
+        glsOp_        *op = gls::dist_op(x->lv[(size_t)l]);
+        gls::RelaxStep rx;
+        rx.b     = x->B[l];
+        rx.omega = 1.0;
+        rx.keep  = false;
+        gls::brick_launch(op, gls::op_vmult_mode(op), x->T[l], x->X[l], 0, op->n_bricks,
+                          gls::BRICK_RUN | gls::BRICK_REDUCE, s, &rx);
+      }
+  else
+    {
+      auto X = per(t, [&](glsDistMG_ *x) { return x->X[l]; });
+      auto T = per(t, [&](glsDistMG_ *x) { return x->T[l]; });
+      gls::team_vmult(t.level(l), T.data(), X.data(), t.n(), s);
+    }
   for (auto *x : t.m)
     {
       const int64_t n = x->n_dofs[(size_t)l];
-      if (x->prec == GLS_F64)
+      if (alone)
+        ; // T already holds b - A x
+      else if (x->prec == GLS_F64)
         hipLaunchKernelGGL(k_rsub<double>, g1(n), dim3(256), 0, s, (double *)x->T[l],
                            (const double *)x->B[l], n);
       else

@@ -212,6 +212,9 @@ fused_relax_ok(const glsOp_ *op)
 // one process drives in lockstep — one RCCL rank, or all members of an
 // in-process group (rank order)
 glsOp_ *dist_op(glsDist d);
+// false: the partition exchanges nothing (world 1): its vmult is the
+// single-domain one and the fused relaxation / residual apply
+bool    dist_has_peers(glsDist d);
 int     dist_rank(glsDist d);
 int     dist_world(glsDist d);
 void    team_vmult(glsDist const *m, void *const *dst, void *const *src, int n, hipStream_t s);
