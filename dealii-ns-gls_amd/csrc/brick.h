@@ -1404,7 +1404,7 @@ __global__ void __launch_bounds__(256)
                   const T *__restrict__ partial, const uint32_t *__restrict__ nodes,
                   const uint32_t *__restrict__ offsets, int64_t n_shared,
                   const T *__restrict__ rb = nullptr, const T *__restrict__ rd = nullptr,
-                  T romega = T(0), int keep = 1)
+                  T romega = T(0), int keep = 1, uint32_t n_relax = 0xFFFFFFFFu)
 {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= n_shared * nc)
@@ -1435,7 +1435,7 @@ __global__ void __launch_bounds__(256)
   const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
   if ((cm >> c) & 1)
     sum = R ? T(0) : src[(size_t)node * nc + c];
-  if (!R && rb)
+  if (!R && rb && node < n_relax)
     {
       const size_t j = (size_t)node * nc + c;
       sum            = (keep ? src[j] : T(0)) + romega * (rd ? rd[j] : T(1)) * (rb[j] - sum);
@@ -1453,7 +1453,7 @@ __global__ void __launch_bounds__(256)
                       const T *__restrict__ partial, const uint32_t *__restrict__ nodes,
                       const ReduceClasses rc, int64_t n_shared,
                       const T *__restrict__ rb = nullptr, const T *__restrict__ rd = nullptr,
-                      T romega = T(0), int keep = 1)
+                      T romega = T(0), int keep = 1, uint32_t n_relax = 0xFFFFFFFFu)
 {
   // 16-byte packs when a node's row is whole packs (nc = 4): one thread per
   // (node, pack), vector loads and stores
@@ -1498,7 +1498,7 @@ __global__ void __launch_bounds__(256)
         for (int w = 0; w < W; ++w)
           if ((cm >> (kp * W + w)) & 1)
             sum[w] = R ? T(0) : src[(size_t)node * nc + kp * W + w];
-      if (!R && rb)
+      if (!R && rb && node < n_relax)
         {
           const size_t j  = (size_t)node * NPK + kp;
           const V      xs = keep ? reinterpret_cast<const V *>(src)[j] : V{};
@@ -1541,7 +1541,7 @@ __global__ void __launch_bounds__(256)
   const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
   if ((cm >> c) & 1)
     sum = R ? T(0) : src[(size_t)node * nc + c];
-  if (!R && rb)
+  if (!R && rb && node < n_relax)
     {
       const size_t j = (size_t)node * nc + c;
       sum            = (keep ? src[j] : T(0)) + romega * (rd ? rd[j] : T(1)) * (rb[j] - sum);

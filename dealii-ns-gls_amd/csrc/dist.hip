@@ -56,12 +56,17 @@ __global__ void __launch_bounds__(256)
 
 // owned rows += the partial sums the peers computed for them (compress(add));
 // one thread per (receiving node, component), contributions summed in a fixed
-// order, constrained components keep their identity-row value
+// order, constrained components keep their identity-row value.  With a fused
+// relaxation / residual on the local part (dst = x + omega d (b - A_loc x),
+// or omega d (b - A_loc x)), the peers' part of A x enters as
+// dst -= omega d (sum): rd the inverse diagonal (null: 1), scale = omega
+// (0: plain compress(add))
 template <typename T, int nc>
 __global__ void __launch_bounds__(256)
   k_unpack_add(T *__restrict__ dst, const T *__restrict__ xrecv,
                const uint32_t *__restrict__ nodes, const uint32_t *__restrict__ off,
-               const uint32_t *__restrict__ entry, int64_t n)
+               const uint32_t *__restrict__ entry, int64_t n, const T *__restrict__ rd,
+               T scale)
 {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= n * nc)
@@ -74,7 +79,10 @@ __global__ void __launch_bounds__(256)
   T s = 0;
   for (uint32_t e = off[u]; e < off[u + 1]; ++e)
     s += xrecv[(size_t)entry[e] * nc + c];
-  dst[(size_t)(packed & NODE_MASK) * nc + c] += s;
+  const size_t j = (size_t)(packed & NODE_MASK) * nc + c;
+  if (scale != T(0))
+    s *= -scale * (rd ? rd[j] : T(1));
+  dst[j] += s;
 }
 } // namespace gls
 
@@ -160,8 +168,10 @@ launch_pack(glsDist_ *d, const void *src, hipStream_t s)
 
 template <typename T>
 void
-launch_unpack(glsDist_ *d, void *dst, hipStream_t s)
+launch_unpack(glsDist_ *d, void *dst, hipStream_t s, const gls::RelaxStep *rx)
 {
+  const T *rd    = rx ? (const T *)rx->d : nullptr;
+  const T  scale = rx ? (T)rx->omega : T(0);
   const int nc = d->op->dim + 1;
   if (d->n_un == 0)
     return;
@@ -169,11 +179,11 @@ launch_unpack(glsDist_ *d, void *dst, hipStream_t s)
   if (nc == 4)
     hipLaunchKernelGGL((gls::k_unpack_add<T, 4>), g, dim3(256), 0, s, (T *)dst,
                        (const T *)d->d_xrecv_buf, d->d_un_nodes, d->d_un_off, d->d_un_entry,
-                       d->n_un);
+                       d->n_un, rd, scale);
   else
     hipLaunchKernelGGL((gls::k_unpack_add<T, 3>), g, dim3(256), 0, s, (T *)dst,
                        (const T *)d->d_xrecv_buf, d->d_un_nodes, d->d_un_off, d->d_un_entry,
-                       d->n_un);
+                       d->n_un, rd, scale);
   HIP_THROW(hipGetLastError());
 }
 
@@ -187,12 +197,12 @@ pack(glsDist_ *d, const void *src, hipStream_t s)
 }
 
 void
-unpack(glsDist_ *d, void *dst, hipStream_t s)
+unpack(glsDist_ *d, void *dst, hipStream_t s, const gls::RelaxStep *rx = nullptr)
 {
   if (d->op->prec == GLS_F64)
-    launch_unpack<double>(d, dst, s);
+    launch_unpack<double>(d, dst, s, rx);
   else
-    launch_unpack<float>(d, dst, s);
+    launch_unpack<float>(d, dst, s, rx);
 }
 
 ncclDataType_t
@@ -443,22 +453,25 @@ gls_dist_destroy(glsDist d)
   delete d;
 }
 
-glsStatus
-gls_dist_vmult(glsDist d, void *dst, void *src, void *stream)
+namespace
 {
-  GLS_TRY
+// the partitioned vmult of one RCCL rank; rx: the damped-Jacobi step (or the
+// residual) fused into the local bricks and reduce on the owned rows, the
+// peers' contributions entering through the unpack (k_unpack_add)
+void
+dist_vmult(glsDist d, void *dst, void *src, hipStream_t s, const gls::RelaxStep *rx)
+{
   check_vectors(d, dst, src);
   if (!d->comm)
     throw std::runtime_error("gls_dist_vmult: in-process group members run gls_dist_vmult_group");
-  hipStream_t   s    = (hipStream_t)stream;
   glsOp_       *op   = d->op;
   const int     mode = gls::op_vmult_mode(op);
   if (d->peers.empty()) // one rank: nothing to exchange
     {
       gls::brick_launch(op, mode, dst, src, 0, op->n_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE,
-                        s);
+                        s, rx);
       zero_ghosts(d, dst, s);
-      return 0;
+      return;
     }
   // import (comm stream) || interior bricks (s)
   pack(d, src, s);
@@ -466,25 +479,23 @@ gls_dist_vmult(glsDist d, void *dst, void *src, void *stream)
   HIP_THROW(hipStreamWaitEvent(d->cs, d->ev_packed, 0));
   nccl_import(d, src);
   HIP_THROW(hipEventRecord(d->ev_imported, d->cs));
-  gls::brick_launch(op, mode, dst, src, 0, op->n_interior_bricks, gls::BRICK_RUN, s);
+  gls::brick_launch(op, mode, dst, src, 0, op->n_interior_bricks, gls::BRICK_RUN, s, rx);
   HIP_THROW(hipStreamWaitEvent(s, d->ev_imported, 0));
   gls::brick_launch(op, mode, dst, src, op->n_interior_bricks, op->n_bricks,
-                    gls::BRICK_RUN | gls::BRICK_REDUCE, s);
+                    gls::BRICK_RUN | gls::BRICK_REDUCE, s, rx);
   // compress(add)
   nccl_export(d, dst, s);
-  unpack(d, dst, s);
+  unpack(d, dst, s, rx);
   zero_ghosts(d, dst, s);
-  GLS_CATCH
 }
 
-glsStatus
-gls_dist_vmult_group(glsDist const *members, void *const *dsts, void *const *srcs, int n,
-                     void *stream)
+// the in-process group's vmult; rx: per member, or null
+void
+dist_vmult_group(glsDist const *members, void *const *dsts, void *const *srcs, int n,
+                 hipStream_t s, const gls::RelaxStep *rx)
 {
-  GLS_TRY
   if (!members || !dsts || !srcs || n < 1)
     throw std::runtime_error("gls_dist_vmult_group: bad arguments");
-  hipStream_t s = (hipStream_t)stream;
   for (int r = 0; r < n; ++r)
     {
       check_vectors(members[r], dsts[r], srcs[r]);
@@ -499,7 +510,7 @@ gls_dist_vmult_group(glsDist const *members, void *const *dsts, void *const *src
     {
       glsOp_ *op = members[r]->op;
       gls::brick_launch(op, gls::op_vmult_mode(op), dsts[r], srcs[r], 0, op->n_interior_bricks,
-                        gls::BRICK_RUN, s);
+                        gls::BRICK_RUN, s, rx ? rx + r : nullptr);
     }
   for (int r = 0; r < n; ++r)
     local_import(members[r], s);
@@ -507,14 +518,31 @@ gls_dist_vmult_group(glsDist const *members, void *const *dsts, void *const *src
     {
       glsOp_ *op = members[r]->op;
       gls::brick_launch(op, gls::op_vmult_mode(op), dsts[r], srcs[r], op->n_interior_bricks,
-                        op->n_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE, s);
+                        op->n_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE, s, rx ? rx + r : nullptr);
     }
   for (int r = 0; r < n; ++r)
     local_export(members[r], s);
   for (int r = 0; r < n; ++r)
-    unpack(members[r], dsts[r], s);
+    unpack(members[r], dsts[r], s, rx ? rx + r : nullptr);
   for (int r = 0; r < n; ++r)
     zero_ghosts(members[r], dsts[r], s);
+}
+} // namespace
+
+glsStatus
+gls_dist_vmult(glsDist d, void *dst, void *src, void *stream)
+{
+  GLS_TRY
+  dist_vmult(d, dst, src, (hipStream_t)stream, nullptr);
+  GLS_CATCH
+}
+
+glsStatus
+gls_dist_vmult_group(glsDist const *members, void *const *dsts, void *const *srcs, int n,
+                     void *stream)
+{
+  GLS_TRY
+  dist_vmult_group(members, dsts, srcs, n, (hipStream_t)stream, nullptr);
   GLS_CATCH
 }
 
@@ -642,12 +670,6 @@ dist_op(glsDist d)
   return d->op;
 }
 
-bool
-dist_has_peers(glsDist d)
-{
-  return !d->peers.empty();
-}
-
 int
 dist_rank(glsDist d)
 {
@@ -661,13 +683,14 @@ dist_world(glsDist d)
 }
 
 void
-team_vmult(glsDist const *m, void *const *dst, void *const *src, int n, hipStream_t s)
+team_vmult(glsDist const *m, void *const *dst, void *const *src, int n, hipStream_t s,
+           const RelaxStep *rx)
 {
   check_team(m, n);
-  glsStatus st = m[0]->comm ? gls_dist_vmult(m[0], dst[0], src[0], s)
-                            : gls_dist_vmult_group(m, dst, src, n, s);
-  if (st)
-    throw std::runtime_error(gls_last_error());
+  if (m[0]->comm)
+    dist_vmult(m[0], dst[0], src[0], s, rx);
+  else
+    dist_vmult_group(m, dst, src, n, s, rx);
 }
 
 void

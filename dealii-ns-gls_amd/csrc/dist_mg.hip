@@ -294,16 +294,15 @@ team_scale(Team &t, int l, const std::vector<void *> &x, double a, hipStream_t s
   HIP_THROW(hipGetLastError());
 }
 
-// true when a partitioned apply on level l exchanges halos (some member has
-// peers); false at world 1, where the fused single-domain kernels apply
+// the level's apply can take the fused relaxation / residual: brick
+// kernels, no outflow faces (their terms come after the cell kernels)
 bool
-exchanges(Team &t, int l)
+fusable(Team &t, int l)
 {
   for (auto *x : t.m)
-    if (gls::dist_has_peers(x->lv[(size_t)l]) || !gls::dist_op(x->lv[(size_t)l])->use_brick ||
-        gls::dist_op(x->lv[(size_t)l])->faces.n > 0)
-      return true;
-  return false;
+    if (!gls::dist_op(x->lv[(size_t)l])->use_brick || gls::dist_op(x->lv[(size_t)l])->faces.n > 0)
+      return false;
+  return true;
 }
 
 // PreconditionRelaxation::vmult (zero start) / step, `iters` damped-Jacobi
@@ -318,25 +317,27 @@ smooth(Team &t, int l, bool zero, int iters, hipStream_t s)
         check(gls_mg_relax(x->tr, l, x->X[l], x->B[l], nullptr, x->invd[l], x->omega[l], 1, s));
       it = 1;
     }
-  const bool alone = !exchanges(t, l);
+  const bool fused = fusable(t, l);
   for (; it < iters; ++it)
     {
-      if (alone)
+      if (fused)
         {
-          // no exchange: the single-domain smoother, the damped-Jacobi step
-          // fused into the brick write-out and the shared-node reduce, into
-          // T; then X and T swap roles
-          for (auto *x : t.m)
+          // the damped-Jacobi step fused into the partitioned apply (brick
+          // write-out and shared-node reduce on the owned rows, the peers'
+          // contributions as -omega d sum in the unpack), into T; then X and
+          // T swap roles
+          std::vector<gls::RelaxStep> rx((size_t)t.n());
+          for (int r = 0; r < t.n(); ++r)
             {
-              glsOp_        *op = gls::dist_op(x->lv[(size_t)l]);
-              gls::RelaxStep rx;
-              rx.b     = x->B[l];
-              rx.d     = x->invd[l];
-              rx.omega = x->omega[l];
-              gls::brick_launch(op, gls::op_vmult_mode(op), x->T[l], x->X[l], 0, op->n_bricks,
-                                gls::BRICK_RUN | gls::BRICK_REDUCE, s, &rx);
-              std::swap(x->X[l], x->T[l]);
+              rx[(size_t)r].b     = t.m[r]->B[l];
+              rx[(size_t)r].d     = t.m[r]->invd[l];
+              rx[(size_t)r].omega = t.m[r]->omega[l];
             }
+          auto X = per(t, [&](glsDistMG_ *x) { return x->X[l]; });
+          auto T = per(t, [&](glsDistMG_ *x) { return x->T[l]; });
+          gls::team_vmult(t.level(l), T.data(), X.data(), t.n(), s, rx.data());
+          for (auto *x : t.m)
+            std::swap(x->X[l], x->T[l]);
           continue;
         }
       auto X = per(t, [&](glsDistMG_ *x) { return x->X[l]; });
@@ -419,26 +420,21 @@ v_step(Team &t, int l, hipStream_t s)
     }
   const int ns = t.m[0]->desc.smoothing_n_iterations;
   smooth(t, l, true, ns, s);
-  const bool alone = !exchanges(t, l);
-  if (alone)
-    // no exchange: the residual b - A x fused into the brick write-out and
-    // the shared-node reduce (RelaxStep with d = 1, omega = 1, keep = false)
-    for (auto *x : t.m)
+  const bool alone = fusable(t, l);
+  {
+    // the residual b - A x fused into the partitioned apply (RelaxStep with
+    // d = 1, omega = 1, keep = false) where the level allows it
+    std::vector<gls::RelaxStep> rx((size_t)t.n());
+    for (int r = 0; r < t.n(); ++r)
       {
-        glsOp_        *op = gls::dist_op(x->lv[(size_t)l]);
-        gls::RelaxStep rx;
-        rx.b     = x->B[l];
-        rx.omega = 1.0;
-        rx.keep  = false;
-        gls::brick_launch(op, gls::op_vmult_mode(op), x->T[l], x->X[l], 0, op->n_bricks,
-                          gls::BRICK_RUN | gls::BRICK_REDUCE, s, &rx);
+        rx[(size_t)r].b     = t.m[r]->B[l];
+        rx[(size_t)r].omega = 1.0;
+        rx[(size_t)r].keep  = false;
       }
-  else
-    {
-      auto X = per(t, [&](glsDistMG_ *x) { return x->X[l]; });
-      auto T = per(t, [&](glsDistMG_ *x) { return x->T[l]; });
-      gls::team_vmult(t.level(l), T.data(), X.data(), t.n(), s);
-    }
+    auto X = per(t, [&](glsDistMG_ *x) { return x->X[l]; });
+    auto T = per(t, [&](glsDistMG_ *x) { return x->T[l]; });
+    gls::team_vmult(t.level(l), T.data(), X.data(), t.n(), s, alone ? rx.data() : nullptr);
+  }
   for (auto *x : t.m)
     {
       const int64_t n = x->n_dofs[(size_t)l];

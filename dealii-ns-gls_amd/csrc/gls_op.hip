@@ -854,7 +854,7 @@ struct Impl
               hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, false>), g3, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)op->d_partial,
                                  op->d_shared_nodes, rc, op->n_shared, a.rb, a.rd, a.romega,
-                                 a.rkeep);
+                                 a.rkeep, (uint32_t)op->n_owned_nodes);
             else if (mode == MODE_RESIDUAL)
               hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, true>), g2, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)op->d_partial,
@@ -863,7 +863,7 @@ struct Impl
               hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, false>), g2, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)op->d_partial,
                                  op->d_shared_nodes, op->d_shared_off, op->n_shared, a.rb,
-                                 a.rd, a.romega, a.rkeep);
+                                 a.rd, a.romega, a.rkeep, (uint32_t)op->n_owned_nodes);
             HIP_THROW(hipGetLastError());
           }
       }

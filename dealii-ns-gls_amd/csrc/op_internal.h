@@ -212,12 +212,11 @@ fused_relax_ok(const glsOp_ *op)
 // one process drives in lockstep — one RCCL rank, or all members of an
 // in-process group (rank order)
 glsOp_ *dist_op(glsDist d);
-// false: the partition exchanges nothing (world 1): its vmult is the
-// single-domain one and the fused relaxation / residual apply
-bool    dist_has_peers(glsDist d);
 int     dist_rank(glsDist d);
 int     dist_world(glsDist d);
-void    team_vmult(glsDist const *m, void *const *dst, void *const *src, int n, hipStream_t s);
+// rx: per member, the damped-Jacobi step / residual fused on the owned rows
+void    team_vmult(glsDist const *m, void *const *dst, void *const *src, int n, hipStream_t s,
+                   const RelaxStep *rx = nullptr);
 void    team_update_ghosts(glsDist const *m, void *const *v, int n, hipStream_t s);
 void    team_compress_add(glsDist const *m, void *const *v, int n, hipStream_t s);
 // buf[r][0 .. count) <- the sum over the team's ranks (ncclAllReduce / member order)
