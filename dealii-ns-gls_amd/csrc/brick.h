@@ -978,7 +978,10 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
 #pragma unroll
           for (int d = 0; d < dim; ++d)
             u2 += cur.U[d] * cur.U[d];
-          delta_qwise(u2, cur.h, a.nu, a.stau, d1, d2);
+          if (GLS_FAST_DELTA)
+            delta_qwise_fast(u2, cur.h, a.nu, a.stau, d1, d2);
+          else
+            delta_qwise(u2, cur.h, a.nu, a.stau, d1, d2);
         }
       if constexpr ((GLS_BABL & 8) != 0)
         {
