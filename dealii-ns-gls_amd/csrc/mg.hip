@@ -771,7 +771,21 @@ __global__ void __launch_bounds__(256)
 // loads (contiguous), x (FP32, the coarse defect's free entries: exact for
 // FP32 levels) from L2, FP64 sums in a fixed order (lane partials, then a
 // fixed shuffle tree), and writes y[free[row]] itself: no partial-sum pass.
-template <typename T>
+typedef float gemv_f4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ float4
+gemv_row_load(const float4 *p)
+{
+  if constexpr (NT)
+    {
+      const gemv_f4 t = __builtin_nontemporal_load(reinterpret_cast<const gemv_f4 *>(p));
+      return make_float4(t.x, t.y, t.z, t.w);
+    }
+  else
+    return *p;
+}
+
+template <typename T, bool NT>
 __global__ void __launch_bounds__(256)
   k_gemv_rows_f32(const float4 *__restrict__ M, const float4 *__restrict__ x,
                   T *__restrict__ y, const int32_t *__restrict__ free, int64_t n, int64_t ld)
@@ -790,7 +804,7 @@ __global__ void __launch_bounds__(256)
       float4 m[4], xv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        m[u] = mr[c + 64 * u];
+        m[u] = gemv_row_load<NT>(mr + c + 64 * u);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         xv[u] = x[c + 64 * u];
@@ -803,7 +817,7 @@ __global__ void __launch_bounds__(256)
     }
   for (; c < l4; c += 64)
     {
-      const float4 m0 = mr[c], x0 = x[c];
+      const float4 m0 = gemv_row_load<NT>(mr + c), x0 = x[c];
       a0 += (double)m0.x * (double)x0.x + (double)m0.y * (double)x0.y;
       a1 += (double)m0.z * (double)x0.z + (double)m0.w * (double)x0.w;
     }
@@ -1162,9 +1176,20 @@ coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
       float *xf = reinterpret_cast<float *>(mg->d_rhs);
       hipLaunchKernelGGL(k_coarse_prep<T>, g1(std::max(n, ld)), dim3(256), 0, s, (T *)mg->sol[0],
                          (const T *)mg->def[0], xf, (const int32_t *)mg->d_free, n, nf, ld);
-      hipLaunchKernelGGL(k_gemv_rows_f32<T>, dim3((unsigned)((nf + 3) / 4)), dim3(256), 0, s,
-                         (const float4 *)mg->d_inv32, (const float4 *)xf, (T *)mg->sol[0],
-                         (const int32_t *)mg->d_free, nf, ld);
+      // the inverse is read once per solve and is larger than the MALL:
+      // non-temporal row loads (GLS_GEMV_NT=0: default policy)
+      static const bool nt = [] {
+        const char *e = getenv("GLS_GEMV_NT");
+        return !e || std::atoi(e) != 0;
+      }();
+      if (nt)
+        hipLaunchKernelGGL((k_gemv_rows_f32<T, true>), dim3((unsigned)((nf + 3) / 4)), dim3(256),
+                           0, s, (const float4 *)mg->d_inv32, (const float4 *)xf, (T *)mg->sol[0],
+                           (const int32_t *)mg->d_free, nf, ld);
+      else
+        hipLaunchKernelGGL((k_gemv_rows_f32<T, false>), dim3((unsigned)((nf + 3) / 4)), dim3(256),
+                           0, s, (const float4 *)mg->d_inv32, (const float4 *)xf, (T *)mg->sol[0],
+                           (const int32_t *)mg->d_free, nf, ld);
       HIP_THROW(hipGetLastError());
       return;
     }
