@@ -33,9 +33,17 @@ $(LIBDIR)/libglsmesh.so: $(MESH_SRC) include/gls_mesh.h
 	@mkdir -p $(LIBDIR)
 	$(CXX) $(CXXFLAGS) -shared -o $@ $(MESH_SRC)
 
-$(LIBDIR)/libglsamd.so: $(AMD_SRC) $(AMD_HDR)
+# one object per source (make -j builds them in parallel), then one link
+OBJDIR   := $(PKG)/build
+AMD_OBJ  := $(patsubst $(PKG)/csrc/%,$(OBJDIR)/%.o,$(AMD_SRC))
+
+$(OBJDIR)/%.o: $(PKG)/csrc/% $(AMD_HDR)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIBDIR)/libglsamd.so: $(AMD_OBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(AMD_SRC) $(AMD_LIBS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(AMD_OBJ) $(AMD_LIBS)
 
 # C++ facade parity program (test infrastructure: links the oracle)
 CPPTEST := tests/cpp/build/test_operator
@@ -50,9 +58,8 @@ $(CPPTEST): tests/cpp/test_operator.cc include/gls_operator.hpp include/gls_op.h
 
 clean:
 	rm -f $(LIBDIR)/*.so $(CPPTEST)
+	rm -rf $(OBJDIR)
 	$(MAKE) -C oracle clean
 
 .PHONY: all mesh amd oracle cpptest clean
 
-# diagnostic variant builds (timing experiments; wrong results by design for
-# the GLS_BABL ablations): scripts/build_variants.sh < "<name> <-D flags>" lines

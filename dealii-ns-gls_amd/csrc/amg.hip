@@ -430,6 +430,13 @@ free_csr(DevCSR &D)
 }
 } // namespace
 
+// largest coarsest level that gets a dense inverse (n^2 doubles)
+int64_t
+amg_dense_limit(const glsAMGParams &prm)
+{
+  return std::max<int64_t>(4 * (int64_t)prm.coarse_max_size, 2048);
+}
+
 struct AmgLevel
 {
   DevCSR  A, P, R; // P: n x n_coarse, R = P^T (none on the coarsest)
@@ -452,7 +459,12 @@ namespace gls
 {
 namespace
 {
-// Chebyshev smoothing of degree s on level l (x, d: pending iterate x + d)
+// Chebyshev smoothing on level l (x, d: pending iterate x + d): s + 1
+// Chebyshev steps in both cases.  The nonzero start forms its first
+// correction from the residual f - A x (one matrix-vector product); the
+// zero start skips that product (A 0 = 0), so pre-smoothing costs s and
+// post-smoothing s + 1 products for the same polynomial (tests/amg_ref.py
+// _cheb runs the same steps).
 void
 chebyshev(glsAMG_ *amg, AmgLevel &L, bool zero_start, hipStream_t st)
 {
@@ -472,7 +484,7 @@ chebyshev(glsAMG_ *amg, AmgLevel &L, bool zero_start, hipStream_t st)
                          (const double *)nullptr, L.f, L.dinv, xo, dn, 0.0, 1.0 / th, n);
       std::swap(x, xo), std::swap(d, dn);
     }
-  for (int k = 0; k < s; ++k) // s further matrix-vector products: degree s
+  for (int k = 0; k < s; ++k) // s further steps, one matrix-vector product each
     {
       const double rn = 1.0 / (2.0 * sg - rho);
       hipLaunchKernelGGL(k_cheb_step, rows_grid(n), dim3(256), 0, st, L.A.rp, L.A.ci, L.A.v, x, d,
@@ -493,8 +505,17 @@ vcycle_level(glsAMG_ *amg, size_t l, hipStream_t st)
   AmgLevel &L = amg->lv[l];
   if (l + 1 == amg->lv.size())
     {
-      hipLaunchKernelGGL(k_dense_gemv, rows_grid(L.A.n), dim3(256), 0, st, amg->d_inv, L.f, L.x,
-                         L.A.n);
+      if (amg->d_inv)
+        hipLaunchKernelGGL(k_dense_gemv, rows_grid(L.A.n), dim3(256), 0, st, amg->d_inv, L.f, L.x,
+                           L.A.n);
+      else
+        {
+          // coarsest level above the dense limit (aggregation stalled or
+          // max_levels reached): smoothing sweeps as its solve, x = x + d
+          chebyshev(amg, L, true, st);
+          hipLaunchKernelGGL(k_add2, elem_grid(L.A.n), dim3(256), 0, st, L.x, L.d, L.x2, L.A.n);
+          std::swap(L.x, L.x2);
+        }
       HIP_THROW(hipGetLastError());
       return;
     }
@@ -567,8 +588,11 @@ gls_amg_create(int64_t n, const int64_t *row_ptr, const int64_t *cols, const dou
   std::vector<HostCSR> hA{A};
   for (int lev = 0;; ++lev)
     {
-      HostCSR            &Al = hA.back();
-      AmgLevel            L;
+      HostCSR &Al = hA.back();
+      // the level joins the hierarchy before any of its buffers exists, so
+      // the guard frees whatever a failure below leaves allocated
+      amg->lv.emplace_back();
+      AmgLevel           &L = amg->lv.back();
       std::vector<double> d = diagonal(Al), dinv((size_t)Al.n);
       for (int64_t i = 0; i < Al.n; ++i)
         dinv[(size_t)i] = d[(size_t)i] != 0.0 ? 1.0 / d[(size_t)i] : 1.0;
@@ -587,10 +611,7 @@ gls_amg_create(int64_t n, const int64_t *row_ptr, const int64_t *cols, const dou
           const std::vector<int32_t> agg   = aggregate(Al, b, prm->threshold, n_agg);
           const int64_t              nc    = (int64_t)n_agg * b;
           if (nc >= Al.n)
-            {
-              amg->lv.push_back(L);
-              break; // no coarsening: this level is the coarsest
-            }
+            break; // no coarsening: this level is the coarsest
           // tentative prolongator: P[i, agg(i) b + comp(i)] = beta_i / |beta_(agg, comp)|
           // (rows of Dirichlet points empty)
           std::vector<double> nrm((size_t)nc, 0.0);
@@ -655,50 +676,57 @@ gls_amg_create(int64_t n, const int64_t *row_ptr, const int64_t *cols, const dou
           HostCSR Ac = multiply(R, multiply(Al, P));
           L.P        = to_device(P);
           L.R        = to_device(R);
-          amg->lv.push_back(L);
           beta.assign(nrm.begin(), nrm.end()); // coarse near-null space (the R of the QR)
           hA.push_back(std::move(Ac));
           continue;
         }
-      amg->lv.push_back(L);
       break;
     }
-  // coarsest: dense inverse (LU + inverse on the device)
+  // coarsest: dense inverse (LU + inverse on the device) up to the dense
+  // limit; a larger coarsest level (aggregation stalled or max_levels
+  // reached) is smoothed instead of factorised (a dense matrix of it would
+  // need n^2 doubles on the host and the device)
+  amg->n_coarse = hA.back().n;
+  if (hA.back().n <= amg_dense_limit(*prm))
   {
     const HostCSR &Ac = hA.back();
     const int64_t  nc = Ac.n;
-    amg->n_coarse     = nc;
     std::vector<double> dense((size_t)nc * nc, 0.0); // column major for rocSOLVER
     for (int64_t r = 0; r < nc; ++r)
       for (int64_t k = Ac.rp[(size_t)r]; k < Ac.rp[(size_t)r + 1]; ++k)
         dense[(size_t)Ac.ci[(size_t)k] * nc + r] = Ac.v[(size_t)k];
-    double      *d_a = nullptr;
-    rocblas_int *ipiv = nullptr, *info = nullptr;
+    double *d_a = nullptr;
     HIP_THROW(hipMalloc((void **)&d_a, dense.size() * 8));
-    HIP_THROW(hipMalloc((void **)&ipiv, (size_t)nc * sizeof(rocblas_int)));
-    HIP_THROW(hipMalloc((void **)&info, sizeof(rocblas_int)));
+    amg->d_inv = d_a; // owned by the guard from here on
+    struct Scratch    // pivots, info and the rocBLAS handle, freed on every path
+    {
+      rocblas_int   *ipiv = nullptr, *info = nullptr;
+      rocblas_handle h    = nullptr;
+      ~Scratch()
+      {
+        (void)hipFree(ipiv), (void)hipFree(info);
+        if (h)
+          rocblas_destroy_handle(h);
+      }
+    } w;
+    HIP_THROW(hipMalloc((void **)&w.ipiv, (size_t)nc * sizeof(rocblas_int)));
+    HIP_THROW(hipMalloc((void **)&w.info, sizeof(rocblas_int)));
     HIP_THROW(hipMemcpy(d_a, dense.data(), dense.size() * 8, hipMemcpyHostToDevice));
-    rocblas_handle h = nullptr;
-    if (rocblas_create_handle(&h) != rocblas_status_success)
+    if (rocblas_create_handle(&w.h) != rocblas_status_success)
       throw std::runtime_error("gls_amg_create: rocblas_create_handle failed");
-    rocblas_status st = rocsolver_dgetrf(h, (rocblas_int)nc, (rocblas_int)nc, d_a,
-                                         (rocblas_int)nc, ipiv, info);
+    rocblas_status st = rocsolver_dgetrf(w.h, (rocblas_int)nc, (rocblas_int)nc, d_a,
+                                         (rocblas_int)nc, w.ipiv, w.info);
     rocblas_int    hinfo = 0;
     if (st == rocblas_status_success)
       {
-        HIP_THROW(hipMemcpy(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost));
+        HIP_THROW(hipMemcpy(&hinfo, w.info, sizeof(hinfo), hipMemcpyDeviceToHost));
         if (hinfo == 0)
-          st = rocsolver_dgetri(h, (rocblas_int)nc, d_a, (rocblas_int)nc, ipiv, info);
+          st = rocsolver_dgetri(w.h, (rocblas_int)nc, d_a, (rocblas_int)nc, w.ipiv, w.info);
       }
     if (st == rocblas_status_success && hinfo == 0)
-      HIP_THROW(hipMemcpy(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost));
-    rocblas_destroy_handle(h);
-    (void)hipFree(ipiv), (void)hipFree(info);
+      HIP_THROW(hipMemcpy(&hinfo, w.info, sizeof(hinfo), hipMemcpyDeviceToHost));
     if (st != rocblas_status_success || hinfo != 0)
-      {
-        (void)hipFree(d_a);
-        throw std::runtime_error("gls_amg_create: singular coarsest AMG matrix");
-      }
+      throw std::runtime_error("gls_amg_create: singular coarsest AMG matrix");
     // column-major inverse -> row major for the wavefront-per-row GEMV
     std::vector<double> inv(dense.size());
     HIP_THROW(hipMemcpy(inv.data(), d_a, inv.size() * 8, hipMemcpyDeviceToHost));
@@ -706,7 +734,6 @@ gls_amg_create(int64_t n, const int64_t *row_ptr, const int64_t *cols, const dou
       for (int64_t c = 0; c < nc; ++c)
         dense[(size_t)r * nc + c] = inv[(size_t)c * nc + r];
     HIP_THROW(hipMemcpy(d_a, dense.data(), dense.size() * 8, hipMemcpyHostToDevice));
-    amg->d_inv = d_a;
   }
   guard.p = nullptr;
   *out    = amg;

@@ -19,9 +19,11 @@
 // FE_Q(k) and QGauss(k+1) both have (k+1)^dim points; a cell never straddles
 // a wavefront (3D Q2: 2 cells = 54 of 64 lanes), so the LDS sum-factorisation
 // sweeps are ordered by wavefront fences, not workgroup barriers.
-// Occupancy is the lever (the kernel is LDS-latency bound at low wave
-// counts): 3 waves/SIMD (FP64, 162 VGPRs, 44 KB LDS per workgroup).
-// Software-pipelining the next round's loads was measured and gave nothing.
+// Occupancy: 3 waves/SIMD for the FP64 kernels with curved bricks (164
+// VGPRs, 44 KB LDS per workgroup), 4 for the Cartesian FP64 and the FP32
+// ones (BrickOcc).  Variants measured and not kept (persistent pipelined
+// bricks, fused last-arriver reduction, ablation builds) are on the git tag
+// r3-variants.
 #pragma once
 
 #include "common.h"
@@ -33,45 +35,19 @@ namespace gls
 constexpr uint32_t SHARED_BIT  = 0x80000000u;
 constexpr uint32_t UNUSED_NODE = 0x0FFFFFFFu; // lattice node outside a split brick
 
-// GLS_STAMPS: diagnostic timeline build (never the product library): lane 0
-// of every wave records s_memrealtime (100 MHz) at phase boundaries of each
-// brick into g_stamps[brick][wave][8].
-#ifdef GLS_STAMPS
-constexpr size_t GLS_STAMP_MAX = 16384 * 4 * 8;
-__device__ unsigned long long g_stamps[GLS_STAMP_MAX];
-#define GLS_STAMP(brick, i)                                                                   \
-  do                                                                                         \
-    {                                                                                        \
-      const size_t si_ = ((size_t)(brick) * (BLOCK / 64) + (threadIdx.x >> 6)) * 8 + (i);    \
-      if ((threadIdx.x & 63) == 0 && si_ < GLS_STAMP_MAX)                                    \
-        g_stamps[si_] = __builtin_amdgcn_s_memrealtime();                                    \
-    }                                                                                        \
-  while (0)
-#else
-#define GLS_STAMP(brick, i)                                                                   \
-  do                                                                                         \
-    {                                                                                        \
-    }                                                                                        \
-  while (0)
-#endif
-
 template <int dim>
 struct BrickMax
 {
   static constexpr int cells = dim == 3 ? 4 : 8; // cells per direction
 };
 
-#ifndef GLS_BRICK_MAXZ
-#define GLS_BRICK_MAXZ 1
-#endif
 template <int dim, int k>
 struct BrickLattice
 {
   // largest lattice the brick kernel takes: 3D bricks of up to 4x4x1 cells
-  // (build_bricks runs 3D bricks as one-cell layers; GLS_BRICK_MAXZ layers in
-  // variant builds), 2D up to 8x8 cells
+  // (build_bricks runs 3D bricks as one-cell layers), 2D up to 8x8 cells
   static constexpr int side = k * BrickMax<dim>::cells + 1;
-  static constexpr int L    = dim == 3 ? side * side * (k * GLS_BRICK_MAXZ + 1) : side * side;
+  static constexpr int L    = dim == 3 ? side * side * (k + 1) : side * side;
   static constexpr bool fits = L <= 729;
 };
 
@@ -135,62 +111,8 @@ struct BrickArgs
   int             PLx, PLy, LP; // padded LDS lattice strides / size (>= L)
   T               nu, w0, theta, stau;
   int             td, cw, have_prev, have_old_grad;
-  // fused shared-node reduction (single-domain full vmult): per shared node
-  // an arrival counter (zero between launches); the brick whose arrival
-  // completes a node sums its partial slots and writes dst there, instead of
-  // k_shared_reduce_cls.  null: partial slots only.
-  uint32_t       *counters;
-  uint32_t        partial_bytes;
-  ReduceClasses   rc;
   Shape<T, n>     sh;
 };
-
-// partial slots of the fused reduction: written through to memory (sc1) and
-// read back the same way, so a brick on another XCD sees them once the
-// writer's arrival is counted (MI355X_MICROARCH.md, inter-workgroup
-// visibility: sc1 stores, vmcnt(0) + barrier before the counter add, sc1
-// loads by the last arriver after its add returned)
-typedef unsigned int U4 __attribute__((ext_vector_type(4)));
-
-template <typename T, int nc>
-__device__ __forceinline__ void
-store_slot_wt(__amdgpu_buffer_rsrc_t rs, uint32_t slot, const T (&r)[nc])
-{
-  constexpr int NB = nc * sizeof(T) / 16; // the fused path runs whole 16-byte slots only
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-    {
-      U4 v;
-      __builtin_memcpy(&v, reinterpret_cast<const char *>(r) + 16 * b, 16);
-      __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(slot * (uint32_t)(nc * sizeof(T)) + 16 * b),
-                                             0, 16);
-    }
-}
-
-template <typename T, int nc>
-__device__ __forceinline__ void
-load_slot_wt(__amdgpu_buffer_rsrc_t rs, uint32_t slot, T (&r)[nc])
-{
-  constexpr int NB = nc * sizeof(T) / 16;
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-    {
-      const U4 v = __builtin_amdgcn_raw_buffer_load_b128(
-        rs, (int)(slot * (uint32_t)(nc * sizeof(T)) + 16 * b), 0, 16);
-      __builtin_memcpy(reinterpret_cast<char *>(r) + 16 * b, &v, 16);
-    }
-}
-
-__device__ __forceinline__ int
-slot_class(const ReduceClasses &rc, uint32_t slot)
-{
-  int kc = 0;
-#pragma unroll
-  for (int j = 1; j < ReduceClasses::MAX; ++j)
-    if (j < rc.n && slot >= rc.slot0[j])
-      kc = j;
-  return kc;
-}
 
 // 1D coefficient tables in LDS: S, S^T, Dq, Dq^T, each row padded to whole
 // 16-byte packs (RP values) so that a lane's row M[pa][*] (or M[*][pa]) is
@@ -290,9 +212,9 @@ struct BrickLDS
   static constexpr int WPB = BLOCK / 64;
   static constexpr int ORG = 64; // cell-origin table entries (cells per brick)
   static size_t
-  bytes(int L, bool pipe = false) // L: padded LDS lattice size; pipe: two src lattices
+  bytes(int L) // L: padded LDS lattice size
   {
-    return 16 * ((size_t)(pipe ? 2 : 1) * NP * L + (size_t)WPB * CPW * WB) + tab_offset(L) +
+    return 16 * ((size_t)NP * L + (size_t)WPB * CPW * WB) + tab_offset(L) +
            sizeof(T) * 4 * n * CoefRow<T, n>::RP + sizeof(int) * ORG;
   }
   __host__ __device__ static size_t
@@ -302,35 +224,15 @@ struct BrickLDS
   }
 };
 
-#ifndef GLS_INV_ZERO
-#define GLS_INV_ZERO 1
-#endif
-// GLS_BABL: diagnostic-only ablation builds of k_brick (timing only, wrong
-// results by design; never the product library): 1 no cell rounds (prologue
-// + write-out), 2 no table / geometry loads, 4 no LDS sweeps, 8 no q-point
-// physics
-#ifndef GLS_BABL
-#define GLS_BABL 0
-#endif
 // Table formulation of the brick kernel (the tables hold
-// the reference's per-q fields, operator_ns.h:120-132, plus T1 and h):
-//   GLS_NEWTON_T1: the Newton vmult streams T1 (Fields::T1, the
-//     linearization-point part of R1, formed once per linearization point
-//     and time weights by k_finalize_t1) instead of grad P* and Ut_old;
-//   GLS_DELTA_OTF: q-wise delta_1 / delta_2 recomputed from U and h at the
-//     q point (delta_qwise, the producer's expression) instead of streamed.
-// Together: 16 instead of the reference's 20 values per q (round 2: r3
-// 283 -> 272 us), and the register budget that lets the Cartesian kernel
-// run 4 waves per SIMD (round 3).
-#ifndef GLS_NEWTON_T1
-#define GLS_NEWTON_T1 1
-#endif
-#ifndef GLS_DELTA_OTF
-#define GLS_DELTA_OTF 1
-#endif
-#ifndef GLS_LATE_PREFETCH
-#define GLS_LATE_PREFETCH 0
-#endif
+// the reference's per-q fields, operator_ns.h:120-132, plus T1 and h): the
+// Newton vmult streams T1 (Fields::T1, the linearization-point part of R1,
+// formed once per linearization point and time weights by k_finalize_t1)
+// instead of grad P* and Ut_old, and recomputes the q-wise delta_1 /
+// delta_2 from U and h at the q point (delta_qwise_fast, the producer's
+// expression) instead of streaming them: 16 instead of the reference's 20
+// values per q (round 2: r3 283 -> 272 us), and the register budget that
+// lets the Cartesian kernel run 4 waves per SIMD (round 3).
 // q-wise delta_1 / delta_2 recomputed in the kernel: the Q2 Newton vmult
 // only (its sqrt / division temporaries push other instantiations over their
 // register budget)
@@ -338,7 +240,7 @@ template <int k, int MODE>
 __host__ __device__ constexpr bool
 delta_otf()
 {
-  return GLS_DELTA_OTF && MODE == MODE_NEWTON && k == 2;
+  return MODE == MODE_NEWTON && k == 2;
 }
 
 // the table fields a brick vmult / residual of MODE streams: Newton U, grad U,
@@ -354,10 +256,8 @@ field_read(int f)
   const bool h    = f == F::H;
   const bool ut   = f >= F::UT && f < F::UT + dim;
   const bool gu   = f >= F::GU && f < F::GU + dim * dim;
-  const bool gp   = f >= F::GP && f < F::GP + dim;
   const bool t1   = f >= F::T1 && f < F::T1 + dim;
-  const bool newt = GLS_NEWTON_T1 ? (gu || t1) : (gu || gp || ut);
-  return (delta_otf<k, MODE>() ? h : d12) || u || (MODE == MODE_NEWTON && newt) ||
+  return (delta_otf<k, MODE>() ? h : d12) || u || (MODE == MODE_NEWTON && (gu || t1)) ||
          (MODE == MODE_RESIDUAL && ut);
 }
 
@@ -380,6 +280,17 @@ group_ut_only(int g, int W)
   return MODE == MODE_NEWTON && any && !other;
 }
 
+// Geometry of a launch's bricks (build_bricks orders the Cartesian and the
+// curved bricks of each segment into separate runs): GEO_CART bricks hold
+// one diagonal J^{-1} and det J per cell, GEO_GEN bricks J^{-1} and JxW per
+// q point, GEO_ANY reads the type per brick (brick_geo bit 0).
+enum
+{
+  GEO_ANY  = 0,
+  GEO_CART = 1,
+  GEO_GEN  = 2
+};
+
 // everything one lane needs from HBM for one (cell, q point)
 template <int dim, typename T, int MODE>
 struct LaneData
@@ -388,7 +299,7 @@ struct LaneData
   T    inv[dim][dim];
   T    JxW; // as loaded: JxW (curved) or det J (Cartesian); see jxw()
   T    U[dim], GU[dim][dim], T1[dim], UT[dim], oldg[NOLD];
-  T    h, d1, d2; // h: q-wise delta from U on the fly (GLS_DELTA_OTF)
+  T    h, d1, d2; // h: q-wise delta from U on the fly (delta_otf)
   bool active;
 };
 
@@ -396,7 +307,7 @@ struct LaneData
 // loads in flight (no data-dependent branch: the geometry type is per brick,
 // read in the prologue), so the whole set issues back to back and is waited
 // for once, at the q-point physics.
-template <int dim, int k, typename T, int MODE>
+template <int dim, int k, typename T, int MODE, int GEO>
 __device__ __forceinline__ void
 load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int ncell,
           bool general, int lcell, bool in_wave, int p, const int (&pa)[3],
@@ -418,43 +329,38 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
     lcell = 0;
   const int64_t cell = cell0 + lcell;
   const int64_t nqc  = a.n_cells * nq;
-#if GLS_INV_ZERO
+  if (GEO == GEO_CART) // (the Cartesian path reads the diagonal only)
 #pragma unroll
-  for (int i = 0; i < dim; ++i)
+    for (int i = 0; i < dim; ++i)
 #pragma unroll
-    for (int e = 0; e < dim; ++e)
-      r.inv[i][e] = 0;
-#endif
+      for (int e = 0; e < dim; ++e)
+        r.inv[i][e] = 0;
   // geometry (MatrixFree-style compressed: Cartesian per cell, else per q).
-  // (GLS_INV_ZERO 0: the off-diagonal inv entries are not written on
-  // Cartesian bricks: that path reads the diagonal only.)
   // loaded values stay untouched here: any arithmetic on them (the
   // quadrature weight, the inactive-lane mask) would make the compiler wait
   // for the loads at the prefetch point (an s_waitcnt vmcnt(0) in the middle
   // of the round); jxw() applies both at the point of use
-  if (GLS_BABL & 2)
+  if (GEO == GEO_ANY)
     {
+      // mixed meshes: one load per entry whatever the brick's type, only the
+      // address selected, and no branch around a load: a VALU write into a
+      // register that the other branch loads makes the waitcnt pass wait
+      // for every load issued before it -- the src gather among them --
+      // before this round's tables are even issued.  Cartesian bricks read
+      // their off-diagonal entries (never used) from distinct fixed
+      // addresses (identical addresses would be merged into one load and a
+      // copy, which waits for it).
+      const int64_t gq = qindex<dim, n>(cell, p, a.n_cells);
+      r.JxW            = *(general ? a.geo_gen + gq : a.geo_cart + dim * a.n_cells + cell);
 #pragma unroll
       for (int i = 0; i < dim; ++i)
 #pragma unroll
         for (int e = 0; e < dim; ++e)
-          r.inv[i][e] = i == e ? T(1) + T(0.01) * p : T(0);
-      r.JxW = T(1) + T(0.001) * lcell;
-#pragma unroll
-      for (int d = 0; d < dim; ++d)
-        {
-          r.U[d] = T(0.1) * d + T(0.01) * p, r.T1[d] = T(0.2), r.UT[d] = T(0.3);
-#pragma unroll
-          for (int e = 0; e < dim; ++e)
-            r.GU[d][e] = T(0.05) * (d + e);
-        }
-#pragma unroll
-      for (int i = 0; i < LaneData<dim, T, MODE>::NOLD; ++i)
-        r.oldg[i] = 0;
-      r.d1 = T(0.5), r.d2 = T(0.25), r.h = T(1);
-      return;
+          r.inv[i][e] = *(general ? a.geo_gen + (1 + i * dim + e) * nqc + gq :
+                          i == e  ? a.geo_cart + i * a.n_cells + cell :
+                                    a.geo_cart + (i * dim + e));
     }
-  if (general)
+  else if (general)
     {
       const int64_t gq = qindex<dim, n>(cell, p, a.n_cells);
       r.JxW            = a.geo_gen[gq];
@@ -497,7 +403,7 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
   for (int d = 0; d < dim; ++d)
     {
       r.U[d]  = tf[F::U + d];
-      r.T1[d] = tf[(GLS_NEWTON_T1 ? F::T1 : F::GP) + d]; // T1, or grad P*
+      r.T1[d] = tf[F::T1 + d];
       r.UT[d] = tf[F::UT + d];
 #pragma unroll
       for (int e = 0; e < dim; ++e)
@@ -551,48 +457,6 @@ to_packs(const T (&x)[nc], V (&v)[NP])
       v[kp][w] = kp * W + w < nc ? x[kp * W + w] : T(0);
 }
 
-// a shared node's final value from its summed partials (constraints, then
-// the fused relaxation), as k_shared_reduce_cls writes it
-template <typename T, int nc, bool R, typename Args>
-__device__ __forceinline__ void
-finish_shared(const Args &a, uint32_t packed, T (&r)[nc])
-{
-  const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
-#pragma unroll
-  for (int c = 0; c < nc; ++c)
-    if ((cm >> c) & 1)
-      r[c] = R ? T(0) : a.src[(size_t)node * nc + c];
-  if (!R && a.rb)
-#pragma unroll
-    for (int c = 0; c < nc; ++c)
-      {
-        const size_t j = (size_t)node * nc + c;
-        r[c]           = (a.rkeep ? a.src[j] : T(0)) + a.romega * (a.rd ? a.rd[j] : T(1)) *
-                                                       (a.rb[j] - r[c]);
-      }
-  store_node<T, nc>(a.dst, node, r);
-}
-
-#ifndef GLS_BRICK_OCC
-#define GLS_BRICK_OCC 3
-#endif
-#ifndef GLS_BRICK_OCC32
-#define GLS_BRICK_OCC32 3
-#endif
-#ifndef GLS_BRICK_OCC_CART
-#define GLS_BRICK_OCC_CART 4
-#endif
-
-// Geometry of a launch's bricks (build_bricks orders the Cartesian and the
-// curved bricks of each segment into separate runs): GEO_CART bricks hold
-// one diagonal J^{-1} and det J per cell, GEO_GEN bricks J^{-1} and JxW per
-// q point, GEO_ANY reads the type per brick (brick_geo bit 0).
-enum
-{
-  GEO_ANY  = 0,
-  GEO_CART = 1,
-  GEO_GEN  = 2
-};
 // The Cartesian FP64 3D Q2 vmult kernel (Newton, fixed point) fits 128
 // VGPRs (4 waves/SIMD) with its tables issued at the start of each round (in
 // flight during the evaluate sweeps) and an unpadded lattice (4 workgroups
@@ -606,33 +470,11 @@ struct BrickOcc
 {
   static constexpr bool cart4 = GEO == GEO_CART && sizeof(T) == 8 && dim == 3 && k == 2 &&
                                 MODE != MODE_RESIDUAL;
-  static constexpr int  waves = cart4 ? GLS_BRICK_OCC_CART :
-                                sizeof(T) == 4 ? GLS_BRICK_OCC32 :
-                                                 GLS_BRICK_OCC;
-  static constexpr bool late  = GLS_LATE_PREFETCH || cart4;
+  static constexpr int  waves = cart4 || sizeof(T) == 4 ? 4 : 3;
+  static constexpr bool late  = cart4; // tables issued at the start of each round
 };
-// PIPE: persistent pipelined variant.  The grid is at most the resident
-// workgroup slots; workgroup g runs the work units brick_begin + g + j *
-// gridDim.x (gridDim.x a multiple of 8 keeps every unit of a workgroup on
-// its XCD's run of bricks, build_bricks).  While a brick's cells run, the
-// next brick's lattice node ids and write targets (issued with the brick's
-// first round), its src gather and its first round's tables (both issued in
-// the brick's last round, behind the Dq^T sweeps, when the q-point tables
-// are dead) are in flight, so a brick switch costs the write-out and one
-// barrier instead of the dependent id -> gather round trips of a
-// workgroup's prologue.  The gather is an LDS-DMA
-// (global_load_lds_dwordx4, one 16-byte pack per lane) straight into a
-// second, unpadded src lattice: lattice node i of the next brick lands at
-// pack i, lane-linear, and occupies no registers while in flight.
-#ifndef GLS_FUSED_BUILD
-#define GLS_FUSED_BUILD 0
-#endif
-// GLS_PIPE_TAB: the next brick's first-round tables are prefetched in the
-// last round (1) or issued at the brick switch (0)
-#ifndef GLS_PIPE_TAB
-#define GLS_PIPE_TAB 1
-#endif
-template <int dim, int k, typename T, int MODE, bool PIPE = false, int GEO = GEO_ANY>
+
+template <int dim, int k, typename T, int MODE, int GEO = GEO_ANY>
 __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves))
   k_brick(BrickArgs<T, dim, k + 1> a)
 {
@@ -647,17 +489,16 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
   constexpr int WPB  = LDS::WPB;
   constexpr int WB   = LDS::WB;
   constexpr bool R   = MODE == MODE_RESIDUAL;
+  constexpr bool LATE = BrickOcc<dim, k, T, MODE, GEO>::late;
   static_assert(nq <= 64, "one cell must fit a wavefront");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int L      = a.L;  // lattice nodes (global order of brick_nodes)
   const int LP     = a.LP; // padded LDS lattice (bank-conflict-free x sweep)
   V        *s_src  = reinterpret_cast<V *>(smem);   // [NP][LP] brick src values
-  // PIPE: the next brick's lattice (LDS-DMA target; LP == L, unpadded)
-  V        *s_alt  = s_src + NP * LP;
-  V        *s_work = s_src + (PIPE ? 2 : 1) * NP * LP; // [WPB*CPW][WB]
+  V        *s_work = s_src + NP * LP;               // [WPB*CPW][WB]
   // the accumulator lattice is FP64 for both precisions: ds_add_f32 costs
-  // ~10 us per FP32 vmult on gfx950 (ablation GLS_ABL_NOATOMIC: 38.1 -> 28.2
+  // ~10 us per FP32 vmult on gfx950 (racy plain-add ablation: 38.1 -> 28.2
   // us), ds_add_f64 next to nothing (40.1 -> 39.7 us)
   double   *s_acc  = reinterpret_cast<double *>(s_work + WPB * CPW * WB); // [nc][LP]
   constexpr int RP = CoefRow<T, n>::RP;
@@ -672,15 +513,10 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
   // runtime brick shape, which the compiler would hoist into registers
   int      *s_org  = reinterpret_cast<int *>(s_tab + 4 * n * RP); // [ORG]
 
-  // 32-bit brick indices and cell / chunk offsets (uniform values: fewer
-  // SGPRs live across the persistent variant's brick loop)
-  int brick = (int)a.brick_begin + (int)blockIdx.x;
-  const int brick_end = (int)a.brick_end;
-  if (brick >= brick_end)
+  const int brick = (int)a.brick_begin + (int)blockIdx.x;
+  if (brick >= (int)a.brick_end)
     return;
-  const int bstride = PIPE ? (int)gridDim.x : 0;
-  const int t   = threadIdx.x;
-  GLS_STAMP(brick, 0);
+  const int t = threadIdx.x;
   if (t < n * RP)
     {
       const int  r = t / RP, j = t % RP;
@@ -724,15 +560,11 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
       pk[it]      = i < L ? bn[i] : 0u;
       tg[it]      = i < L ? bt[i] : 0u;
     }
-  uint32_t binfo   = a.brick_geo[brick];
-#ifndef GLS_FORCE_CART
-#define GLS_FORCE_CART 0
-#endif
-  constexpr bool LATE = BrickOcc<dim, k, T, MODE, GEO>::late;
-  bool     general = GEO == GEO_GEN || (GEO == GEO_ANY && !GLS_FORCE_CART && (binfo & 1u) != 0);
-  int      ncell   = (int)(binfo >> 8);
-  uint32_t cell0   = a.brick_cell0[brick];
-  uint32_t chunk0  = a.brick_chunk0[brick];
+  const uint32_t binfo   = a.brick_geo[brick];
+  const bool     general = GEO == GEO_GEN || (GEO == GEO_ANY && (binfo & 1u) != 0);
+  const int      ncell   = (int)(binfo >> 8);
+  const uint32_t cell0   = a.brick_cell0[brick];
+  const uint32_t chunk0  = a.brick_chunk0[brick];
 
   // ---- stage the brick's src values once per node (read_dof_values:
   // homogeneous constraints read as 0; the residual reads plain values).
@@ -755,10 +587,7 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
   // unmodified src of the exclusive nodes are loaded here, behind the
   // gather, instead of after the cell rounds (one memory round trip less at
   // the end of every brick; FP64 has no registers to spare for them)
-#ifndef GLS_RELAX_PREFETCH
-#define GLS_RELAX_PREFETCH 1
-#endif
-  constexpr bool PRE = GLS_RELAX_PREFETCH && sizeof(T) == 4 && !R;
+  constexpr bool PRE = sizeof(T) == 4 && !R;
   constexpr int  NPR = PRE ? NI : 1;
   T              xb[NPR][nc], xd[NPR][nc], xs[NPR][nc];
   if constexpr (PRE)
@@ -784,17 +613,16 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
         }
     }
   LaneData<dim, T, MODE> cur;
-  load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, wave * CPW + slot, in_wave, p, pa,
-                             cur);
+  load_lane<dim, k, T, MODE, GEO>(a, cell0, chunk0, ncell, general, wave * CPW + slot, in_wave, p,
+                                  pa, cur);
 #pragma unroll
   for (int it = 0; it < NI; ++it)
     {
       const int i = t + it * BLOCK;
       if (i >= L)
         break;
-      // PIPE runs the unpadded lattice (the LDS-DMA lands lane-linearly)
-      const int      iz = PIPE ? 0 : i / Lxy, iy = PIPE ? 0 : (i - iz * Lxy) / a.Lx;
-      const int      ip = PIPE ? i : (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
+      const int      iz = i / Lxy, iy = (i - iz * Lxy) / a.Lx;
+      const int      ip = (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
       const uint32_t cm = pk[it] >> 28;
 #pragma unroll
       for (int c = 0; c < nc; ++c)
@@ -810,81 +638,65 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
         s_src[kp * LP + ip] = v[kp];
     }
   __syncthreads();
-  GLS_STAMP(brick, 1);
 
   // the lane's tensor quadrature weight (Cartesian bricks: JxW = det J w_q)
   T wq_lane = a.sh.w[pa[0]] * a.sh.w[pa[1]];
   if (dim == 3)
     wq_lane *= a.sh.w[pa[2]];
-  for (;;) // the workgroup's bricks (one pass unless PIPE)
-  {
-  // PIPE: the thread index made opaque per brick (and again before the
-  // write-out) so that index arithmetic of the write-out / staging passes is
-  // recomputed there instead of being hoisted out of the brick loop and held
-  // in registers through the cell rounds
-  int tl = t;
-  if (PIPE)
-    asm volatile("" : "+v"(tl));
-  const int     next     = brick + bstride;
-  const bool    has_next = PIPE && next < brick_end;
-  constexpr int NIP      = PIPE ? NI : 1;
-  uint32_t      pk_n[NIP], tg_n[NIP];
-  uint32_t      binfo_n  = 0;
-  uint32_t      cell0_n = 0, chunk0_n = 0;
-  if (PIPE && has_next)
+  for (int base = 0; base < ncell; base += step)
     {
-      // the next brick's ids and write targets: in flight during this
-      // brick's rounds (the next brick's gather depends on them)
-      const uint32_t *bnn = a.brick_nodes + next * (int64_t)L;
-      const uint32_t *btn = a.brick_target + next * (int64_t)L;
-#pragma unroll
-      for (int it = 0; it < NIP; ++it)
-        {
-          const int i = tl + it * BLOCK;
-          pk_n[it]    = i < L ? bnn[i] : 0u;
-          tg_n[it]    = i < L ? btn[i] : 0u;
-        }
-      binfo_n  = a.brick_geo[next];
-      cell0_n  = a.brick_cell0[next];
-      chunk0_n = a.brick_chunk0[next];
-    }
-  for (int base = 0; base < ((GLS_BABL & 1) ? 0 : ncell); base += step)
-    {
-      // GLS_LATE_PREFETCH: a round's geometry and tables are issued at the
-      // start of that round (in flight during its evaluate sweeps) instead
-      // of before the previous round's integrate sweeps: fewer registers
-      // live across the integrate sweeps
+      // LATE: a round's geometry and tables are issued at the start of that
+      // round (in flight during its evaluate sweeps) instead of before the
+      // previous round's integrate sweeps: fewer registers live across the
+      // integrate sweeps
       if (LATE && base > 0)
-        load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, base + wave * CPW + slot,
-                                   in_wave, p, pa, cur);
+        load_lane<dim, k, T, MODE, GEO>(a, cell0, chunk0, ncell, general,
+                                        base + wave * CPW + slot, in_wave, p, pa, cur);
 
       // the lane's lattice node this round (inactive lanes: the first cell's)
       const int li = (cur.active ? s_org[base + wave * CPW + slot] : 0) + lpa;
-      // ---- evaluate: x sweep straight from the src lattice, then y (, z)
-      if (!(GLS_BABL & 4))
-      {
-        const int lb = li - pa[0];
-        if (in_wave)
+      // ---- evaluate: x sweep straight from the src lattice, then y (, z).
+      // Each sweep reads its coefficient row once for every pack and issues
+      // every pack's reads before the first store (a store could alias the
+      // tables or the next pack's reads: interleaved, each pack would wait
+      // one LDS round trip of its own)
+      if (in_wave)
+        {
+          T c[n];
+          coefs<n>(sS, pa[0], c);
+          V r[NP];
 #pragma unroll
           for (int kp = 0; kp < NP; ++kp)
-            A[kp * BL::KS + q] = contract_v<n>(s_src + kp * LP, sS, pa[0], lb, 1);
-      }
+            r[kp] = contract_c<n>(s_src + kp * LP, c, li - pa[0], 1);
+#pragma unroll
+          for (int kp = 0; kp < NP; ++kp)
+            A[kp * BL::KS + q] = r[kp];
+        }
       wave_sync();
       V *in = A, *out = B;
 #pragma unroll
-      for (int ax = 1; ax < ((GLS_BABL & 4) ? 1 : dim); ++ax)
+      for (int ax = 1; ax < dim; ++ax)
         {
           if (in_wave)
+            {
+              T c[n];
+              coefs<n>(sS, pa[ax], c);
+              V r[NP];
 #pragma unroll
-            for (int kp = 0; kp < NP; ++kp)
-              out[kp * BL::KS + q] =
-                contract_v<n>(in + kp * BL::KS, sS, pa[ax], q - pa[ax] * st[ax], st[ax]);
+              for (int kp = 0; kp < NP; ++kp)
+                r[kp] = contract_c<n>(in + kp * BL::KS, c, q - pa[ax] * st[ax], st[ax]);
+#pragma unroll
+              for (int kp = 0; kp < NP; ++kp)
+                out[kp * BL::KS + q] = r[kp];
+            }
           wave_sync();
           V *tmp = in;
           in     = out;
           out    = tmp;
         }
-      // values and reference-space gradients (collocation derivative)
+      // values and reference-space gradients (collocation derivative);
+      // left-over lanes stay out of the reads (they would only add bank
+      // conflicts in their ds_read_b128 lane groups)
       T val[nc], gref[nc][dim];
 #pragma unroll
       for (int c = 0; c < nc; ++c)
@@ -894,47 +706,27 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
           for (int ax = 0; ax < dim; ++ax)
             gref[c][ax] = T(0);
         }
-      // left-over lanes stay out of the reads (they would only add bank
-      // conflicts in their ds_read_b128 lane groups)
-      if (GLS_BABL & 4)
-        {
+      if (in_wave)
 #pragma unroll
-          for (int kp = 0; kp < NP; ++kp)
-            {
-              const V v = s_src[kp * LP + li];
+        for (int kp = 0; kp < NP; ++kp)
+          {
+            const V v = in[kp * BL::KS + q];
+            V       g[dim];
 #pragma unroll
-              for (int w = 0; w < W; ++w)
-                if (kp * W + w < nc)
-                  {
-                    val[kp * W + w] = v[w];
+            for (int ax = 0; ax < dim; ++ax)
+              g[ax] = contract_v<n>(in + kp * BL::KS, sD, pa[ax], q - pa[ax] * st[ax], st[ax]);
 #pragma unroll
-                    for (int ax = 0; ax < dim; ++ax)
-                      gref[kp * W + w][ax] = v[w] * sS[ax];
-                  }
-            }
-        }
-      else if (in_wave)
+            for (int w = 0; w < W; ++w)
+              if (kp * W + w < nc)
+                {
+                  val[kp * W + w] = v[w];
 #pragma unroll
-      for (int kp = 0; kp < NP; ++kp)
-        {
-          const V v = in[kp * BL::KS + q];
-          V       g[dim];
-#pragma unroll
-          for (int ax = 0; ax < dim; ++ax)
-            g[ax] = contract_v<n>(in + kp * BL::KS, sD, pa[ax], q - pa[ax] * st[ax], st[ax]);
-#pragma unroll
-          for (int w = 0; w < W; ++w)
-            if (kp * W + w < nc)
-              {
-                val[kp * W + w] = v[w];
-#pragma unroll
-                for (int ax = 0; ax < dim; ++ax)
-                  gref[kp * W + w][ax] = g[ax][w];
-              }
-        }
+                  for (int ax = 0; ax < dim; ++ax)
+                    gref[kp * W + w][ax] = g[ax][w];
+                }
+          }
       wave_sync();
 
-      GLS_STAMP(brick, base == 0 ? 2 : 4);
       // ---- q-point physics (do_vmult_cell)
       // real-space gradients J^{-T} grad_ref: Cartesian bricks (wave-uniform
       // branch) have a diagonal J^{-1}
@@ -978,23 +770,9 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
 #pragma unroll
           for (int d = 0; d < dim; ++d)
             u2 += cur.U[d] * cur.U[d];
-          if (GLS_FAST_DELTA)
-            delta_qwise_fast(u2, cur.h, a.nu, a.stau, d1, d2);
-          else
-            delta_qwise(u2, cur.h, a.nu, a.stau, d1, d2);
+          delta_qwise_fast(u2, cur.h, a.nu, a.stau, d1, d2);
         }
-      if constexpr ((GLS_BABL & 8) != 0)
-        {
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-            {
-              vr[c] = val[c] * cur.U[c % dim] + cur.d1;
-#pragma unroll
-              for (int e = 0; e < dim; ++e)
-                gr[c][e] = (c < dim ? gu[c][e] : gp[e]) * cur.GU[c % dim][e] + cur.d2 * cur.T1[e] + cur.UT[e];
-            }
-        }
-      else if constexpr (MODE == MODE_NEWTON && GLS_NEWTON_T1)
+      if constexpr (MODE == MODE_NEWTON)
         qpoint_newton_t1<dim, T>(val, val[dim], gu, gp, cur.U, cur.GU, cur.T1, d1, d2, a.nu,
                                  a.w0, a.td, vr, gr);
       else
@@ -1043,20 +821,8 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
       // fused with the accumulation into the brick lattice
       V wv[NP];
       to_packs<V, T, nc, NP, W>(wq, wv);
-      if (GLS_BABL & 4)
-        {
 #pragma unroll
-          for (int kp = 0; kp < NP; ++kp)
-#pragma unroll
-            for (int ax = 0; ax < dim; ++ax)
-              {
-                V g0[NP];
-                to_packs<V, T, nc, NP, W>(ghat[ax], g0);
-                wv[kp] += g0[kp];
-              }
-        }
-#pragma unroll
-      for (int ax0 = 0; ax0 < ((GLS_BABL & 4) ? 0 : dim); ax0 += 2)
+      for (int ax0 = 0; ax0 < dim; ax0 += 2)
         {
           if (in_wave)
             {
@@ -1077,17 +843,17 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
           wave_sync();
           if (in_wave)
 #pragma unroll
-          for (int kp = 0; kp < NP; ++kp)
-            {
-              wv[kp] += contract_v<n>(A + kp * BL::KS, sDT, pa[ax0], q - pa[ax0] * st[ax0],
-                                            st[ax0]);
-              if (ax0 + 1 < dim)
-                {
-                  const int ax1 = (ax0 + 1) % dim;
-                  wv[kp] += contract_v<n>(B + kp * BL::KS, sDT, pa[ax1],
-                                                q - pa[ax1] * st[ax1], st[ax1]);
-                }
-            }
+            for (int kp = 0; kp < NP; ++kp)
+              {
+                wv[kp] += contract_v<n>(A + kp * BL::KS, sDT, pa[ax0], q - pa[ax0] * st[ax0],
+                                        st[ax0]);
+                if (ax0 + 1 < dim)
+                  {
+                    const int ax1 = (ax0 + 1) % dim;
+                    wv[kp] += contract_v<n>(B + kp * BL::KS, sDT, pa[ax1],
+                                            q - pa[ax1] * st[ax1], st[ax1]);
+                  }
+              }
           wave_sync();
         }
       if (in_wave)
@@ -1097,53 +863,29 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
       // the next round's geometry and tables: issued here (few registers
       // live), in flight during the S^T sweeps and the next evaluate (this
       // round's lattice position is kept: the prefetch overwrites cur)
-      GLS_STAMP(brick, base == 0 ? 3 : 5);
       const int  li_now     = li;
       const bool active_now = cur.active;
       if (!LATE && base + step < ncell)
-        load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, base + step + wave * CPW + slot,
-                                   in_wave, p, pa, cur);
-      else if (!LATE && PIPE && GLS_PIPE_TAB && has_next)
-        load_lane<dim, k, T, MODE>(a, cell0_n, chunk0_n, (int)(binfo_n >> 8), (binfo_n & 1u) != 0,
-                                   wave * CPW + slot, in_wave, p, pa, cur);
-      if constexpr (PIPE && nc * sizeof(T) % 16 == 0)
-      if (has_next && base + step >= ncell)
-        {
-          // last round: the next brick's src gather (read_dof_values of its
-          // lattice) by LDS-DMA into the other lattice, one 16-byte pack per
-          // lane and instruction; lattice positions outside the next brick's
-          // cells (UNUSED_NODE) read node 0 (never read back)
-#pragma unroll
-          for (int it = 0; it < NIP; ++it)
-            {
-              const int i = tl + it * BLOCK;
-              if (i < L)
-                {
-                  uint32_t node = pk_n[it] & NODE_MASK;
-                  if (node == UNUSED_NODE)
-                    node = 0;
-                  const V *g = reinterpret_cast<const V *>(a.src) + (size_t)node * NP;
-#pragma unroll
-                  for (int kp = 0; kp < NP; ++kp)
-                    __builtin_amdgcn_global_load_lds(
-                      (const void *)(g + kp),
-                      (__attribute__((address_space(3))) void *)(s_alt + kp * LP + it * BLOCK +
-                                                                 wave * 64),
-                      16, 0, 0);
-                }
-            }
-        }
+        load_lane<dim, k, T, MODE, GEO>(a, cell0, chunk0, ncell, general,
+                                        base + step + wave * CPW + slot, in_wave, p, pa, cur);
       wave_sync();
       in  = A;
       out = B;
 #pragma unroll
-      for (int ax = dim - 1; ax >= ((GLS_BABL & 4) ? dim : 1); --ax)
+      for (int ax = dim - 1; ax >= 1; --ax)
         {
           if (in_wave)
+            {
+              T c[n];
+              coefs<n>(sST, pa[ax], c);
+              V r[NP];
 #pragma unroll
-            for (int kp = 0; kp < NP; ++kp)
-              out[kp * BL::KS + q] =
-                contract_v<n>(in + kp * BL::KS, sST, pa[ax], q - pa[ax] * st[ax], st[ax]);
+              for (int kp = 0; kp < NP; ++kp)
+                r[kp] = contract_c<n>(in + kp * BL::KS, c, q - pa[ax] * st[ax], st[ax]);
+#pragma unroll
+              for (int kp = 0; kp < NP; ++kp)
+                out[kp * BL::KS + q] = r[kp];
+            }
           wave_sync();
           V *tmp = in;
           in     = out;
@@ -1155,245 +897,70 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
 #pragma unroll
         for (int kp = 0; kp < NP; ++kp)
           {
-            const V r = (GLS_BABL & 4) ? wv[kp] : contract_c<n>(in + kp * BL::KS, cx, q - pa[0], 1);
+            const V r = contract_c<n>(in + kp * BL::KS, cx, q - pa[0], 1);
 #pragma unroll
             for (int w = 0; w < W; ++w)
               if (kp * W + w < nc)
-#ifdef GLS_ABL_NOATOMIC // diagnostic timing build only: racy plain adds
-                s_acc[(kp * W + w) * LP + li_now] += (double)r[w];
-#else
                 lds_add(s_acc + (kp * W + w) * LP + li_now, (double)r[w]);
-#endif
           }
       wave_sync();
     }
-  if constexpr (PIPE)
-    // a bare barrier: __syncthreads() would also wait for the next brick's
-    // LDS-DMA gather (a pending LDS write on the VM counter)
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else
-    __syncthreads();
-  GLS_STAMP(brick, 6);
+  __syncthreads();
 
-  if (PIPE)
-    asm volatile("" : "+v"(tl));
   // ---- write out: exclusive nodes -> dst, boundary nodes -> partials
-  // the fused last-arriver reduction (measured slower) is only
-  // compiled into GLS_FUSED_BUILD=1 diagnostic builds
-  constexpr bool FUSE = GLS_FUSED_BUILD && nc * sizeof(T) % 16 == 0; // 3D: 4 comps per slot
-  const __amdgpu_buffer_rsrc_t prs =
-    __builtin_amdgcn_make_buffer_rsrc(a.partial, 0, (int)a.partial_bytes, 0x00020000);
 #pragma unroll
   for (int it = 0; it < NI; ++it)
     {
-      const int i = tl + it * BLOCK;
+      const int i = t + it * BLOCK;
       if (i >= L)
         break;
-      // PIPE runs the unpadded lattice (the LDS-DMA lands lane-linearly)
-      const int      iz = PIPE ? 0 : i / Lxy, iy = PIPE ? 0 : (i - iz * Lxy) / a.Lx;
-      const int      ip = PIPE ? i : (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
+      const int      iz  = i / Lxy, iy = (i - iz * Lxy) / a.Lx;
+      const int      ip  = (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
       const uint32_t tgt = tg[it];
-      double         acc[nc];
-#pragma unroll
-      for (int c = 0; c < nc; ++c)
-        {
-          acc[c] = s_acc[c * LP + ip];
-          if (PIPE)
-            s_acc[c * LP + ip] = 0.0; // the next brick's accumulator
-        }
       if (tgt == UNUSED_NODE)
         continue;
+      double acc[nc];
+#pragma unroll
+      for (int c = 0; c < nc; ++c)
+        acc[c] = s_acc[c * LP + ip];
+      T r[nc];
       if (tgt & SHARED_BIT)
         {
-          T r[nc];
 #pragma unroll
           for (int c = 0; c < nc; ++c)
             r[c] = (T)(R ? -acc[c] : acc[c]);
-          bool done = false;
-          if constexpr (FUSE)
-            if (a.counters)
-              {
-                const uint32_t slot = tgt & ~SHARED_BIT;
-                if (a.rc.mult[slot_class(a.rc, slot)] == 1)
-                  finish_shared<T, nc, R>(a, pk[it], r); // the node's only brick
-                else
-                  store_slot_wt<T, nc>(prs, slot, r);
-                done = true;
-              }
-          if (!done)
-            store_node<T, nc>(a.partial, tgt & ~SHARED_BIT, r);
+          store_node<T, nc>(a.partial, tgt & ~SHARED_BIT, r);
+          continue;
         }
-      else
-        {
-          const uint32_t cm = pk[it] >> 28;
-          T              r[nc];
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-            {
-              r[c] = (T)(R ? -acc[c] : acc[c]);
-              if ((cm >> c) & 1)
-                r[c] = R ? T(0) : (PRE ? xs[PRE ? it : 0][c] : a.src[(size_t)tgt * nc + c]);
-            }
-          if constexpr (PRE)
-            {
-              if (a.rb)
-#pragma unroll
-                for (int c = 0; c < nc; ++c)
-                  {
-                    const T base = a.rkeep ? xs[it][c] : T(0);
-                    r[c]         = base + a.romega * xd[it][c] * (xb[it][c] - r[c]);
-                  }
-            }
-          else if constexpr (!R)
-            if (a.rb)
-#pragma unroll
-              for (int c = 0; c < nc; ++c)
-                {
-                  const size_t j = (size_t)tgt * nc + c;
-                  const T  base  = a.rkeep ? a.src[j] : T(0);
-                  r[c]           = base + a.romega * (a.rd ? a.rd[j] : T(1)) * (a.rb[j] - r[c]);
-                }
-          store_node<T, nc>(a.dst, tgt, r);
-        }
-    }
-  if constexpr (FUSE)
-  if (a.counters)
-    {
-      // every wave's slot stores have reached memory before any arrival of
-      // this brick is counted
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-#pragma unroll
-      for (int it = 0; it < NI; ++it)
-        {
-          const int i = tl + it * BLOCK;
-          if (i >= L)
-            break;
-          const uint32_t tgt = tg[it];
-          if (tgt == UNUSED_NODE || !(tgt & SHARED_BIT))
-            continue;
-          const uint32_t slot = tgt & ~SHARED_BIT;
-          const int      kc   = slot_class(a.rc, slot);
-          const uint32_t m    = a.rc.mult[kc];
-          if (m == 1)
-            continue;
-          const uint32_t sn  = a.rc.first[kc] + (slot - a.rc.slot0[kc]) / m;
-          const uint32_t b0s = a.rc.slot0[kc] + (sn - a.rc.first[kc]) * m;
-          const uint32_t old = __hip_atomic_fetch_add(a.counters + sn, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-          if (old != m - 1)
-            continue;
-          // last arrival: the node's slots in slot order, summed as
-          // k_shared_reduce_cls sums them
-          T        sum[nc] = {};
-          uint32_t j       = 0;
-          for (; j + 4 <= m; j += 4)
-            {
-              T x0[nc], x1[nc], x2[nc], x3[nc];
-              load_slot_wt<T, nc>(prs, b0s + j, x0);
-              load_slot_wt<T, nc>(prs, b0s + j + 1, x1);
-              load_slot_wt<T, nc>(prs, b0s + j + 2, x2);
-              load_slot_wt<T, nc>(prs, b0s + j + 3, x3);
-#pragma unroll
-              for (int c = 0; c < nc; ++c)
-                sum[c] += (x0[c] + x1[c]) + (x2[c] + x3[c]);
-            }
-          if (j + 2 <= m)
-            {
-              T x0[nc], x1[nc];
-              load_slot_wt<T, nc>(prs, b0s + j, x0);
-              load_slot_wt<T, nc>(prs, b0s + j + 1, x1);
-#pragma unroll
-              for (int c = 0; c < nc; ++c)
-                sum[c] += x0[c] + x1[c];
-              j += 2;
-            }
-          if (j < m)
-            {
-              T x0[nc];
-              load_slot_wt<T, nc>(prs, b0s + j, x0);
-#pragma unroll
-              for (int c = 0; c < nc; ++c)
-                sum[c] += x0[c];
-            }
-          finish_shared<T, nc, R>(a, pk[it], sum);
-          __hip_atomic_store(a.counters + sn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-  GLS_STAMP(brick, 7);
-  if (!has_next)
-    break;
-  // ---- switch to the next brick: its lattice has landed in s_alt (the
-  // accumulator was zeroed by the write-out), its ids / targets / scalars
-  // come from this brick's prefetch
-  brick   = next;
-  binfo   = binfo_n;
-  general = GEO == GEO_GEN || (GEO == GEO_ANY && !GLS_FORCE_CART && (binfo & 1u) != 0);
-  ncell   = (int)(binfo >> 8);
-  cell0   = cell0_n;
-  chunk0  = chunk0_n;
-#pragma unroll
-  for (int it = 0; it < NIP; ++it)
-    {
-      pk[it] = pk_n[it];
-      tg[it] = tg_n[it];
-    }
-  // the DMA (and the next round's tables issued before it) complete
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  {
-    V *tmp = s_src;
-    s_src  = s_alt;
-    s_alt  = tmp;
-  }
-#pragma unroll
-  for (int it = 0; it < NIP; ++it)
-    {
-      const int i = tl + it * BLOCK;
-      if (i >= L)
-        break;
       const uint32_t cm = pk[it] >> 28;
+#pragma unroll
+      for (int c = 0; c < nc; ++c)
+        {
+          r[c] = (T)(R ? -acc[c] : acc[c]);
+          if ((cm >> c) & 1)
+            r[c] = R ? T(0) : (PRE ? xs[PRE ? it : 0][c] : a.src[(size_t)tgt * nc + c]);
+        }
       if constexpr (PRE)
         {
-          // the fused relaxation's operands of the exclusive nodes: the raw
-          // src values from the landed lattice, b and d from memory
-          const bool excl = tg[it] != UNUSED_NODE && !(tg[it] & SHARED_BIT);
+          if (a.rb)
 #pragma unroll
-          for (int kp = 0; kp < NP; ++kp)
-            {
-              const V v = s_src[kp * LP + i];
-#pragma unroll
-              for (int w = 0; w < W; ++w)
-                if (kp * W + w < nc)
-                  xs[it][kp * W + w] = v[w];
-            }
+            for (int c = 0; c < nc; ++c)
+              {
+                const T base = a.rkeep ? xs[it][c] : T(0);
+                r[c]         = base + a.romega * xd[it][c] * (xb[it][c] - r[c]);
+              }
+        }
+      else if constexpr (!R)
+        if (a.rb)
 #pragma unroll
           for (int c = 0; c < nc; ++c)
             {
-              xb[it][c] = T(0);
-              xd[it][c] = T(1);
+              const size_t j    = (size_t)tgt * nc + c;
+              const T      base = a.rkeep ? a.src[j] : T(0);
+              r[c]              = base + a.romega * (a.rd ? a.rd[j] : T(1)) * (a.rb[j] - r[c]);
             }
-          if (excl && a.rb)
-            {
-              load_node<T, nc>(a.rb, tg[it], xb[it]);
-              if (a.rd)
-                load_node<T, nc>(a.rd, tg[it], xd[it]);
-            }
-        }
-      // homogeneous constraints read as 0 (read_dof_values)
-      if (!R && cm)
-        {
-          T *sv = reinterpret_cast<T *>(s_src);
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-            if ((cm >> c) & 1)
-              sv[((c / W) * LP + i) * W + c % W] = T(0);
-        }
+      store_node<T, nc>(a.dst, tgt, r);
     }
-  if (LATE || !GLS_PIPE_TAB)
-    load_lane<dim, k, T, MODE>(a, cell0, chunk0, ncell, general, wave * CPW + slot, in_wave, p,
-                               pa, cur);
-  __syncthreads();
-  } // brick loop
 }
 
 // Sum the per-brick partials of every brick-boundary node (one contiguous

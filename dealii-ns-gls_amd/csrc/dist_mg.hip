@@ -529,7 +529,7 @@ gls_dist_mg_create(const glsDistMGDesc *d, const glsDist *levels, glsDistMG *out
         }
       m->prec = ops[0]->prec;
       m->nc   = ops[0]->dim + 1;
-      HIP_THROW(hipSetDevice(ops[0]->device));
+      gls::DeviceScope dev(ops[0]->device); // the caller's device is restored
       // transfers / relaxation kernels over the rank-local level operators
       // (the coarse solve of this glsMG is not used)
       glsMGDesc td          = d->mg;

@@ -147,10 +147,6 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
       int z = 1;
       while (bx * by * z * 2 <= 8 && bz % (z * 2) == 0)
         z *= 2;
-      // variant builds (GLS_BRICK_MAXZ > 1): GLS_BRICK_BZ layers per brick
-      if (const char *e = getenv("GLS_BRICK_BZ"))
-        while (z * 2 <= std::min(std::atoi(e), GLS_BRICK_MAXZ) && bz % (z * 2) == 0)
-          z *= 2;
       bz = z;
     }
   const int64_t cpb = (int64_t)bx * by * bz;
@@ -159,8 +155,8 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
   const int Lx = k * bx + 1, Ly = k * by + 1, Lz = dim == 3 ? k * bz + 1 : 1;
   const int L  = Lx * Ly * Lz;
   const int side_max = k * (dim == 3 ? 4 : 8) + 1;
-  const int lmax     = dim == 3 ? side_max * side_max * (k * GLS_BRICK_MAXZ + 1) : side_max * side_max;
-  if (L > lmax || lmax > 729 || (dim == 3 && (bx > 4 || by > 4 || bx * by * bz > 16 * GLS_BRICK_MAXZ)) ||
+  const int lmax     = dim == 3 ? side_max * side_max * (k + 1) : side_max * side_max;
+  if (L > lmax || lmax > 729 || (dim == 3 && (bx > 4 || by > 4 || bx * by * bz > 16)) ||
       (dim == 2 && (bx > 8 || by > 8)))
     return; // lattice does not fit the brick kernel's LDS: per-cell path
   const int64_t nb_full = d->n_cells / cpb;
@@ -374,10 +370,6 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
   upload((void **)&op->d_shared_off, off);
   HIP_THROW(hipMalloc(&op->d_partial,
                       std::max<size_t>(1, (size_t)slot * (dim + 1) * op->tsize())));
-  // arrival counters of the fused reduction (k_brick, BrickArgs::counters):
-  // zero between launches, every completing brick resets its nodes'
-  HIP_THROW(hipMalloc((void **)&op->d_counters, std::max<size_t>(1, shared_nodes.size() * 4)));
-  HIP_THROW(hipMemset(op->d_counters, 0, std::max<size_t>(1, shared_nodes.size() * 4)));
 }
 
 // storage field (kernels.h Fields) of canonical host field f: the host
@@ -658,67 +650,21 @@ struct Impl
     HIP_THROW(hipGetLastError());
   }
 
-#ifndef GLS_FUSED_REDUCE_DEFAULT
-#define GLS_FUSED_REDUCE_DEFAULT 0
-#endif
-#ifndef GLS_BRICK_PIPE_DEFAULT
-#define GLS_BRICK_PIPE_DEFAULT 0
-#endif
-#ifndef GLS_PIPE_BUILD
-#define GLS_PIPE_BUILD 0
-#endif
-  // resident workgroup slots of a kernel on the current device (occupancy x
-  // CUs), queried once per (kernel, LDS bytes): the query costs several
-  // microseconds of host time, which short coarse-level launches cannot hide
-  template <typename K>
-  static int64_t
-  resident_slots(K kernel, size_t lds)
-  {
-    static std::vector<std::pair<std::pair<const void *, size_t>, int64_t>> cache;
-    const auto key = std::make_pair((const void *)kernel, lds);
-    int        dev = 0;
-    HIP_THROW(hipGetDevice(&dev));
-    for (const auto &e : cache)
-      if (e.first == key)
-        return e.second;
-    int n_cu = 0, per_cu = 0;
-    HIP_THROW(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    HIP_THROW(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, BLOCK, lds));
-    const int64_t slots = (int64_t)std::max(1, per_cu) * std::max(1, n_cu);
-    cache.emplace_back(key, slots);
-    return slots;
-  }
-
-  // the brick kernel over n_units work units of one geometry type: one
-  // workgroup per unit, or (GLS_PIPE_BUILD diagnostic builds with
-  // GLS_BRICK_PIPE=1, more units than resident slots) the persistent
-  // pipelined variant on the resident slots rounded down to a multiple of 8
+  // the brick kernel over n_units work units of one geometry type, one
+  // workgroup per unit
   template <int M>
   static void
-  launch_brick(int64_t n_units, size_t lds, bool pipe, int geo, hipStream_t s,
-               const BrickArgs<T, dim, n> &a)
+  launch_brick(int64_t n_units, size_t lds, int geo, hipStream_t s, const BrickArgs<T, dim, n> &a)
   {
-#if GLS_PIPE_BUILD
-    if (pipe)
-      {
-        const int64_t slots = resident_slots(k_brick<dim, k, T, M, true>, lds) / 8 * 8;
-        if (slots >= 8 && n_units > slots)
-          {
-            hipLaunchKernelGGL((k_brick<dim, k, T, M, true>), dim3((unsigned)slots),
-                               dim3(BLOCK), lds, s, a);
-            return;
-          }
-      }
-#endif
     if (geo == GEO_GEN)
-      hipLaunchKernelGGL((k_brick<dim, k, T, M, false, GEO_GEN>), dim3((unsigned)n_units),
-                         dim3(BLOCK), lds, s, a);
+      hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_GEN>), dim3((unsigned)n_units), dim3(BLOCK),
+                         lds, s, a);
     else if (geo == GEO_CART)
-      hipLaunchKernelGGL((k_brick<dim, k, T, M, false, GEO_CART>), dim3((unsigned)n_units),
-                         dim3(BLOCK), lds, s, a);
+      hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_CART>), dim3((unsigned)n_units), dim3(BLOCK),
+                         lds, s, a);
     else
-      hipLaunchKernelGGL((k_brick<dim, k, T, M, false, GEO_ANY>), dim3((unsigned)n_units),
-                         dim3(BLOCK), lds, s, a);
+      hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_ANY>), dim3((unsigned)n_units), dim3(BLOCK),
+                         lds, s, a);
   }
 
   // brick kernel over work units [b0, b1) (what & BRICK_RUN) and the
@@ -760,21 +706,13 @@ struct Impl
         // padded LDS lattice: 3D Q2 bricks of 4x4 cells in x, y use strides
         // 11, 12 (ds_read_b128 conflict-free x sweep, exhaustive search);
         // the FP64 Cartesian kernel takes the unpadded lattice (4 workgroups
-        // per CU in LDS), and so does the persistent variant (its LDS-DMA
-        // lands lane-linearly, two lattices in LDS)
-        static const bool pad32 = !getenv("GLS_PAD32") || std::atoi(getenv("GLS_PAD32")) != 0;
-        static const bool pad64 = getenv("GLS_PAD64") && std::atoi(getenv("GLS_PAD64")) != 0;
-        static const int pipe_env = getenv("GLS_BRICK_PIPE") ?
-                                      std::atoi(getenv("GLS_BRICK_PIPE")) :
-                                      GLS_BRICK_PIPE_DEFAULT;
-        const bool pipe = GLS_PIPE_BUILD && pipe_env != 0 && (dim + 1) * sizeof(T) % 16 == 0 &&
-                          b1 - b0 > 0 && (what & BRICK_RUN);
+        // per CU in LDS)
         auto set_lattice = [&](bool general) {
           // (the 4-wave Cartesian FP64 kernels: BrickOcc<...>::cart4)
           const bool cart4 = !general && sizeof(T) == 8 && mode != MODE_RESIDUAL && dim == 3 &&
                              k == 2;
-          const bool pad   = !pipe && dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9 &&
-                           op->L == 243 && (sizeof(T) == 8 ? (!cart4 || pad64) : pad32);
+          const bool pad   = dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9 && op->L == 243 &&
+                           (sizeof(T) == 8 ? !cart4 : true);
           a.PLx = pad ? 11 : op->Lx;
           a.PLy = pad ? 12 : op->Ly;
           a.LP  = a.PLx * a.PLy * (op->L / (op->Lx * op->Ly));
@@ -789,24 +727,7 @@ struct Impl
         a.have_prev     = op->have_prev ? 1 : 0;
         a.have_old_grad = (op->have_old_grad && op->prm.theta != 1.0) ? 1 : 0;
         a.sh            = make_shape<T, n>(op->basis);
-        // fused shared-node reduction: a whole single-domain vmult whose
-        // shared nodes all have at least one brick (GLS_FUSED_REDUCE=0: the
-        // separate k_shared_reduce_cls launch)
-        static const int fuse_env = getenv("GLS_FUSED_REDUCE") ? std::atoi(getenv("GLS_FUSED_REDUCE"))
-                                                               : GLS_FUSED_REDUCE_DEFAULT;
-        const size_t pbytes = (size_t)op->n_slots * (dim + 1) * sizeof(T);
-        const ReduceClasses &rc0 = op->reduce_classes;
-        const bool fused = GLS_FUSED_BUILD && fuse_env != 0 && ((dim + 1) * sizeof(T)) % 16 == 0 &&
-                           what == (BRICK_RUN | BRICK_REDUCE) && b0 == 0 &&
-                           b1 == op->n_bricks && op->n_owned_nodes == op->n_nodes &&
-                           rc0.n > 0 && rc0.mult[0] > 0 && pbytes < ((size_t)1 << 31) &&
-                           op->d_counters;
-        a.counters      = fused ? op->d_counters : nullptr;
-        a.partial_bytes = (uint32_t)std::min<size_t>(pbytes, ((size_t)1 << 31) - 1);
-        a.rc            = rc0;
-        if (fused)
-          what = BRICK_RUN;
-        if ((what & BRICK_RUN) && b1 > b0 && mode == MODE_NEWTON && GLS_NEWTON_T1)
+        if ((what & BRICK_RUN) && b1 > b0 && mode == MODE_NEWTON)
           {
             // T1 (Fields::T1) from the current tables and time weights
             if (!op->t1_valid || op->t1_w0 != op->prm.w0 || op->t1_td != a.td)
@@ -824,18 +745,17 @@ struct Impl
           }
         if ((what & BRICK_RUN) && b1 > b0)
           {
-            const bool pl  = pipe && !fused;
-            const int  geo = op->n_curved_bricks == 0            ? GEO_CART :
-                             op->n_curved_bricks == op->n_bricks ? GEO_GEN :
-                                                                   GEO_ANY;
+            const int geo = op->n_curved_bricks == 0            ? GEO_CART :
+                            op->n_curved_bricks == op->n_bricks ? GEO_GEN :
+                                                                  GEO_ANY;
             set_lattice(geo != GEO_CART);
-            const size_t lds = BrickLDS<dim, k, T>::bytes(a.LP, pl);
+            const size_t lds = BrickLDS<dim, k, T>::bytes(a.LP);
             if (mode == MODE_NEWTON)
-              launch_brick<MODE_NEWTON>(b1 - b0, lds, pl, geo, s, a);
+              launch_brick<MODE_NEWTON>(b1 - b0, lds, geo, s, a);
             else if (mode == MODE_FIXED)
-              launch_brick<MODE_FIXED>(b1 - b0, lds, pl, geo, s, a);
+              launch_brick<MODE_FIXED>(b1 - b0, lds, geo, s, a);
             else
-              launch_brick<MODE_RESIDUAL>(b1 - b0, lds, pl, geo, s, a);
+              launch_brick<MODE_RESIDUAL>(b1 - b0, lds, geo, s, a);
             HIP_THROW(hipGetLastError());
           }
         if ((what & BRICK_REDUCE) && op->n_shared > 0)
@@ -1700,8 +1620,7 @@ gls_op_destroy(glsOp op)
                   op->d_brick_target, op->d_shared_nodes, op->d_shared_off,
                   op->d_partial,      op->d_bgeo_cart,    op->d_bgeo_gen,
                   op->d_brick_geo,    op->d_brick_cell0,  op->d_brick_chunk0, op->d_tab_cbase,
-                  op->d_node_cmask,   op->d_inhom,        op->gmres_ws,
-                  op->d_counters};
+                  op->d_node_cmask,   op->d_inhom,        op->gmres_ws};
   for (void *b : bufs)
     if (b)
       (void)hipFree(b);
@@ -2480,8 +2399,8 @@ gls_op_vmult_bytes(glsOp op)
   // with n_tab the table values per q this build streams, in whole 16-byte
   // groups (brick.h field_read): the reference's 20 in 3D (operator_ns.h:
   // 120-132) with the time derivative, the U_t-only group skipped without it
-  // (18 in FP64); 16 with GLS_NEWTON_T1; the per-cell path the reference's
-  // set
+  // (18 in FP64); 16 for the brick Newton vmult (T1 tables, delta from U and
+  // h); the per-cell path the reference's set
   const double s   = (double)op->tsize();
   const int    dim = op->dim;
   const bool   td  = (op->prm.flags & GLS_CONSIDER_TIME_DERIVATIVE) && op->prm.order > 0;
@@ -2523,23 +2442,6 @@ gls_op_vmult_bytes(glsOp op)
   if (op->prm.flags & GLS_CELL_WISE_STAB)
     b += s * 2.0 * C;
   return b;
-}
-
-// diagnostic timeline builds only (GLS_STAMPS): copy g_stamps to the host
-int
-gls_debug_stamps(void *host, size_t bytes)
-{
-  GLS_TRY
-#ifdef GLS_STAMPS
-  const size_t nb = bytes < sizeof(g_stamps) ? bytes : sizeof(g_stamps);
-  HIP_THROW(hipDeviceSynchronize());
-  HIP_THROW(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), nb, 0, hipMemcpyDeviceToHost));
-#else
-  (void)host;
-  (void)bytes;
-  throw std::runtime_error("gls_debug_stamps: not a GLS_STAMPS build");
-#endif
-  GLS_CATCH
 }
 
 } // extern "C"

@@ -17,13 +17,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// GLS_ABL: diagnostic-only ablation builds (never the product library):
-//   1 plain (racy) read-modify-write instead of atomics, 2 no scatter,
-//   4 no table/geometry loads, 8 no gather
-#ifndef GLS_ABL
-#define GLS_ABL 0
-#endif
-
 namespace gls
 {
 constexpr uint32_t NODE_MASK  = 0x0FFFFFFFu;
@@ -212,9 +205,7 @@ delta_qwise(T u2, T h, T nu, T stau, T &d1, T &d2)
 // root estimates refined by Newton steps (two for FP64: ~1 ulp) instead of
 // IEEE divisions and square roots: ~25 instead of ~55 VALU instructions per
 // q point in the brick kernel; equal to delta_qwise to a few ulp
-#ifndef GLS_FAST_DELTA
-#define GLS_FAST_DELTA 1 // round 3: r2 FP64 -3.5 %, r3 FP64 -2 %, FP32 -2..3.5 % (kernel_ms)
-#endif
+// (round 3: r2 FP64 -3.5 %, r3 FP64 -2 %, FP32 -2..3.5 % kernel time)
 __device__ __forceinline__ double
 nr_rcp(double x)
 {
@@ -620,12 +611,8 @@ __global__ void __launch_bounds__(BLOCK)
       const uint32_t packed = a.nodes[cell * nq + p];
       node                  = packed & NODE_MASK;
       cm                    = packed >> 28;
-      if (!DIAG && !(GLS_ABL & 8))
+      if (!DIAG)
         load_node<T, nc>(a.src, node, u);
-      if (GLS_ABL & 8)
-#pragma unroll
-        for (int c = 0; c < nc; ++c)
-          u[c] = T(0.001) * (p + c);
     }
 
   // ---- prefetch geometry and per-q tables (consumed after evaluate)
@@ -651,19 +638,7 @@ __global__ void __launch_bounds__(BLOCK)
 #pragma unroll
   for (int i = 0; i < dim * dim + dim; ++i)
     oldg[i] = 0;
-  if (active && (GLS_ABL & 4))
-    {
-      g.JxW = T(1e-6);
-#pragma unroll
-      for (int i = 0; i < dim; ++i)
-        {
-          g.inv[i][i] = T(10) + p;
-          U[i]        = T(1) + i;
-        }
-      d1 = T(1e-4) * p;
-      d2 = T(1e-3);
-    }
-  if (active && !(GLS_ABL & 4))
+  if (active)
     {
       const uint32_t cg = a.cell_geo[cell];
       if (cg & GEO_GENERAL)
@@ -859,12 +834,7 @@ __global__ void __launch_bounds__(BLOCK)
         if (!((cm >> c) & 1))
           {
             const T r = in[c * nq + p];
-            if (GLS_ABL & 2)
-              asm volatile("" ::"v"(r));
-            else if (GLS_ABL & 1)
-              a.dst[(size_t)node * nc + c] += r;
-            else
-              unsafeAtomicAdd(a.dst + (size_t)node * nc + c, MODE == MODE_RESIDUAL ? -r : r);
+            unsafeAtomicAdd(a.dst + (size_t)node * nc + c, MODE == MODE_RESIDUAL ? -r : r);
           }
     }
 }

@@ -1809,8 +1809,11 @@ gls_mg_setup(glsMG mg, void *stream)
   if (mg->partitioned)
     throw std::runtime_error("gls_mg_setup: partitioned levels are set up by the host-driven "
                              "distributed multigrid (glsdist.py)");
-  hipStream_t  s  = (hipStream_t)stream;
-  const size_t nl = mg->ops.size();
+  // every allocation and launch of the setup (the AMG hierarchy included)
+  // on the levels' device; the caller's current device is restored
+  gls::DeviceScope dev(mg->ops[0]->device);
+  hipStream_t      s  = (hipStream_t)stream;
+  const size_t     nl = mg->ops.size();
   // the levels are independent here: each level's diagonal and power
   // iteration run on a stream of its own (forked from and joined back into
   // s by events), so the small levels' launch-bound steps overlap the fine

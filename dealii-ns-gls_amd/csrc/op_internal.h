@@ -126,7 +126,6 @@ struct glsOp_
   uint32_t *d_shared_off   = nullptr;
   gls::ReduceClasses reduce_classes{}; // multiplicity classes of the shared nodes
   void     *d_partial      = nullptr;
-  uint32_t *d_counters     = nullptr; // [n_shared] arrivals of the fused reduction
   void     *d_bgeo_cart    = nullptr; // brick path: cell-indexed geometry
   void     *d_bgeo_gen     = nullptr;
   uint32_t *d_brick_geo    = nullptr; // per brick: curved (bit 0) | cells << 8

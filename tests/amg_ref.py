@@ -115,9 +115,13 @@ class AMGRef:
                 continue
             self.levels.append(L)
             break
-        self.inv = np.linalg.inv(self.levels[-1]["A"].toarray())
+        # coarsest above the library's dense limit (amg_dense_limit): smoothed
+        n_last = self.levels[-1]["A"].shape[0]
+        self.inv = (np.linalg.inv(self.levels[-1]["A"].toarray())
+                    if n_last <= max(4 * coarse_max_size, 2048) else None)
 
     def _cheb(self, L, f, x):
+        # s + 1 Chebyshev steps; the zero start (x None) skips the product A 0
         s = max(1, self.sweeps)
         b = 1.1 * L["lam"]
         a = b / 30.0
@@ -141,7 +145,7 @@ class AMGRef:
     def _vcycle(self, l, f):
         L = self.levels[l]
         if l + 1 == len(self.levels):
-            return self.inv @ f
+            return self.inv @ f if self.inv is not None else self._cheb(L, f, None)
         x = self._cheb(L, f, None)
         r = f - L["A"] @ x
         xc = self._vcycle(l + 1, L["R"] @ r)

@@ -136,8 +136,8 @@ def test_vcycle_re3900_r0_r2():
     assert rel_err(_np(dst), ref.vcycle(b)) < 5e-4
 
 
-def _re3900(n_ref=2):
-    d = deck("input_hoffmann_3D_Re3900.json")
+def _re3900(n_ref=2, name="input_hoffmann_3D_Re3900.json"):
+    d = deck(name)
     meshes = [d.mesh(r) for r in range(n_ref + 1)]
     vel, p, slip = d.boundary_descriptor()
     cm = [m.constraint_mask(vel, p, slip) for m in meshes]
@@ -216,6 +216,54 @@ def test_vcycle_re3900_f64_levels_tight(coarse):
     torch.cuda.synchronize()
     err = rel_err(_np(dst), ref.vcycle(b))
     print(f"Re3900 r0..r2 FP64-level V-cycle (coarse {coarse}) rel err {err:.2e}")
+    assert err < 1e-9
+
+
+def test_vcycle_turek3d_direct_coarse():
+    """Config 3's own multigrid (input_turek_3D_Re100.json: GMG over r0..r3,
+    "gmg coarse grid solver": "direct", cylinder shift 0.005, no-slip walls,
+    main.cc:396-568, multigrid.cc:448-455) at the largest hierarchy the
+    oracle multigrid sets up in seconds, r0..r2: FP32 levels with the GPU's
+    dense coarse solve against the oracle's FP64 diagonals and FP64 LU, and
+    the GPU's relaxation factors against the oracle's power iteration."""
+    import torch
+    import glsamd
+    meshes, cm, params, w, u, hist = _re3900(2, "input_turek_3D_Re100.json")
+    mg, ops = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f32",
+                               coarse_n_iterations=-1)
+    ref = OracleGMG(meshes, cm, params, u, hist, w, coarse_iters=-1)
+    for l in range(1, len(meshes)):  # (the direct-solved coarsest level is not smoothed)
+        lg, lr = mg.relaxation(l)[1], ref.estimate(l)
+        assert abs(lg - lr) <= 1e-3 * lr, (l, lg, lr)
+    ref.set_omega([mg.relaxation(l)[0] for l in range(len(meshes))])
+    b = gi.rnd(13, meshes[-1].n_dofs)
+    src = torch.from_numpy(b).cuda()
+    dst = torch.zeros_like(src)
+    mg.vcycle(dst, src)
+    torch.cuda.synchronize()
+    err = rel_err(_np(dst), ref.vcycle(b))
+    print(f"Turek-3D r0..r2 direct-coarse V-cycle rel err {err:.2e}")
+    assert err < 5e-4
+
+
+def test_vcycle_turek3d_f64_levels_tight():
+    """Config 3's V-cycle with FP64 levels and the deck's direct coarse
+    solve against the oracle multigrid (its own FP64 diagonals and LU; the
+    relaxation factors shared): the algorithmic difference at 1e-9."""
+    import torch
+    import glsamd
+    meshes, cm, params, w, u, hist = _re3900(2, "input_turek_3D_Re100.json")
+    mg, ops = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f64",
+                               coarse_n_iterations=-1)
+    ref = OracleGMG(meshes, cm, params, u, hist, w, coarse_iters=-1)
+    ref.set_omega([mg.relaxation(l)[0] for l in range(len(meshes))])
+    b = gi.rnd(13, meshes[-1].n_dofs)
+    src = torch.from_numpy(b).cuda()
+    dst = torch.zeros_like(src)
+    mg.vcycle(dst, src)
+    torch.cuda.synchronize()
+    err = rel_err(_np(dst), ref.vcycle(b))
+    print(f"Turek-3D r0..r2 FP64-level V-cycle rel err {err:.2e}")
     assert err < 1e-9
 
 

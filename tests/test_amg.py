@@ -77,11 +77,18 @@ def test_ref_dirichlet_points_not_aggregated():
 @pytest.mark.gpu
 @pytest.mark.parametrize("params", [dict(block_size=1, threshold=0.0, coarse_max_size=300),
                                     dict(block_size=1, threshold=0.0, coarse_max_size=300,
-                                         elliptic=False, smoother_sweeps=3)])
+                                         elliptic=False, smoother_sweeps=3),
+                                    # coarsest level above the dense limit
+                                    # (max_levels reached): smoothed, not factorised
+                                    dict(block_size=1, threshold=0.0, coarse_max_size=300,
+                                         max_levels=1),
+                                    dict(block_size=1, threshold=0.0, coarse_max_size=300,
+                                         max_levels=2, n=160)])
 def test_gpu_amg_poisson(params):
     import torch
     import glsamd
-    A = _poisson(80)
+    params = dict(params)
+    A = _poisson(params.pop("n", 80))
     ref = AMGRef(A, **params)
     amg = glsamd.AMG(A, **params)
     info = amg.info()

@@ -29,12 +29,15 @@ def _hierarchy(n_ref=1):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("prec,coarse", [("f64", 10), ("f64", -1), ("f32", 10)])
-def test_native_group_vcycle(world, prec, coarse):
+@pytest.mark.parametrize("prec,coarse,n_ref", [("f64", 10, 1), ("f64", -1, 1), ("f32", 10, 1),
+                                               # the production setup: FP32 levels with the
+                                               # redundant direct coarse solve, 2 and 3 levels
+                                               ("f32", -1, 1), ("f32", -1, 2)])
+def test_native_group_vcycle(world, prec, coarse, n_ref):
     import torch
     import glsamd
     import glsdist
-    meshes, cm, params, w, u, hist = _hierarchy(1)
+    meshes, cm, params, w, u, hist = _hierarchy(n_ref)
     ref, _ = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision=prec,
                               coarse_n_iterations=coarse)
     g = glsdist.NativeGroupMultigrid(meshes, cm, world, precision=prec,
@@ -53,7 +56,8 @@ def test_native_group_vcycle(world, prec, coarse):
     ref.vcycle(dst, src)
     torch.cuda.synchronize()
     err = rel_err(g.gather(xs).cpu().numpy(), dst.cpu().numpy())
-    print(f"world {world} {prec} coarse {coarse}: partitioned vs single-domain V-cycle {err:.2e}")
+    print(f"world {world} {prec} coarse {coarse} levels {n_ref + 1}: partitioned vs "
+          f"single-domain V-cycle {err:.2e}")
     assert err < (1e-10 if prec == "f64" else 1e-5)
 
 
