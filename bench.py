@@ -309,6 +309,24 @@ def mg_companions(d, params, weights, n_ref, reps=20):
             torch.cuda.synchronize()
             t.append(e0.elapsed_time(e1))
         lu["ms"] = float(np.median(t))
+        # the same cycle replayed from its captured hipGraph (GLS_MG_GRAPH=1;
+        # correctness: tests/test_gpu_mg.py::test_vcycle_graph_replay)
+        os.environ["GLS_MG_GRAPH"] = "1"
+        try:
+            for _ in range(3):
+                mg_lu.vcycle(x, b)
+            torch.cuda.synchronize()
+            t = []
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                mg_lu.vcycle(x, b)
+                e1.record()
+                torch.cuda.synchronize()
+                t.append(e0.elapsed_time(e1))
+            lu["ms_hipgraph_replay"] = float(np.median(t))
+        finally:
+            os.environ.pop("GLS_MG_GRAPH")
         lu["coarse_dofs"] = meshes[0].n_dofs
         lu["coarse_free_dofs"] = int(sum(((c >> k) & 1 == 0).sum() for c in [cm[0]]
                                          for k in range(4)))

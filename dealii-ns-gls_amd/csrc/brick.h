@@ -464,7 +464,10 @@ to_packs(const T (&x)[nc], V (&v)[NP])
 // the earlier prefetch (issued behind the previous round's Dq^T sweeps), as
 // do the other instantiations.
 // (A GEO_ANY kernel whose curved bricks load J^{-1} at its two points of
-// use instead of with the tables still needs 162 VGPRs: measured round 3.)
+// use instead of with the tables still needs 162 VGPRs: measured round 3;
+// forced to 4 waves it spills 140 B/lane inside the round loop and takes
+// 63.7 instead of 40.2 us at r2, 517 instead of 276 us at r3: round 4,
+// profiles/r04/explore/ab_any4_spill.txt.)
 template <int dim, int k, typename T, int MODE, int GEO>
 struct BrickOcc
 {

@@ -56,10 +56,15 @@ struct DeviceScope
   DeviceScope &operator=(const DeviceScope &) = delete;
 };
 
+// what a brick launch runs: the brick kernel, and the shared-node reduction
+// of the owned rows, of the ghost rows (a partitioned operator's export
+// block), or of both
 enum
 {
-  BRICK_RUN    = 1,
-  BRICK_REDUCE = 2
+  BRICK_RUN          = 1,
+  BRICK_REDUCE_OWNED = 2,
+  BRICK_REDUCE_GHOST = 4,
+  BRICK_REDUCE       = BRICK_REDUCE_OWNED | BRICK_REDUCE_GHOST
 };
 
 // multiplicity classes of the brick-boundary nodes (k_shared_reduce_cls)

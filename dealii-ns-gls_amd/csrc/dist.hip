@@ -9,18 +9,24 @@
 //                                        ghost entries zeroed   (export-add)
 //   dst[c] = src[c] on constrained owned dofs        (identity rows)
 //
-// One gls_dist_vmult on stream s:
+// One gls_dist_vmult on stream s (deal.II's overlapped cell_loop: ghost
+// import behind the first interior cells, export-add behind the rest):
 //   pack      k_pack: send buffer <- src[send nodes]                  (s)
 //   import    ncclSend/ncclRecv per peer, the receives land directly in
 //             src's ghost block of that owner                          (comm stream)
-//   interior  k_brick over the work units that read no ghost node      (s, overlaps the import)
-//   boundary  k_brick over the rest, after the import event            (s)
-//   reduce    k_shared_reduce_cls: brick boundaries, ghost rows, identity rows
+//   interior1 k_brick over the first half of the work units that read no
+//             ghost node                                               (s, overlaps the import)
+//   boundary  k_brick over the units that read ghost nodes, after the
+//             import event, then the reduction of the GHOST rows only
+//             (their partial sums come from these units alone)         (s)
 //   export    ncclSend of each owner's ghost block of dst, ncclRecv into
-//             the export buffer                                        (s)
-//   unpack    k_unpack_add: owned rows += received partials (fixed order
-//             per node, constrained components skipped: their identity
-//             value stands), then the ghost block of dst is zeroed.
+//             the export buffer, after the ghost-reduce event          (comm stream)
+//   interior2 k_brick over the other interior units, then the reduction of
+//             the owned rows (brick boundaries, identity rows)         (s, overlaps the export)
+//   unpack    after the export event, k_unpack_add: owned rows +=
+//             received partials (fixed order per node, constrained
+//             components skipped: their identity value stands), then the
+//             ghost block of dst is zeroed.
 // The in-process group (gls_dist_create with nccl_id NULL) runs the same
 // phases with device copies in place of RCCL, so the whole orchestration
 // is testable on one GPU (tests/test_dist.py).
@@ -116,6 +122,7 @@ struct glsDist_
   Group            *group = nullptr;
   hipStream_t       cs   = nullptr;
   hipEvent_t        ev_packed = nullptr, ev_imported = nullptr;
+  hipEvent_t        ev_ghosts = nullptr, ev_exported = nullptr;
   std::vector<Peer> peers;
   int64_t           n_send = 0, n_recv_nodes = 0;
   uint32_t         *d_send_nodes = nullptr; // [n_send] node | cmask << 28
@@ -231,7 +238,7 @@ nccl_import(glsDist_ *d, void *src)
 }
 
 void
-nccl_export(glsDist_ *d, void *dst, hipStream_t s)
+nccl_export(glsDist_ *d, const void *dst, hipStream_t s)
 {
   const size_t rb = row_bytes(d->op);
   const int    nc = d->op->dim + 1;
@@ -400,6 +407,8 @@ gls_dist_create(glsOp op, const glsDistDesc *desc, glsDist *out)
   HIP_THROW(hipStreamCreateWithFlags(&d->cs, hipStreamNonBlocking));
   HIP_THROW(hipEventCreateWithFlags(&d->ev_packed, hipEventDisableTiming));
   HIP_THROW(hipEventCreateWithFlags(&d->ev_imported, hipEventDisableTiming));
+  HIP_THROW(hipEventCreateWithFlags(&d->ev_ghosts, hipEventDisableTiming));
+  HIP_THROW(hipEventCreateWithFlags(&d->ev_exported, hipEventDisableTiming));
   if (desc->nccl_id)
     {
       ncclUniqueId id;
@@ -448,6 +457,9 @@ gls_dist_destroy(glsDist d)
     (void)hipEventDestroy(d->ev_packed);
   if (d->ev_imported)
     (void)hipEventDestroy(d->ev_imported);
+  for (hipEvent_t e : {d->ev_ghosts, d->ev_exported})
+    if (e)
+      (void)hipEventDestroy(e);
   if (d->cs)
     (void)hipStreamDestroy(d->cs);
   delete d;
@@ -473,18 +485,26 @@ dist_vmult(glsDist d, void *dst, void *src, hipStream_t s, const gls::RelaxStep 
       zero_ghosts(d, dst, s);
       return;
     }
-  // import (comm stream) || interior bricks (s)
+  const int64_t ni = op->n_interior_bricks, nh = ni / 2;
+  // import (comm stream) || first interior half (s)
   pack(d, src, s);
   HIP_THROW(hipEventRecord(d->ev_packed, s));
   HIP_THROW(hipStreamWaitEvent(d->cs, d->ev_packed, 0));
   nccl_import(d, src);
   HIP_THROW(hipEventRecord(d->ev_imported, d->cs));
-  gls::brick_launch(op, mode, dst, src, 0, op->n_interior_bricks, gls::BRICK_RUN, s, rx);
+  gls::brick_launch(op, mode, dst, src, 0, nh, gls::BRICK_RUN, s, rx);
+  // boundary units and the ghost rows they complete
   HIP_THROW(hipStreamWaitEvent(s, d->ev_imported, 0));
-  gls::brick_launch(op, mode, dst, src, op->n_interior_bricks, op->n_bricks,
-                    gls::BRICK_RUN | gls::BRICK_REDUCE, s, rx);
-  // compress(add)
-  nccl_export(d, dst, s);
+  gls::brick_launch(op, mode, dst, src, ni, op->n_bricks,
+                    gls::BRICK_RUN | gls::BRICK_REDUCE_GHOST, s, rx);
+  HIP_THROW(hipEventRecord(d->ev_ghosts, s));
+  // compress(add) of the ghost rows (comm stream) || second interior half
+  // and the owned rows' reduction (s)
+  HIP_THROW(hipStreamWaitEvent(d->cs, d->ev_ghosts, 0));
+  nccl_export(d, dst, d->cs);
+  HIP_THROW(hipEventRecord(d->ev_exported, d->cs));
+  gls::brick_launch(op, mode, dst, src, nh, ni, gls::BRICK_RUN | gls::BRICK_REDUCE_OWNED, s, rx);
+  HIP_THROW(hipStreamWaitEvent(s, d->ev_exported, 0));
   unpack(d, dst, s, rx);
   zero_ghosts(d, dst, s);
 }
@@ -504,13 +524,14 @@ dist_vmult_group(glsDist const *members, void *const *dsts, void *const *srcs, i
       members[r]->cur_dst = dsts[r];
       members[r]->cur_src = srcs[r];
     }
+  // the phases of dist_vmult, member by member in lockstep on one stream
   for (int r = 0; r < n; ++r)
     pack(members[r], srcs[r], s);
   for (int r = 0; r < n; ++r)
     {
       glsOp_ *op = members[r]->op;
-      gls::brick_launch(op, gls::op_vmult_mode(op), dsts[r], srcs[r], 0, op->n_interior_bricks,
-                        gls::BRICK_RUN, s, rx ? rx + r : nullptr);
+      gls::brick_launch(op, gls::op_vmult_mode(op), dsts[r], srcs[r], 0,
+                        op->n_interior_bricks / 2, gls::BRICK_RUN, s, rx ? rx + r : nullptr);
     }
   for (int r = 0; r < n; ++r)
     local_import(members[r], s);
@@ -518,10 +539,18 @@ dist_vmult_group(glsDist const *members, void *const *dsts, void *const *srcs, i
     {
       glsOp_ *op = members[r]->op;
       gls::brick_launch(op, gls::op_vmult_mode(op), dsts[r], srcs[r], op->n_interior_bricks,
-                        op->n_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE, s, rx ? rx + r : nullptr);
+                        op->n_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE_GHOST, s,
+                        rx ? rx + r : nullptr);
     }
   for (int r = 0; r < n; ++r)
     local_export(members[r], s);
+  for (int r = 0; r < n; ++r)
+    {
+      glsOp_ *op = members[r]->op;
+      gls::brick_launch(op, gls::op_vmult_mode(op), dsts[r], srcs[r], op->n_interior_bricks / 2,
+                        op->n_interior_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE_OWNED, s,
+                        rx ? rx + r : nullptr);
+    }
   for (int r = 0; r < n; ++r)
     unpack(members[r], dsts[r], s, rx ? rx + r : nullptr);
   for (int r = 0; r < n; ++r)

@@ -295,36 +295,52 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
           shared_nodes.push_back((uint32_t)node);
         }
     }
-  // order the shared nodes by brick multiplicity (then node): inside a
-  // class of multiplicity m node j's slots start at slot0 + j * m, so
-  // k_shared_reduce computes its slot addresses instead of loading them
-  std::stable_sort(shared_nodes.begin(), shared_nodes.end(),
-                   [&](uint32_t x, uint32_t y) { return mult[x] < mult[y]; });
+  // order the shared nodes owned rows first, then by brick multiplicity
+  // (then node): inside a class of multiplicity m node j's slots start at
+  // slot0 + j * m, so k_shared_reduce computes its slot addresses instead of
+  // loading them; the ghost rows (a partitioned operator's export block)
+  // form a separately launchable tail
+  const int64_t n_own_nodes = d->n_owned_nodes;
+  std::stable_sort(shared_nodes.begin(), shared_nodes.end(), [&](uint32_t x, uint32_t y) {
+    const bool gx = (int64_t)x >= n_own_nodes, gy = (int64_t)y >= n_own_nodes;
+    return gx != gy ? gy : mult[x] < mult[y];
+  });
   for (size_t s = 0; s < shared_nodes.size(); ++s)
     shared_index[shared_nodes[s]] = (int64_t)s;
   std::vector<uint32_t> off(shared_nodes.size() + 1, 0);
   for (size_t s = 0; s < shared_nodes.size(); ++s)
     off[s + 1] = off[s] + mult[shared_nodes[s]];
-  ReduceClasses rc{};
-  for (size_t s = 0; s < shared_nodes.size(); ++s)
-    {
-      const uint32_t m = mult[shared_nodes[s]];
-      if (rc.n == 0 || rc.mult[rc.n - 1] != m)
-        {
-          if (rc.n == ReduceClasses::MAX)
-            {
-              rc.n = -1; // too many classes: offsets kernel
-              break;
-            }
-          rc.first[rc.n] = (uint32_t)s;
-          rc.mult[rc.n]  = m;
-          rc.slot0[rc.n] = off[s];
-          rc.n++;
-        }
-    }
-  if (rc.n >= 0)
-    rc.first[rc.n] = (uint32_t)shared_nodes.size();
-  op->reduce_classes = rc;
+  // multiplicity classes of the shared nodes [s0, s1) (first[] relative to
+  // s0); n = -1: too many classes (offset-table kernel)
+  auto classes = [&](size_t s0, size_t s1) {
+    ReduceClasses rc{};
+    for (size_t s = s0; s < s1; ++s)
+      {
+        const uint32_t m = mult[shared_nodes[s]];
+        if (rc.n == 0 || rc.mult[rc.n - 1] != m)
+          {
+            if (rc.n == ReduceClasses::MAX)
+              {
+                rc.n = -1;
+                break;
+              }
+            rc.first[rc.n] = (uint32_t)(s - s0);
+            rc.mult[rc.n]  = m;
+            rc.slot0[rc.n] = off[s];
+            rc.n++;
+          }
+      }
+    if (rc.n >= 0)
+      rc.first[rc.n] = (uint32_t)(s1 - s0);
+    return rc;
+  };
+  size_t n_sh_own = 0;
+  while (n_sh_own < shared_nodes.size() && (int64_t)shared_nodes[n_sh_own] < n_own_nodes)
+    ++n_sh_own;
+  op->n_shared_owned = (int64_t)n_sh_own;
+  op->reduce_classes = classes(0, shared_nodes.size());
+  op->reduce_owned   = classes(0, n_sh_own);
+  op->reduce_ghost   = classes(n_sh_own, shared_nodes.size());
   const uint64_t n_slot_total = off.back();
   if (n_slot_total >= SHARED_BIT)
     throw std::runtime_error("gls_op_create: too many partial slots");
@@ -758,32 +774,45 @@ struct Impl
               launch_brick<MODE_RESIDUAL>(b1 - b0, lds, geo, s, a);
             HIP_THROW(hipGetLastError());
           }
-        if ((what & BRICK_REDUCE) && op->n_shared > 0)
+        // the shared-node reduction over all shared nodes, or over the owned
+        // / ghost part alone ([owned | ghost] order, build_bricks)
+        int64_t              r0 = 0, r1 = 0;
+        const ReduceClasses *rcp = &op->reduce_classes;
+        if ((what & BRICK_REDUCE) == BRICK_REDUCE)
+          r1 = op->n_shared;
+        else if (what & BRICK_REDUCE_OWNED)
+          r1 = op->n_shared_owned, rcp = &op->reduce_owned;
+        else if (what & BRICK_REDUCE_GHOST)
+          r0 = op->n_shared_owned, r1 = op->n_shared, rcp = &op->reduce_ghost;
+        const int64_t nr = r1 - r0;
+        if (nr > 0)
           {
-            const dim3 g2((unsigned)((op->n_shared * (dim + 1) + 255) / 256));
+            const dim3 g2((unsigned)((nr * (dim + 1) + 255) / 256));
             // the class kernel runs one thread per 16-byte pack when nc = 4
             const int  npk = (dim + 1) % (16 / (int)sizeof(T)) == 0 ?
                                (dim + 1) / (16 / (int)sizeof(T)) : dim + 1;
-            const dim3 g3((unsigned)((op->n_shared * npk + 255) / 256));
-            const ReduceClasses &rc = op->reduce_classes;
+            const dim3 g3((unsigned)((nr * npk + 255) / 256));
+            const ReduceClasses &rc   = *rcp;
+            const uint32_t      *nods = op->d_shared_nodes + r0;
+            const uint32_t      *offs = op->d_shared_off + r0;
             if (rc.n > 0 && mode == MODE_RESIDUAL)
               hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, true>), g3, dim3(256), 0, s,
-                                 (T *)dst, (const T *)src, (const T *)op->d_partial,
-                                 op->d_shared_nodes, rc, op->n_shared);
+                                 (T *)dst, (const T *)src, (const T *)op->d_partial, nods, rc,
+                                 nr);
             else if (rc.n > 0)
               hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, false>), g3, dim3(256), 0, s,
-                                 (T *)dst, (const T *)src, (const T *)op->d_partial,
-                                 op->d_shared_nodes, rc, op->n_shared, a.rb, a.rd, a.romega,
-                                 a.rkeep, (uint32_t)op->n_owned_nodes);
+                                 (T *)dst, (const T *)src, (const T *)op->d_partial, nods, rc,
+                                 nr, a.rb, a.rd, a.romega, a.rkeep,
+                                 (uint32_t)op->n_owned_nodes);
             else if (mode == MODE_RESIDUAL)
               hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, true>), g2, dim3(256), 0, s,
-                                 (T *)dst, (const T *)src, (const T *)op->d_partial,
-                                 op->d_shared_nodes, op->d_shared_off, op->n_shared);
+                                 (T *)dst, (const T *)src, (const T *)op->d_partial, nods, offs,
+                                 nr);
             else
               hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, false>), g2, dim3(256), 0, s,
-                                 (T *)dst, (const T *)src, (const T *)op->d_partial,
-                                 op->d_shared_nodes, op->d_shared_off, op->n_shared, a.rb,
-                                 a.rd, a.romega, a.rkeep, (uint32_t)op->n_owned_nodes);
+                                 (T *)dst, (const T *)src, (const T *)op->d_partial, nods, offs,
+                                 nr, a.rb, a.rd, a.romega, a.rkeep,
+                                 (uint32_t)op->n_owned_nodes);
             HIP_THROW(hipGetLastError());
           }
       }

@@ -290,9 +290,10 @@ k_residual(T *__restrict__ t, const T *__restrict__ b, int64_t n)
     t[i] = b[i] - t[i];
 }
 
-// zero fill / copy as kernels: the captured V-cycle graph holds kernel
-// nodes only (graphs with captured memset / memcpy nodes were measured to
-// race on ROCm 7.2: scripts/graph_diag.py)
+// zero fill / copy of the V-cycle's own buffers: kernels by default;
+// GLS_MG_MEMNODES=1 issues hipMemsetAsync / hipMemcpyAsync instead (in a
+// captured V-cycle: memset / memcpy graph nodes).  Both are checked bit for
+// bit against the eager V-cycle (tests/test_gpu_mg.py::test_vcycle_graph_*).
 __global__ void
 k_zero(uint32_t *__restrict__ x, int64_t n_words)
 {
@@ -435,6 +436,35 @@ g1(int64_t n)
 {
   return dim3((unsigned)((n + 255) / 256));
 }
+
+bool
+mem_nodes()
+{
+  const char *e = getenv("GLS_MG_MEMNODES");
+  return e && std::atoi(e) != 0;
+}
+
+void
+zero_words(void *x, int64_t n_words, hipStream_t s)
+{
+  if (mem_nodes())
+    HIP_THROW(hipMemsetAsync(x, 0, (size_t)n_words * 4, s));
+  else
+    hipLaunchKernelGGL(k_zero, g1(n_words), dim3(256), 0, s, (uint32_t *)x, n_words);
+  HIP_THROW(hipGetLastError());
+}
+
+void
+copy_words(void *y, const void *x, int64_t n_words, hipStream_t s)
+{
+  if (mem_nodes())
+    HIP_THROW(hipMemcpyAsync(y, x, (size_t)n_words * 4, hipMemcpyDeviceToDevice, s));
+  else
+    hipLaunchKernelGGL(k_copy, g1(n_words), dim3(256), 0, s, (uint32_t *)y,
+                       (const uint32_t *)x, n_words);
+  HIP_THROW(hipGetLastError());
+}
+
 
 } // namespace
 
@@ -638,9 +668,7 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
       if (start_in_tmp)
         {
           const int64_t w = (int64_t)((size_t)op->n_dofs * mg->ts() / 4);
-          hipLaunchKernelGGL(k_copy, g1(w), dim3(256), 0, s, (uint32_t *)x, (const uint32_t *)tmp,
-                             w);
-          HIP_THROW(hipGetLastError());
+          copy_words(x, tmp, w, s);
         }
       if (zero_start && iters > 0)
         {
@@ -681,8 +709,7 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
   if (cur != x)
     {
       const int64_t w = (int64_t)((size_t)op->n_dofs * mg->ts() / 4);
-      hipLaunchKernelGGL(k_copy, g1(w), dim3(256), 0, s, (uint32_t *)x, (const uint32_t *)cur, w);
-      HIP_THROW(hipGetLastError());
+      copy_words(x, cur, w, s);
     }
   return zero_start && iters > 0;
 }
@@ -1194,9 +1221,7 @@ coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
       return;
     }
   // constrained dofs: x_c = b_c (their rows of A are the identity)
-  const int64_t w = n * (int64_t)sizeof(T) / 4;
-  hipLaunchKernelGGL(k_copy, g1(w), dim3(256), 0, s, (uint32_t *)mg->sol[0],
-                     (const uint32_t *)mg->def[0], w);
+  copy_words(mg->sol[0], mg->def[0], n * (int64_t)sizeof(T) / 4, s);
   hipLaunchKernelGGL(k_gather_free<T>, g1(nf), dim3(256), 0, s, mg->d_rhs,
                      (const T *)mg->def[0], (const int32_t *)mg->d_free, nf);
   double *part = mg->d_rhs + 2 * ld;
@@ -1248,10 +1273,7 @@ coarse_apply(glsMG_ *mg, hipStream_t s)
     }
   else if (mg->desc.coarse_n_iterations == 0)
     {
-      const int64_t w = (int64_t)(bytes / 4);
-      hipLaunchKernelGGL(k_copy, g1(w), dim3(256), 0, s, (uint32_t *)mg->sol[0],
-                         (const uint32_t *)mg->def[0], w);
-      HIP_THROW(hipGetLastError());
+      copy_words(mg->sol[0], mg->def[0], (int64_t)(bytes / 4), s);
     }
   else
     smooth(mg, 0, mg->sol[0], mg->def[0], true, mg->desc.coarse_n_iterations, s);
@@ -1479,8 +1501,7 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
   if (!folded)
     {
       const int64_t w = (int64_t)((size_t)mg->ops[l - 1]->n_dofs * mg->ts() / 4);
-      hipLaunchKernelGGL(k_zero, g1(w), dim3(256), 0, s, (uint32_t *)mg->def[l - 1], w);
-      HIP_THROW(hipGetLastError());
+      zero_words(mg->def[l - 1], w, s);
     }
   transfer(mg, 1, l, mg->def[l - 1], mg->tmp[l], s);
   v_step(mg, l - 1, s);
@@ -1555,8 +1576,8 @@ run_v_step(glsMG_ *mg, int top, hipStream_t s)
   // the kernels' own duration, not by host launch overhead; off by default
   const char *e   = getenv("GLS_MG_GRAPH");
   const bool  use = (e && std::atoi(e) != 0) &&
-                   mg->desc.coarse_n_iterations >= 0 && // rocSOLVER coarse LU: not captured
-                   !mg->desc.coarse_iterate;            // coarse GMRES syncs the host
+                   !mg->desc.coarse_iterate && // coarse GMRES syncs the host
+                   !mg->desc.coarse_amg;       // (AMG cycle: not captured)
   if (!use)
     {
       v_step(mg, top, s);

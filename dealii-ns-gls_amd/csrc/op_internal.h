@@ -125,6 +125,12 @@ struct glsOp_
   uint32_t *d_shared_nodes = nullptr;
   uint32_t *d_shared_off   = nullptr;
   gls::ReduceClasses reduce_classes{}; // multiplicity classes of the shared nodes
+  // the shared nodes are ordered [owned | ghost]: the first n_shared_owned
+  // are owned rows; classes of each part on its own (first[] relative to the
+  // part's first node, slot0 absolute), so the ghost rows of a partitioned
+  // vmult are reduced (and exported) before the rest of the cell loop
+  int64_t            n_shared_owned = 0;
+  gls::ReduceClasses reduce_owned{}, reduce_ghost{};
   void     *d_partial      = nullptr;
   void     *d_bgeo_cart    = nullptr; // brick path: cell-indexed geometry
   void     *d_bgeo_gen     = nullptr;

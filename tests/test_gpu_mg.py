@@ -223,3 +223,75 @@ def test_coarse_gmres_vcycle(name, n_ref, coarse):
     assert conv and it > 0
     assert abs(it - ref.coarse_gmres_iterations) <= 3, (it, ref.coarse_gmres_iterations)
     assert rel_err(_np(dst), xr) < 2e-3
+
+
+def _re3900_gmg(coarse, prec="f32"):
+    import glsamd
+    meshes, cmasks, params, w, u, hist = _hierarchy("input_hoffmann_3D_Re3900.json", 2)
+    mg, ops = glsamd.build_gmg(meshes, cmasks, params, u, hist, w, precision=prec,
+                               coarse_n_iterations=coarse)
+    A = glsamd.NavierStokesOperator(meshes[-1], cmasks[-1], "f64")
+    A.set_parameters(**params)
+    A.set_linearization_point(u)
+    A.set_previous_solution(hist, w)
+    return meshes, mg, A
+
+
+@pytest.mark.parametrize("prec,coarse", [("f32", 10), ("f32", -1), ("f64", -1)])
+@pytest.mark.parametrize("memnodes", [False, True])
+def test_vcycle_graph_replay(prec, coarse, memnodes, monkeypatch):
+    """The hipGraph V-cycle (GLS_MG_GRAPH=1: v_step captured once on the
+    multigrid's own stream, replayed between events on the caller's stream,
+    multigrid.cc:202-220) against the eager V-cycle on the headline hierarchy
+    r0..r2 (FP32 levels, FP64 in / out), with the deck's direct coarse solve
+    and with relaxation sweeps, with the V-cycle's zero fills / copies as
+    kernels and as memset / memcpy graph nodes (GLS_MG_MEMNODES=1): three
+    replays on changing inputs (the capture must read the current defect, not
+    the one of the capture) and a GMRES(28) solve preconditioned by the
+    replayed cycle.  The brick kernels accumulate cells in LDS with atomics,
+    so two eager cycles already differ in the last bits (measured with FP32
+    levels: 6e-8 relative, the FP32 rounding of reordered FP64 sums carried
+    through the cycle; FP64 levels: ~1e-15); a missing dependency (a node
+    reading a buffer before its producer) shows up as an O(1e-2..1)
+    difference.  Tolerances: FP64 levels 1e-12; FP32 levels the larger of
+    1e-6 and 20x the eager-vs-eager difference, and the same GMRES iteration
+    count."""
+    import torch
+    import glsamd
+    meshes, mg, A = _re3900_gmg(coarse, prec)
+    bs = [A._dev(gi.rnd(21 + i, meshes[-1].n_dofs)) for i in range(3)]
+
+    def cycles():
+        out = []
+        for b in bs:
+            x = torch.zeros_like(b)
+            mg.vcycle(x, b)
+            out.append(x)
+        torch.cuda.synchronize()
+        return [_np(x) for x in out]
+
+    def gmres():
+        x = torch.zeros_like(bs[0])
+        s = glsamd.LinearSolverGMRES(A, mg, relative_tolerance=1e-8, absolute_tolerance=0.0)
+        s.solve(x, bs[0])
+        torch.cuda.synchronize()
+        return _np(x), s.last["n_iterations"]
+
+    eager, eager2 = cycles(), cycles()
+    x_e, it_e = gmres()
+    if memnodes:
+        monkeypatch.setenv("GLS_MG_MEMNODES", "1")
+    monkeypatch.setenv("GLS_MG_GRAPH", "1")
+    graph = cycles()  # capture + replays
+    graph2 = cycles()
+    x_g, it_g = gmres()
+    monkeypatch.delenv("GLS_MG_GRAPH")
+    d_ee = max(rel_err(a, b) for a, b in zip(eager2, eager))
+    d_ge = max(rel_err(a, b) for a, b in zip(graph + graph2, eager + eager))
+    n_bits = sum(int(np.count_nonzero(a != b)) for a, b in zip(graph, eager))
+    print(f"{prec} coarse {coarse} memnodes {memnodes}: eager vs eager {d_ee:.1e}, graph vs "
+          f"eager {d_ge:.1e} ({n_bits} differing entries), GMRES {it_g} vs {it_e} iterations, "
+          f"x diff {rel_err(x_g, x_e):.1e}")
+    tol = 1e-12 if prec == "f64" else max(1e-6, 20 * d_ee)
+    assert d_ge < tol
+    assert it_g == it_e and rel_err(x_g, x_e) < (1e-10 if prec == "f64" else 1e-5)
