@@ -414,7 +414,11 @@ def amg_companions(reps=5):
         b = torch.from_numpy(gi.src_vector(meshes[-1].n_dofs)).cuda()
         x = torch.zeros_like(b)
         line = {"finest_dofs": meshes[-1].n_dofs, "levels": n_ref + 1}
-        variants = [("amg", dict(coarse_amg=d.amg_parameters()))]
+        # the AMG with deal.II's "smoother: Chebyshev alpha" 10 (the default)
+        # and with ML's own default 30
+        variants = [("amg", dict(coarse_amg=d.amg_parameters())),
+                    ("amg_alpha30", dict(coarse_amg=dict(d.amg_parameters(),
+                                                         chebyshev_alpha=30.0)))]
         if relax:
             variants.append(("relax10", dict(coarse_n_iterations=10)))
         for key, kw in variants:
@@ -433,10 +437,10 @@ def amg_companions(reps=5):
                 it, conv = mg.coarse_statistics()
                 r = {"vcycle_ms": float(np.median(t)), "coarse_gmres_iterations": it,
                      "converged": conv, "coarse_dofs": meshes[0].n_dofs}
-                if key == "amg":
+                if key.startswith("amg"):
                     info, setup_ms = mg.coarse_amg()
-                    r.update(amg_setup_ms=setup_ms, amg_sizes=info["sizes"],
-                             amg_nnz=info["nnz"])
+                    r.update(amg_setup_ms=setup_ms, amg_levels=info["levels"],
+                             amg_sizes=info["sizes"], amg_nnz=info["nnz"])
                 line[key] = r
                 del mg
             except Exception as e:  # reported, never fatal

@@ -259,8 +259,11 @@ aggregate(const HostCSR &A, int b, double theta, int32_t &n_agg)
 }
 
 // ------------------------------------------------------------ device kernels
-// one wavefront per row: out_i = (f_i - sum_j A_ij (x_j + d_j)) and the
-// Chebyshev update (cheb_step), or plain forms (below)
+// G lanes per row (G = 64 / 32 / 16 / 8, chosen per matrix from its mean row
+// length: rows of the iso-Q1 coarse levels hold ~90 entries, a full
+// wavefront per row would idle 40 % of its lanes on the second pass):
+// out_i = (f_i - sum_j A_ij (x_j + d_j)) and the Chebyshev update
+// (cheb_step), or plain forms (below)
 __device__ __forceinline__ double
 wave_sum(double s)
 {
@@ -270,21 +273,26 @@ wave_sum(double s)
   return s;
 }
 
+template <int G>
 __device__ __forceinline__ double
 row_dot(const int32_t *__restrict__ rp, const int32_t *__restrict__ ci,
         const double *__restrict__ v, const double *__restrict__ x,
         const double *__restrict__ d, int64_t r, int lane)
 {
   double s = 0;
-  for (int32_t k = rp[r] + lane; k < rp[r + 1]; k += 64)
+  for (int32_t k = rp[r] + lane; k < rp[r + 1]; k += G)
     {
       const int32_t j = ci[k];
       s += v[k] * (d ? x[j] + d[j] : x[j]);
     }
-  return wave_sum(s);
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1)
+    s += __shfl_xor(s, o);
+  return s;
 }
 
 // Chebyshev step: t = dinv (f - A (x + d)); xo = x + d; do = alpha d + beta t
+template <int G>
 __global__ void __launch_bounds__(256)
   k_cheb_step(const int32_t *__restrict__ rp, const int32_t *__restrict__ ci,
               const double *__restrict__ v, const double *__restrict__ x,
@@ -292,11 +300,11 @@ __global__ void __launch_bounds__(256)
               const double *__restrict__ dinv, double *__restrict__ xo, double *__restrict__ dout,
               double alpha, double beta, int64_t n)
 {
-  const int64_t r    = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int     lane = threadIdx.x & 63;
+  const int64_t r    = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  const int     lane = threadIdx.x & (G - 1);
   if (r >= n)
     return;
-  const double s = row_dot(rp, ci, v, x, d, r, lane);
+  const double s = row_dot<G>(rp, ci, v, x, d, r, lane);
   if (lane == 0)
     {
       const double dr = d ? d[r] : 0.0;
@@ -320,17 +328,18 @@ k_cheb_first(const double *__restrict__ f, const double *__restrict__ dinv, doub
 }
 
 // residual of the pending iterate: xo = x + d, r = f - A (x + d)
+template <int G>
 __global__ void __launch_bounds__(256)
   k_residual(const int32_t *__restrict__ rp, const int32_t *__restrict__ ci,
              const double *__restrict__ v, const double *__restrict__ x,
              const double *__restrict__ d, const double *__restrict__ f, double *__restrict__ xo,
              double *__restrict__ res, int64_t n)
 {
-  const int64_t r    = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int     lane = threadIdx.x & 63;
+  const int64_t r    = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  const int     lane = threadIdx.x & (G - 1);
   if (r >= n)
     return;
-  const double s = row_dot(rp, ci, v, x, d, r, lane);
+  const double s = row_dot<G>(rp, ci, v, x, d, r, lane);
   if (lane == 0)
     {
       xo[r]  = x[r] + d[r];
@@ -339,16 +348,17 @@ __global__ void __launch_bounds__(256)
 }
 
 // y = M x (add = 0) or y += M x (add = 1)
+template <int G>
 __global__ void __launch_bounds__(256)
   k_spmv(const int32_t *__restrict__ rp, const int32_t *__restrict__ ci,
          const double *__restrict__ v, const double *__restrict__ x, double *__restrict__ y,
          int add, int64_t n)
 {
-  const int64_t r    = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int     lane = threadIdx.x & 63;
+  const int64_t r    = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  const int     lane = threadIdx.x & (G - 1);
   if (r >= n)
     return;
-  const double s = row_dot(rp, ci, v, x, nullptr, r, lane);
+  const double s = row_dot<G>(rp, ci, v, x, nullptr, r, lane);
   if (lane == 0)
     y[r] = add ? y[r] + s : s;
 }
@@ -381,9 +391,9 @@ __global__ void __launch_bounds__(256)
 }
 
 dim3
-rows_grid(int64_t n)
+rows_grid(int64_t n, int G = 64)
 {
-  return dim3((unsigned)((n * 64 + 255) / 256));
+  return dim3((unsigned)((n * G + 255) / 256));
 }
 dim3
 elem_grid(int64_t n)
@@ -396,7 +406,24 @@ struct DevCSR
   int64_t  n = 0, nnz = 0;
   int32_t *rp = nullptr, *ci = nullptr;
   double  *v  = nullptr;
+  int      g  = 64; // lanes per row of its row kernels
 };
+
+// launch a row kernel K<G>(args...) with the matrix's lanes per row
+#define GLS_ROWS(K, M, st, ...)                                                               \
+  do                                                                                         \
+    {                                                                                        \
+      const DevCSR &m_ = (M);                                                                \
+      if (m_.g == 8)                                                                         \
+        hipLaunchKernelGGL(K<8>, rows_grid(m_.n, 8), dim3(256), 0, st, __VA_ARGS__);         \
+      else if (m_.g == 16)                                                                   \
+        hipLaunchKernelGGL(K<16>, rows_grid(m_.n, 16), dim3(256), 0, st, __VA_ARGS__);       \
+      else if (m_.g == 32)                                                                   \
+        hipLaunchKernelGGL(K<32>, rows_grid(m_.n, 32), dim3(256), 0, st, __VA_ARGS__);       \
+      else                                                                                   \
+        hipLaunchKernelGGL(K<64>, rows_grid(m_.n, 64), dim3(256), 0, st, __VA_ARGS__);       \
+    }                                                                                        \
+  while (0)
 
 template <typename T>
 void
@@ -415,6 +442,9 @@ to_device(const HostCSR &A)
   DevCSR               D;
   D.n   = A.n;
   D.nnz = A.rp.back();
+  // lanes per row: the smallest power of two >= 8 covering half a mean row
+  const double mean = A.n > 0 ? (double)D.nnz / (double)A.n : 0.0;
+  D.g               = mean > 96 ? 64 : mean > 48 ? 32 : mean > 24 ? 16 : 8;
   std::vector<int32_t> rp(A.rp.begin(), A.rp.end());
   upload_vec(&D.rp, rp);
   upload_vec(&D.ci, A.ci);
@@ -469,7 +499,8 @@ void
 chebyshev(glsAMG_ *amg, AmgLevel &L, bool zero_start, hipStream_t st)
 {
   const int    s   = std::max(1, amg->prm.smoother_sweeps);
-  const double b   = 1.1 * L.lambda, a = b / 30.0;
+  const double al  = amg->prm.chebyshev_alpha > 0 ? amg->prm.chebyshev_alpha : 10.0;
+  const double b   = 1.1 * L.lambda, a = b / al;
   const double th  = 0.5 * (b + a), de = 0.5 * (b - a), sg = th / de;
   double       rho = 1.0 / sg;
   const int64_t n  = L.A.n;
@@ -480,15 +511,15 @@ chebyshev(glsAMG_ *amg, AmgLevel &L, bool zero_start, hipStream_t st)
   else
     {
       // d = dinv (f - A x) / theta (pending part zero)
-      hipLaunchKernelGGL(k_cheb_step, rows_grid(n), dim3(256), 0, st, L.A.rp, L.A.ci, L.A.v, x,
-                         (const double *)nullptr, L.f, L.dinv, xo, dn, 0.0, 1.0 / th, n);
+      GLS_ROWS(k_cheb_step, L.A, st, L.A.rp, L.A.ci, L.A.v, x, (const double *)nullptr, L.f,
+               L.dinv, xo, dn, 0.0, 1.0 / th, n);
       std::swap(x, xo), std::swap(d, dn);
     }
   for (int k = 0; k < s; ++k) // s further steps, one matrix-vector product each
     {
       const double rn = 1.0 / (2.0 * sg - rho);
-      hipLaunchKernelGGL(k_cheb_step, rows_grid(n), dim3(256), 0, st, L.A.rp, L.A.ci, L.A.v, x, d,
-                         L.f, L.dinv, xo, dn, rn * rho, 2.0 * rn / de, n);
+      GLS_ROWS(k_cheb_step, L.A, st, L.A.rp, L.A.ci, L.A.v, x, d, L.f, L.dinv, xo, dn,
+               rn * rho, 2.0 * rn / de, n);
       std::swap(x, xo), std::swap(d, dn);
       rho = rn;
     }
@@ -522,10 +553,10 @@ vcycle_level(glsAMG_ *amg, size_t l, hipStream_t st)
   AmgLevel &C = amg->lv[l + 1];
   chebyshev(amg, L, true, st);
   // residual of x + d; x <- x + d
-  hipLaunchKernelGGL(k_residual, rows_grid(L.A.n), dim3(256), 0, st, L.A.rp, L.A.ci, L.A.v, L.x,
+  GLS_ROWS(k_residual, L.A, st, L.A.rp, L.A.ci, L.A.v, L.x,
                      L.d, L.f, L.x2, L.r, L.A.n);
   std::swap(L.x, L.x2);
-  hipLaunchKernelGGL(k_spmv, rows_grid(L.R.n), dim3(256), 0, st, L.R.rp, L.R.ci, L.R.v, L.r, C.f,
+  GLS_ROWS(k_spmv, L.R, st, L.R.rp, L.R.ci, L.R.v, L.r, C.f,
                      0, L.R.n);
   vcycle_level(amg, l + 1, st);
   const double *xc = C.x;
@@ -535,7 +566,7 @@ vcycle_level(glsAMG_ *amg, size_t l, hipStream_t st)
       hipLaunchKernelGGL(k_add2, elem_grid(C.A.n), dim3(256), 0, st, C.x, C.d, C.x2, C.A.n);
       xc = C.x2;
     }
-  hipLaunchKernelGGL(k_spmv, rows_grid(L.P.n), dim3(256), 0, st, L.P.rp, L.P.ci, L.P.v, xc, L.x, 1,
+  GLS_ROWS(k_spmv, L.P, st, L.P.rp, L.P.ci, L.P.v, xc, L.x, 1,
                      L.P.n);
   chebyshev(amg, L, false, st);
   HIP_THROW(hipGetLastError());

@@ -16,6 +16,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "op_internal.h"
+#include "cgs.h"
 
 #include <chrono>
 #include <string>
@@ -519,6 +520,8 @@ struct glsMG_
   const double *top_b64 = nullptr;
   double *cg_ws    = nullptr;
   void   *cg_lvl   = nullptr;
+  double *cg_host  = nullptr; // pinned: two Hessenberg columns (software pipeline)
+  hipEvent_t cg_ev[2] = {nullptr, nullptr};
   int     cg_iters = 0, cg_conv = 0;
   // "gmg coarse grid solver": "AMG" (desc.coarse_amg): the smoothed-
   // aggregation AMG on the coarse level's system matrix (amg.hip), rebuilt by
@@ -1296,7 +1299,11 @@ k_sub(double *__restrict__ r, const double *__restrict__ b, int64_t n)
 // relaxation sweeps or the dense LU).  FP64 Krylov vectors, the level
 // operator and preconditioner in the level precision (the reference solves
 // with the FP64 system matrix assembled from the MGNumber operator).  Every
-// vector stays on the device; per iteration the Hessenberg column crosses.
+// vector stays on the device.  The Arnoldi step runs as the outer solver's
+// (krylov.hip): fused CGS2 passes (cgs.h), |w| and v_{j+1} = w / |w| on the
+// device, and step j + 1 enqueued before the host waits for step j's
+// Hessenberg column (pinned, double-buffered), so the device never idles
+// through the host round trip; a converged solve runs one discarded step.
 template <typename T>
 void
 coarse_gmres_t(glsMG_ *mg, hipStream_t s)
@@ -1304,6 +1311,7 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
   glsOp         op = mg->ops[0];
   const int64_t n  = op->n_dofs;
   const int     m  = 28;
+  const int     HC = 2 * (m + 1) + 1; // both CGS passes' coefficients and |w|
   if (n > (int64_t)0x7fffffff)
     throw std::runtime_error("coarse GMRES: level too large for 32-bit rocBLAS sizes");
   if (!mg->blas)
@@ -1313,11 +1321,15 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
   rocblas_handle h = mg->blas;
   if (!mg->cg_ws)
     {
-      HIP_THROW(hipMalloc((void **)&mg->cg_ws, ((size_t)(m + 4) * n + 2 * (m + 1)) * 8));
+      HIP_THROW(hipMalloc((void **)&mg->cg_ws,
+                          ((size_t)(m + 4) * n + HC + (size_t)CGS_PART) * 8));
       HIP_THROW(hipMalloc(&mg->cg_lvl, (size_t)2 * n * sizeof(T)));
+      HIP_THROW(hipHostMalloc((void **)&mg->cg_host, (size_t)2 * HC * 8));
+      for (hipEvent_t &e : mg->cg_ev)
+        HIP_THROW(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
   double *V = mg->cg_ws, *w = V + (size_t)(m + 1) * n, *x = w + n, *b = x + n,
-         *dh = b + n;
+         *dh = b + n, *cpart = dh + HC;
   T *la = (T *)mg->cg_lvl, *lb = la + n;
   auto cvt_in = [&](T *dst, const double *src) {
     hipLaunchKernelGGL((k_convert<double, T>), g1(n), dim3(256), 0, s, dst, src, n);
@@ -1348,6 +1360,52 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
     return r;
   };
   auto vc = [&](int j) { return V + (size_t)j * n; };
+  // Arnoldi step j, enqueued only: v_{j+1} = P^{-1} A v_j orthogonalised
+  // (CGS2) and normalised on the device, its Hessenberg column to pinned
+  // host buffer j % 2 (event cg_ev[j % 2])
+  auto arnoldi = [&](int j) {
+    apply_A(w, vc(j));
+    double *wv = vc(j + 1);
+    prec(wv, w);
+    double *hn = dh + 2 * (m + 1);
+    const int J = j + 1;
+    if (J <= CGS_MAXJ)
+      {
+        hipLaunchKernelGGL(k_cgs_dots, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V, J,
+                           (const double *)wv, cpart, n, n);
+        hipLaunchKernelGGL(k_cgs_finish, dim3(J), dim3(256), 0, s, (const double *)cpart, dh, 0);
+        hipLaunchKernelGGL(k_cgs_update, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V, J,
+                           (const double *)dh, wv, cpart, n, n, n, 0);
+        hipLaunchKernelGGL(k_cgs_finish, dim3(J), dim3(256), 0, s, (const double *)cpart,
+                           dh + (m + 1), 0);
+        hipLaunchKernelGGL(k_cgs_update, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V, J,
+                           (const double *)(dh + (m + 1)), wv, cpart, n, n, n, 1);
+        hipLaunchKernelGGL(k_cgs_finish, dim3(1), dim3(256), 0, s, (const double *)cpart, hn, 1);
+        HIP_THROW(hipGetLastError());
+      }
+    else
+      {
+        const double one = 1.0, zero = 0.0, mone = -1.0;
+        for (int pass = 0; pass < 2; ++pass)
+          {
+            double *hp = dh + pass * (m + 1);
+            check_blas(rocblas_dgemv(h, rocblas_operation_transpose, (rocblas_int)n, J, &one, V,
+                                     (rocblas_int)n, wv, 1, &zero, hp, 1),
+                       "rocblas_dgemv");
+            check_blas(rocblas_dgemv(h, rocblas_operation_none, (rocblas_int)n, J, &mone, V,
+                                     (rocblas_int)n, hp, 1, &one, wv, 1),
+                       "rocblas_dgemv");
+          }
+        check_blas(rocblas_set_pointer_mode(h, rocblas_pointer_mode_device), "pointer mode");
+        check_blas(rocblas_dnrm2(h, (rocblas_int)n, wv, 1, hn), "rocblas_dnrm2");
+        check_blas(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host), "pointer mode");
+      }
+    HIP_THROW(hipMemcpyAsync(mg->cg_host + (j % 2) * HC, dh, HC * 8, hipMemcpyDeviceToHost, s));
+    HIP_THROW(hipEventRecord(mg->cg_ev[j % 2], s));
+    hipLaunchKernelGGL(k_unit_col, g1(n), dim3(256), 0, s, wv, (const double *)wv,
+                       (const double *)hn, n);
+    HIP_THROW(hipGetLastError());
+  };
   cvt_out(b, (const T *)mg->def[0]);
   HIP_THROW(hipMemsetAsync(x, 0, n * 8, s));
   // r0 = P^{-1} (b - A 0)
@@ -1355,7 +1413,7 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
   double       res = nrm2(vc(0));
   const double tol = std::max(mg->desc.coarse_reltol * res, 1e-20);
   int          it  = 0;
-  std::vector<double> H((size_t)(m + 1) * m), g(m + 1), cs(m), sn(m), hc(2 * (m + 1)), y(m);
+  std::vector<double> H((size_t)(m + 1) * m), g(m + 1), cs(m), sn(m), y(m);
   while (res > tol && it < mg->desc.coarse_maxiter)
     {
       const double sc = 1.0 / res;
@@ -1363,34 +1421,18 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
       std::fill(g.begin(), g.end(), 0.0);
       g[0]   = res;
       int jd = 0;
+      arnoldi(0);
       for (int j = 0; j < m && it < mg->desc.coarse_maxiter; ++j)
         {
-          apply_A(w, vc(j));   // w = A v_j
-          prec(vc(j + 1), w); // v_{j+1} = P^{-1} A v_j
-          double *wv = vc(j + 1);
-          const double one = 1.0, zero = 0.0, mone = -1.0;
-          for (int pass = 0; pass < 2; ++pass)
-            {
-              double *hp = dh + pass * (m + 1);
-              check_blas(rocblas_dgemv(h, rocblas_operation_transpose, (rocblas_int)n, j + 1,
-                                       &one, V, (rocblas_int)n, wv, 1, &zero, hp, 1),
-                         "rocblas_dgemv");
-              check_blas(rocblas_dgemv(h, rocblas_operation_none, (rocblas_int)n, j + 1, &mone, V,
-                                       (rocblas_int)n, hp, 1, &one, wv, 1),
-                         "rocblas_dgemv");
-            }
-          HIP_THROW(hipMemcpyAsync(hc.data(), dh, 2 * (m + 1) * 8, hipMemcpyDeviceToHost, s));
-          const double hn = nrm2(wv);
-          HIP_THROW(hipStreamSynchronize(s));
-          double *Hj = &H[(size_t)j * (m + 1)];
+          if (j + 1 < m && it + 1 < mg->desc.coarse_maxiter)
+            arnoldi(j + 1);
+          HIP_THROW(hipEventSynchronize(mg->cg_ev[j % 2]));
+          const double *hc = mg->cg_host + (j % 2) * HC;
+          const double  hn = hc[2 * (m + 1)];
+          double       *Hj = &H[(size_t)j * (m + 1)];
           for (int i = 0; i <= j; ++i)
             Hj[i] = hc[i] + hc[(m + 1) + i];
           Hj[j + 1] = hn;
-          if (hn > 0)
-            {
-              const double sc2 = 1.0 / hn;
-              check_blas(rocblas_dscal(h, (rocblas_int)n, &sc2, wv, 1), "rocblas_dscal");
-            }
           for (int i = 0; i < j; ++i)
             {
               const double t = cs[i] * Hj[i] + sn[i] * Hj[i + 1];
@@ -1801,6 +1843,11 @@ gls_mg_destroy(glsMG mg)
                   (void *)mg->d_free, (void *)mg->d_inv32, (void *)mg->cg_ws, mg->cg_lvl})
     if (p)
       (void)hipFree(p);
+  if (mg->cg_host)
+    (void)hipHostFree(mg->cg_host);
+  for (hipEvent_t ev : mg->cg_ev)
+    if (ev)
+      (void)hipEventDestroy(ev);
   if (mg->blas)
     rocblas_destroy_handle(mg->blas);
   if (mg->amg)

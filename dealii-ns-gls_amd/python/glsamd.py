@@ -71,16 +71,19 @@ class OpParams(C.Structure):
 class AMGParams(C.Structure):
     _fields_ = [("block_size", C.c_int), ("threshold", C.c_double),
                 ("smoother_sweeps", C.c_int), ("coarse_max_size", C.c_int),
-                ("elliptic", C.c_int), ("max_levels", C.c_int)]
+                ("elliptic", C.c_int), ("max_levels", C.c_int),
+                ("chebyshev_alpha", C.c_double)]
 
 
 def amg_params(block_size=1, threshold=1e-4, smoother_sweeps=2, coarse_max_size=2000,
-               elliptic=True, max_levels=10):
+               elliptic=True, max_levels=10, chebyshev_alpha=10.0):
     """glsAMGParams; the defaults are TrilinosWrappers::PreconditionAMG::
     AdditionalData()'s (one constant mode, threshold 1e-4, 2 smoother sweeps,
-    elliptic) with deal.II's "coarse: max size" 2000."""
+    elliptic) with the ML parameters deal.II sets ("coarse: max size" 2000,
+    "smoother: Chebyshev alpha" 10)."""
     return AMGParams(int(block_size), float(threshold), int(smoother_sweeps),
-                     int(coarse_max_size), int(bool(elliptic)), int(max_levels))
+                     int(coarse_max_size), int(bool(elliptic)), int(max_levels),
+                     float(chebyshev_alpha))
 
 
 class MGDesc(C.Structure):

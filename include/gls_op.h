@@ -297,6 +297,10 @@ typedef struct
   int    elliptic;        /* 1: smoothed prolongator (omega 4/3 / lambda);
                              0: tentative prolongator (non-elliptic)       */
   int    max_levels;      /* ML "max levels" (10)                            */
+  double chebyshev_alpha; /* ML "smoother: Chebyshev alpha": the smoother
+                             damps [lambda_max / alpha, lambda_max]; deal.II's
+                             PreconditionAMG sets 10 (ML's own default 30);
+                             <= 0: 10                                       */
 } glsAMGParams;
 /* PreconditionAMG::initialize(matrix, data): n x n CSR (host, int64
  * row_ptr[n + 1], cols / vals [nnz]); setup on the host, the hierarchy and

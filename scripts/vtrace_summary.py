@@ -8,16 +8,18 @@ path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/vtrace/run_kernel_trace
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 # a cycle starts at the finest level's first relaxation (k_relax_first or,
 # unfused, the copy_to_mg conversion)
+g_top = max([int(r["Grid_Size_X"]) for r in rows if "k_relax_first" in r["Kernel_Name"]] or [0])
 mark = [i for i, r in enumerate(rows)
-        if "k_relax_first" in r["Kernel_Name"] and int(r["Grid_Size_X"]) >= 800000
-        or "k_convert<double, float>" in r["Kernel_Name"]]
+        if "k_relax_first" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == g_top]
+if len(mark) < 2:  # unfused finest level: the copy_to_mg conversion
+    mark = [i for i, r in enumerate(rows) if "k_convert<double, float>" in r["Kernel_Name"]]
 a, b = mark[-2], mark[-1]
 cyc = rows[a:b]
 agg, tot = {}, 0
 for r in cyc:
     d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("gls::", "")
-    name = name.replace("(anonymous namespace)::", "")
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+    name = name.split("(")[0].replace("void ", "").replace("gls::", "")
     key = (name[:44], r["Grid_Size_X"])
     agg.setdefault(key, [0, 0])
     agg[key][0] += 1

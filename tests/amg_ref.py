@@ -8,7 +8,8 @@ published algorithm (csrc/amg.hip header): strength of connection on the
 block node graph, three-pass standard aggregation, constant-mode tentative
 prolongator, Jacobi-smoothed prolongator (omega 4/3 / lambda, 15 power
 iterations from a fixed start vector), Galerkin R A P, dense coarsest solve,
-Chebyshev smoothing of D^-1 A over [1.1 lambda / 30, 1.1 lambda]."""
+Chebyshev smoothing of D^-1 A over [1.1 lambda / alpha, 1.1 lambda] (alpha 10:
+the "smoother: Chebyshev alpha" deal.II passes to ML)."""
 import numpy as np
 import scipy.sparse as sp
 
@@ -78,8 +79,9 @@ def aggregate(A, b, theta):
 
 class AMGRef:
     def __init__(self, A, block_size=1, threshold=1e-4, smoother_sweeps=2,
-                 coarse_max_size=2000, elliptic=True, max_levels=10):
+                 coarse_max_size=2000, elliptic=True, max_levels=10, chebyshev_alpha=10.0):
         self.sweeps = smoother_sweeps
+        self.alpha = chebyshev_alpha if chebyshev_alpha > 0 else 10.0
         b = block_size
         A = sp.csr_matrix(A, dtype=np.float64)
         beta = np.ones(A.shape[0])
@@ -124,7 +126,7 @@ class AMGRef:
         # s + 1 Chebyshev steps; the zero start (x None) skips the product A 0
         s = max(1, self.sweeps)
         b = 1.1 * L["lam"]
-        a = b / 30.0
+        a = b / self.alpha
         th, de = 0.5 * (b + a), 0.5 * (b - a)
         sg = th / de
         rho = 1.0 / sg
