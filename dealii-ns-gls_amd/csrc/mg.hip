@@ -507,6 +507,10 @@ struct glsMG_
   rocblas_int   *d_info = nullptr;
   double        *d_rhs  = nullptr; // [(2 + GEMV_CHUNKS) nf]: rhs | solution | partials
   int32_t       *d_free = nullptr; // [nf] the free (unconstrained) coarse dofs
+  // [nf] the GEMV's input gather: the free dof whose entry multiplies column
+  // i of the stored inverse (free[p[i]] for the unpermuted U^-1 L^-1 of the
+  // trtri path, A^-1 = U^-1 L^-1 P^T; free[i] otherwise)
+  int32_t       *d_free_in = nullptr;
   int64_t        n_free = 0, ld_free = 0; // ld_free: nf rounded up to 4
   float         *d_inv32 = nullptr; // [nf][nf] FP32 copy of the inverse (inv_f32)
   bool           inv_f32 = false;
@@ -745,6 +749,18 @@ k_iota1(rocblas_int *p, int64_t n)
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n)
     p[i] = (rocblas_int)(i + 1);
+}
+
+// X = the unit lower triangle of the LU factors (column major n x n):
+// strictly lower entries copied, 1 on the diagonal, 0 above
+__global__ void
+k_unit_lower(double *__restrict__ X, const double *__restrict__ LU, int64_t n)
+{
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n * n)
+    return;
+  const int64_t c = k / n, r = k - c * n;
+  X[k]            = r > c ? LU[k] : (r == c ? 1.0 : 0.0);
 }
 
 // X[i][i] = 1 (column major n x n, X zeroed)
@@ -1070,6 +1086,7 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
       HIP_THROW(hipMalloc((void **)&mg->d_rhs,
                           (size_t)(2 + GEMV_CHUNKS) * mg->ld_free * sizeof(double)));
       HIP_THROW(hipMalloc((void **)&mg->d_free, (size_t)nf * sizeof(int32_t)));
+      HIP_THROW(hipMalloc((void **)&mg->d_free_in, (size_t)nf * sizeof(int32_t)));
       mg->n_free = nf;
     }
   if (mg->n_free != nf)
@@ -1123,13 +1140,18 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
                              std::to_string(info) + ")");
   // the inverse from the LU factors, once: every coarse solve is then one
   // GEMV streaming the nf x nf matrix at HBM rate (the two triangular solves
-  // of getrs ran 33.7 ms per V-cycle at n = 16,704 on MI355X; the GEMV,
-  // k_gemv_part, streams the matrix instead)
-  // GLS_COARSE_INVERT=getri: rocsolver_dgetri in place; default: getrs with
-  // the identity as right-hand side (two triangular solves of nf columns,
-  // rocBLAS trsm) into a second nf x nf buffer that then replaces the factors
+  // of getrs ran 33.7 ms per V-cycle at n = 16,704 on MI355X).  Default
+  // (GLS_COARSE_INVERT unset or "trtri"): Z = U^-1 L^-1 from the unit lower
+  // factor inverted in place (rocsolver_dtrtri, n^3 / 3 flops) and one
+  // triangular solve with U (rocblas_dtrsm, n^3): 4/3 n^3 instead of the
+  // 2 n^3 of getrs with the identity, and A^-1 = Z P^T needs no column
+  // permutation of the matrix: the GEMV gathers its input through free[p[i]]
+  // (d_free_in).  "getrs": the identity as right-hand side (rocsolver
+  // dgetrs); "getri": rocsolver_dgetri in place.
+  std::vector<int32_t> fin = freel; // the GEMV's input gather
   const char *ci = getenv("GLS_COARSE_INVERT");
-  if (ci && std::string(ci) == "getri")
+  const std::string inv_mode = ci ? ci : "trtri";
+  if (inv_mode == "getri")
     {
       check_blas(rocsolver_dgetri(mg->blas, (rocblas_int)nf, mg->d_lu, (rocblas_int)nf,
                                   mg->d_ipiv, mg->d_info),
@@ -1142,17 +1164,54 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
     }
   else
     {
-      double *X = nullptr;
+      const bool trtri = inv_mode != "getrs";
+      double    *X     = nullptr;
       HIP_THROW(hipMalloc((void **)&X, (size_t)nf * nf * sizeof(double)));
-      HIP_THROW(hipMemsetAsync(X, 0, (size_t)nf * nf * sizeof(double), s));
-      hipLaunchKernelGGL(k_set_diag, g1(nf), dim3(256), 0, s, X, nf);
-      HIP_THROW(hipGetLastError());
       try
         {
-          check_blas(rocsolver_dgetrs(mg->blas, rocblas_operation_none, (rocblas_int)nf,
-                                      (rocblas_int)nf, mg->d_lu, (rocblas_int)nf, mg->d_ipiv, X,
-                                      (rocblas_int)nf),
-                     "rocsolver_dgetrs");
+          if (trtri)
+            {
+              hipLaunchKernelGGL(k_unit_lower, g1(nf * nf), dim3(256), 0, s, X,
+                                 (const double *)mg->d_lu, nf);
+              HIP_THROW(hipGetLastError());
+              check_blas(rocsolver_dtrtri(mg->blas, rocblas_fill_lower, rocblas_diagonal_unit,
+                                          (rocblas_int)nf, X, (rocblas_int)nf, mg->d_info),
+                         "rocsolver_dtrtri");
+              const double one = 1.0;
+              check_blas(rocblas_set_pointer_mode(mg->blas, rocblas_pointer_mode_host),
+                         "pointer mode");
+              check_blas(rocblas_dtrsm(mg->blas, rocblas_side_left, rocblas_fill_upper,
+                                       rocblas_operation_none, rocblas_diagonal_non_unit,
+                                       (rocblas_int)nf, (rocblas_int)nf, &one, mg->d_lu,
+                                       (rocblas_int)nf, X, (rocblas_int)nf),
+                         "rocblas_dtrsm");
+              // P^T from the pivots (1-based row interchanges, in order)
+              std::vector<rocblas_int> ip((size_t)nf);
+              HIP_THROW(hipMemcpyAsync(ip.data(), mg->d_ipiv, (size_t)nf * sizeof(rocblas_int),
+                                       hipMemcpyDeviceToHost, s));
+              HIP_THROW(hipMemcpyAsync(&info, mg->d_info, sizeof(info), hipMemcpyDeviceToHost, s));
+              HIP_THROW(hipStreamSynchronize(s));
+              if (info != 0)
+                throw std::runtime_error("dense LU coarse solver: singular unit factor (info " +
+                                         std::to_string(info) + ")");
+              std::vector<int32_t> p((size_t)nf);
+              for (int64_t i = 0; i < nf; ++i)
+                p[(size_t)i] = (int32_t)i;
+              for (int64_t j = 0; j < nf; ++j)
+                std::swap(p[(size_t)j], p[(size_t)ip[(size_t)j] - 1]);
+              for (int64_t i = 0; i < nf; ++i)
+                fin[(size_t)i] = freel[(size_t)p[(size_t)i]];
+            }
+          else
+            {
+              HIP_THROW(hipMemsetAsync(X, 0, (size_t)nf * nf * sizeof(double), s));
+              hipLaunchKernelGGL(k_set_diag, g1(nf), dim3(256), 0, s, X, nf);
+              HIP_THROW(hipGetLastError());
+              check_blas(rocsolver_dgetrs(mg->blas, rocblas_operation_none, (rocblas_int)nf,
+                                          (rocblas_int)nf, mg->d_lu, (rocblas_int)nf, mg->d_ipiv,
+                                          X, (rocblas_int)nf),
+                         "rocsolver_dgetrs");
+            }
           HIP_THROW(hipStreamSynchronize(s));
         }
       catch (...)
@@ -1163,6 +1222,8 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
       HIP_THROW(hipFree(mg->d_lu));
       mg->d_lu = X;
     }
+  HIP_THROW(hipMemcpyAsync(mg->d_free_in, fin.data(), (size_t)nf * sizeof(int32_t),
+                           hipMemcpyHostToDevice, s));
   const auto t3 = std::chrono::steady_clock::now();
   auto       ms = [](auto a, auto b) {
     return std::chrono::duration<double, std::milli>(b - a).count();
@@ -1205,7 +1266,7 @@ coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
       // identity), then sol[free] = A_ff^{-1} def[free], one wave per row
       float *xf = reinterpret_cast<float *>(mg->d_rhs);
       hipLaunchKernelGGL(k_coarse_prep<T>, g1(std::max(n, ld)), dim3(256), 0, s, (T *)mg->sol[0],
-                         (const T *)mg->def[0], xf, (const int32_t *)mg->d_free, n, nf, ld);
+                         (const T *)mg->def[0], xf, (const int32_t *)mg->d_free_in, n, nf, ld);
       // the inverse is read once per solve and is larger than the MALL:
       // non-temporal row loads (GLS_GEMV_NT=0: default policy)
       static const bool nt = [] {
@@ -1226,7 +1287,7 @@ coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
   // constrained dofs: x_c = b_c (their rows of A are the identity)
   copy_words(mg->sol[0], mg->def[0], n * (int64_t)sizeof(T) / 4, s);
   hipLaunchKernelGGL(k_gather_free<T>, g1(nf), dim3(256), 0, s, mg->d_rhs,
-                     (const T *)mg->def[0], (const int32_t *)mg->d_free, nf);
+                     (const T *)mg->def[0], (const int32_t *)mg->d_free_in, nf);
   double *part = mg->d_rhs + 2 * ld;
   hipLaunchKernelGGL(k_gemv_part<double>, dim3((unsigned)((nf + 255) / 256), GEMV_CHUNKS),
                      dim3(256), 0, s, (const double *)mg->d_lu, (const double *)mg->d_rhs, part,
@@ -1840,7 +1901,8 @@ gls_mg_destroy(glsMG mg)
   for (hipEvent_t ev : mg->side_ev)
     (void)hipEventDestroy(ev);
   for (void *p : {(void *)mg->d_lu, (void *)mg->d_ipiv, (void *)mg->d_info, (void *)mg->d_rhs,
-                  (void *)mg->d_free, (void *)mg->d_inv32, (void *)mg->cg_ws, mg->cg_lvl})
+                  (void *)mg->d_free, (void *)mg->d_free_in, (void *)mg->d_inv32,
+                  (void *)mg->cg_ws, mg->cg_lvl})
     if (p)
       (void)hipFree(p);
   if (mg->cg_host)

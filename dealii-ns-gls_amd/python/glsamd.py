@@ -834,12 +834,13 @@ class Multigrid:
         return it.value, bool(cv.value)
 
     def coarse_setup_times(self):
-        """{assembly_ms, getrf_ms, getri_ms, colors} of the last dense-coarse
-        setup (coarse_n_iterations=-1)."""
+        """{assembly_ms, getrf_ms, inverse_ms, colors} of the last dense-coarse
+        setup (coarse_n_iterations=-1); inverse_ms: the inverse from the LU
+        factors (trtri + trsm by default, GLS_COARSE_INVERT)."""
         ms = (C.c_double * 3)()
         nc = C.c_int()
         _check(lib().gls_mg_coarse_setup_times(self.h, ms, C.byref(nc)))
-        return {"assembly_ms": ms[0], "getrf_ms": ms[1], "getri_ms": ms[2],
+        return {"assembly_ms": ms[0], "getrf_ms": ms[1], "inverse_ms": ms[2],
                 "colors": nc.value}
 
     def coarse_amg(self):

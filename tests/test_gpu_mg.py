@@ -295,3 +295,37 @@ def test_vcycle_graph_replay(prec, coarse, memnodes, monkeypatch):
     tol = 1e-12 if prec == "f64" else max(1e-6, 20 * d_ee)
     assert d_ge < tol
     assert it_g == it_e and rel_err(x_g, x_e) < (1e-10 if prec == "f64" else 1e-5)
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_coarse_inverse_trtri_vs_getrs(prec, monkeypatch):
+    """The dense coarse solver's inverse (multigrid.cc:448-455 substitute):
+    the default Z = U^-1 L^-1 (rocsolver_dtrtri + rocblas_dtrsm, pivots
+    applied to the GEMV's input gather) against getrs with the identity
+    (the round-3 path), on the headline hierarchy r0..r2: the V-cycles agree
+    to the FP64 rounding of two orderings of the same inverse (FP64 levels,
+    5e-12)
+    and to the FP32 storage of the inverse (FP32 levels); the setup times of
+    both are printed."""
+    import torch
+    import glsamd
+    meshes, cmasks, params, w, u, hist = _hierarchy("input_hoffmann_3D_Re3900.json", 2)
+    b = gi.rnd(31, meshes[-1].n_dofs)
+    out = {}
+    for mode in ("getrs", "trtri"):
+        monkeypatch.setenv("GLS_COARSE_INVERT", mode)
+        mg, _ = glsamd.build_gmg(meshes, cmasks, params, u, hist, w, precision=prec,
+                                 coarse_n_iterations=-1)
+        src = torch.from_numpy(b).cuda()
+        dst = torch.zeros_like(src)
+        mg.vcycle(dst, src)
+        torch.cuda.synchronize()
+        out[mode] = (_np(dst), mg.coarse_setup_times())
+        del mg
+    err = rel_err(out["trtri"][0], out["getrs"][0])
+    print(f"{prec}: trtri vs getrs V-cycle {err:.2e}; setup getrs {out['getrs'][1]}, "
+          f"trtri {out['trtri'][1]}")
+    # FP64: two orderings of the same inverse of a coarse matrix whose FP64 LU
+    # already differs from the oracle's numpy LU by ~4e-12 in the V-cycle
+    # (test_vcycle_re3900_f64_levels_tight[-1]); measured 1.15e-12
+    assert err < (5e-12 if prec == "f64" else 1e-6)
