@@ -904,7 +904,10 @@ def main():
                          "kernel": "vmult = gls::k_brick<3,2,double,MODE_NEWTON> + "
                                    "gls::k_shared_reduce_cls (both inside the events)",
                          "kernel_ms": kernel_ms, "algorithmic_bytes": bytes_per_vmult,
-                         "streamed_bytes": op.vmult_bytes()},
+                         "streamed_bytes": op.vmult_bytes(),
+                         # the same launch time against what the kernel reads
+                         # (16 instead of SURVEY's 20 table values per q)
+                         "frac_streamed": op.vmult_bytes() / (kernel_ms * 1e-3) / HBM_PEAK},
             "cpu_baseline": cpu,
             "parity": parity,
             "companions": comp if dist_comp is None else dict(comp or {}, **dist_comp),

@@ -59,6 +59,19 @@ lds_add(T *p, T v)
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// multiplicity class of partial slot `slot` (the shared nodes are ordered by
+// class, build_bricks): the node's slots are slot0 + j m + [0, m)
+__device__ __forceinline__ int
+slot_class(const ReduceClasses &rc, uint32_t slot)
+{
+  int kc = 0;
+#pragma unroll
+  for (int j = 1; j < ReduceClasses::MAX; ++j)
+    if (j < rc.n && slot >= rc.slot0[j])
+      kc = j;
+  return kc;
+}
+
 // 16-byte LDS packs of solution components: the sum-factorisation sweeps
 // move (dim+1) components as ceil((dim+1)/W) ds_read_b128 / ds_write_b128
 // instead of one 8-byte access per component (and no ds_read2_b64, which
@@ -105,6 +118,19 @@ struct BrickArgs
   T               romega;
   int             rkeep; // 1: src + omega rd (rb - A src); 0: omega rd (rb - A src)
                          // (rd null: 1) — the multigrid residual b - A x
+  // deferred shared-node reduction (FP32 3D smoothing levels):
+  // with qslots set, src's brick-boundary rows are not in memory: each is
+  // the previous apply's reduction, rebuilt in the gather exactly as
+  // k_shared_reduce_cls would have written it -- its partial slots (qslots,
+  // slot ranges from rc), the iterate before it (qprev) and that step's
+  // relaxation (qb, qd, qomega, keep 1) -- and stored into src (qsrc_w)
+  const T        *qslots;
+  const T        *qprev;
+  const T        *qb;
+  const T        *qd;
+  T               qomega;
+  T              *qsrc_w;
+  ReduceClasses   rc;
   int64_t         brick_begin, brick_end;
   int             bx, by, bz;
   int             L, Lx, Ly;
@@ -575,12 +601,54 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
   // the staging then waits for the gather only.
   const int Lxy = a.Lx * a.Ly;
   T         u[NI][nc];
+  // deferred reduction of the previous apply (one 16-byte pack per node)
+  constexpr bool QREC = sizeof(T) == 4 && !R && nc * sizeof(T) == 16;
 #pragma unroll
   for (int it = 0; it < NI; ++it)
     {
-      const int i = t + it * BLOCK;
-      if (i < L && (pk[it] & NODE_MASK) != UNUSED_NODE)
-        load_node<T, nc>(a.src, pk[it] & NODE_MASK, u[it]);
+      const int      i    = t + it * BLOCK;
+      const uint32_t node = pk[it] & NODE_MASK;
+      if (QREC && i < L && node != UNUSED_NODE && a.qslots && (tg[it] & SHARED_BIT))
+        {
+          // the previous apply's shared-node reduction of this node, in
+          // k_shared_reduce_cls's order and arithmetic (bitwise the same)
+          const uint32_t slt = tg[it] & ~SHARED_BIT;
+          const int      kc  = slot_class(a.rc, slt);
+          const uint32_t m   = a.rc.mult[kc];
+          const uint32_t b0  = a.rc.slot0[kc] + (slt - a.rc.slot0[kc]) / m * m;
+          const V       *pp  = reinterpret_cast<const V *>(a.qslots);
+          V              sum = {};
+          uint32_t       j   = 0;
+          for (; j + 4 <= m; j += 4)
+            {
+              const V x0 = pp[b0 + j], x1 = pp[b0 + j + 1], x2 = pp[b0 + j + 2],
+                      x3 = pp[b0 + j + 3];
+              sum += (x0 + x1) + (x2 + x3);
+            }
+          if (j + 2 <= m)
+            {
+              const V x0 = pp[b0 + j], x1 = pp[b0 + j + 1];
+              sum += x0 + x1;
+              j += 2;
+            }
+          if (j < m)
+            sum += pp[b0 + j];
+          const V        xs = reinterpret_cast<const V *>(a.qprev)[node];
+          const V        bb = reinterpret_cast<const V *>(a.qb)[node];
+          const V        dd = a.qd ? reinterpret_cast<const V *>(a.qd)[node] : V{} + T(1);
+          const uint32_t cm = pk[it] >> 28;
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            if ((cm >> w) & 1)
+              sum[w] = xs[w];
+          const V v = xs + a.qomega * dd * (bb - sum);
+          reinterpret_cast<V *>(a.qsrc_w)[node] = v;
+#pragma unroll
+          for (int c = 0; c < nc; ++c)
+            u[it][c] = v[c % W];
+        }
+      else if (i < L && node != UNUSED_NODE)
+        load_node<T, nc>(a.src, node, u[it]);
       else
 #pragma unroll
         for (int c = 0; c < nc; ++c)

@@ -706,11 +706,22 @@ struct Impl
         a.old_grad      = (const T *)op->d_old_grad;
         a.dst           = (T *)dst;
         a.src           = (const T *)src;
-        a.partial       = (T *)op->d_partial;
+        a.partial       = (T *)(rx && rx->partial ? rx->partial : op->d_partial);
         a.rb            = rx ? (const T *)rx->b : nullptr;
         a.rd            = rx ? (const T *)rx->d : nullptr;
         a.romega        = rx ? (T)rx->omega : T(0);
         a.rkeep         = rx ? (rx->keep ? 1 : 0) : 1;
+        a.qslots        = rx ? (const T *)rx->prev_partial : nullptr;
+        a.qprev         = rx ? (const T *)rx->prev_src : nullptr;
+        a.qb            = rx ? (const T *)rx->prev_b : nullptr;
+        a.qd            = rx ? (const T *)rx->prev_d : nullptr;
+        a.qomega        = rx ? (T)rx->prev_omega : T(0);
+        a.qsrc_w        = (T *)src;
+        a.rc            = op->reduce_classes;
+        if (a.qslots && !(sizeof(T) == 4 && dim == 3 && op->reduce_classes.n > 0))
+          throw std::runtime_error("deferred shared-node reduction: FP32 3D brick levels only");
+        if (rx && rx->defer)
+          what &= ~BRICK_REDUCE;
         a.brick_begin   = b0;
         a.brick_end     = b1;
         a.bx            = op->bx;
@@ -797,20 +808,20 @@ struct Impl
             const uint32_t      *offs = op->d_shared_off + r0;
             if (rc.n > 0 && mode == MODE_RESIDUAL)
               hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, true>), g3, dim3(256), 0, s,
-                                 (T *)dst, (const T *)src, (const T *)op->d_partial, nods, rc,
+                                 (T *)dst, (const T *)src, (const T *)a.partial, nods, rc,
                                  nr);
             else if (rc.n > 0)
               hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, false>), g3, dim3(256), 0, s,
-                                 (T *)dst, (const T *)src, (const T *)op->d_partial, nods, rc,
+                                 (T *)dst, (const T *)src, (const T *)a.partial, nods, rc,
                                  nr, a.rb, a.rd, a.romega, a.rkeep,
                                  (uint32_t)op->n_owned_nodes);
             else if (mode == MODE_RESIDUAL)
               hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, true>), g2, dim3(256), 0, s,
-                                 (T *)dst, (const T *)src, (const T *)op->d_partial, nods, offs,
+                                 (T *)dst, (const T *)src, (const T *)a.partial, nods, offs,
                                  nr);
             else
               hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, false>), g2, dim3(256), 0, s,
-                                 (T *)dst, (const T *)src, (const T *)op->d_partial, nods, offs,
+                                 (T *)dst, (const T *)src, (const T *)a.partial, nods, offs,
                                  nr, a.rb, a.rd, a.romega, a.rkeep,
                                  (uint32_t)op->n_owned_nodes);
             HIP_THROW(hipGetLastError());

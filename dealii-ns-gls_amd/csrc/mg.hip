@@ -477,6 +477,11 @@ struct glsMG_
   std::vector<uint32_t *> d_child;  // level l >= 1: [cells(l-1)][nl]
   std::vector<void *>     d_weight; // level l >= 1: [n_dofs(l)]
   std::vector<void *>     invdiag, sol, def, tmp;
+  // deferred shared-node reductions of the smoother (smooth): per level two
+  // partial-slot buffers the applies alternate between (beside the
+  // operator's own, which the residual and the explicit reductions use);
+  // GLS_MG_DEFER=0 reduces after every apply instead
+  std::vector<void *>     qslot[2];
   std::vector<double>     omega, lambda;
   // power iteration: per level, block partials | 2 scalars (the levels'
   // estimates run concurrently, gls_mg_setup)
@@ -512,6 +517,17 @@ struct glsMG_
   // trtri path, A^-1 = U^-1 L^-1 P^T; free[i] otherwise)
   int32_t       *d_free_in = nullptr;
   int64_t        n_free = 0, ld_free = 0; // ld_free: nf rounded up to 4
+  // static condensation of the cells' interior dofs (coarse_lu_setup_t):
+  // the dense inverse covers the remaining free dofs only; per cell
+  // C = E_II^-1 [ni][ni], F = E_BI E_II^-1 [nb][ni], G = E_II^-1 E_IB [ni][nb]
+  // (constrained boundary dofs: zero rows / columns), the interior / boundary
+  // dofs' global indices (-1: constrained), y = C b_I per solve, and per GEMV
+  // column i the (cell, boundary slot) pairs of its dof (CSR)
+  bool           cond = false;
+  int            cond_ni = 0, cond_nb = 0;
+  std::vector<int32_t> cond_lint, cond_lbnd; // local interior / boundary dofs of a cell
+  double        *d_cC = nullptr, *d_cF = nullptr, *d_cG = nullptr, *d_cy = nullptr;
+  int32_t       *d_cint = nullptr, *d_cbnd = nullptr, *d_rg_off = nullptr, *d_rg_ent = nullptr;
   float         *d_inv32 = nullptr; // [nf][nf] FP32 copy of the inverse (inv_f32)
   bool           inv_f32 = false;
   // last dense-coarse setup: assembly / getrf / getri wall ms, cell colours
@@ -650,6 +666,27 @@ relax_first_t(const glsMG_ *mg, int level, void *x, void *b, const FirstRelax &f
   HIP_THROW(hipGetLastError());
 }
 
+// the last apply of a smoothing sequence whose shared-node reduction is
+// still pending (deferred): its slots, its src (the iterate before) and its
+// relaxation
+struct PendingReduce
+{
+  const void *slots = nullptr, *src = nullptr, *b = nullptr, *d = nullptr;
+  double      omega = 0.0;
+  bool        valid = false;
+};
+
+bool
+defer_reduce(const glsMG_ *mg, int level)
+{
+  static const bool on = [] {
+    const char *e = getenv("GLS_MG_DEFER");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on && gls::deferred_reduce_ok(mg->ops[level]) && mg->qslot[0].size() > (size_t)level &&
+         mg->qslot[0][(size_t)level];
+}
+
 // PreconditionRelaxation::vmult (zero start) / step, `iters` iterations;
 // the result in x.  x_in (step only): the starting iterate is in tmp[level]
 // instead of x (the multigrid's out-of-place prolongation put it there).
@@ -657,7 +694,8 @@ relax_first_t(const glsMG_ *mg, int level, void *x, void *b, const FirstRelax &f
 // was none (iters == 0), so the caller does that work itself
 bool
 smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int iters,
-       hipStream_t s, bool start_in_tmp = false, const FirstRelax *fr = nullptr)
+       hipStream_t s, bool start_in_tmp = false, const FirstRelax *fr = nullptr,
+       PendingReduce *pend = nullptr)
 {
   auto  relax = mg->prec == GLS_F64 ? relax_t<double> : relax_t<float>;
   auto  first = [&](void *xx) {
@@ -706,12 +744,44 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
   rx.b     = b;
   rx.d     = mg->invdiag[level];
   rx.omega = mg->omega[level];
+  // deferred reductions: apply j writes its boundary partials to slot
+  // buffer j % 2 and skips its reduction; apply j + 1 rebuilds those rows in
+  // its gather (and stores them into its src); the last apply's reduction
+  // runs explicitly below, or is handed to the caller (pend), whose next
+  // apply of the operator to x rebuilds it the same way
+  const bool    defer = defer_reduce(mg, level);
+  PendingReduce pr;
   for (; it < iters; ++it)
     {
-      void *oth = cur == x ? tmp : x;
+      void          *oth = cur == x ? tmp : x;
+      gls::RelaxStep r   = rx;
+      if (defer)
+        {
+          r.defer   = true;
+          r.partial = mg->qslot[it % 2][(size_t)level];
+          if (pr.valid)
+            {
+              r.prev_partial = pr.slots, r.prev_src = pr.src;
+              r.prev_b = pr.b, r.prev_d = pr.d, r.prev_omega = pr.omega;
+            }
+        }
       gls::brick_launch(op, gls::op_vmult_mode(op), oth, cur, 0, op->n_bricks,
-                        gls::BRICK_RUN | gls::BRICK_REDUCE, s, &rx);
+                        gls::BRICK_RUN | gls::BRICK_REDUCE, s, &r);
+      if (defer)
+        pr = PendingReduce{r.partial, cur, rx.b, rx.d, rx.omega, true};
       cur = oth;
+    }
+  if (pr.valid)
+    {
+      if (pend && cur == x)
+        *pend = pr;
+      else
+        {
+          gls::RelaxStep r = rx;
+          r.partial        = const_cast<void *>(pr.slots);
+          gls::brick_launch(op, gls::op_vmult_mode(op), cur, pr.src, 0, 0, gls::BRICK_REDUCE, s,
+                            &r);
+        }
     }
   if (cur != x)
     {
@@ -937,6 +1007,169 @@ k_narrow(float *__restrict__ out, const double *__restrict__ in, int64_t n, int6
   out[e] = j < n ? (float)in[j * n + i] : 0.0f;
 }
 
+// Static condensation of the cells' interior dofs, one workgroup per cell:
+// from the element matrix E (column major per cell: E[c][j][i] = entry
+// (i, j)) with interior local dofs lint[ni] and boundary local dofs
+// lbnd[nb] (free[b] = 0: a constrained boundary dof, its couplings dropped
+// as the assembly drops them), C = E_II^-1 (Gauss-Jordan with partial
+// pivoting, FP64), F = E_BI C, G = C E_IB, and the element Schur complement
+// S = E_BB - F E_IB (column major [c][b2][b1]), assembled like E.
+constexpr int COND_MAXI = 32;
+template <typename T>
+__global__ void __launch_bounds__(256)
+  k_condense(const T *__restrict__ E, int ndof, const int32_t *__restrict__ lint, int ni,
+             const int32_t *__restrict__ lbnd, int nb, const int32_t *__restrict__ bfree,
+             double *__restrict__ S, double *__restrict__ Cm, double *__restrict__ F,
+             double *__restrict__ G)
+{
+  __shared__ double a[COND_MAXI][2 * COND_MAXI];
+  __shared__ double f[128 * COND_MAXI / 4]; // F rows of this cell (nb <= 128, ni <= 8)
+  const int64_t c   = blockIdx.x;
+  const size_t  per = (size_t)ndof * ndof;
+  const T      *Ec  = E + (size_t)c * per;
+  auto          e   = [&](int row, int col) { return (double)Ec[(size_t)col * ndof + row]; };
+  const int     t   = threadIdx.x;
+  const int32_t *fr = bfree + (size_t)c * nb;
+  // [E_II | I] in LDS, then Gauss-Jordan by one thread (ni <= COND_MAXI)
+  for (int k = t; k < ni * 2 * ni; k += blockDim.x)
+    {
+      const int r = k / (2 * ni), q = k % (2 * ni);
+      a[r][q] = q < ni ? e(lint[r], lint[q]) : (q - ni == r ? 1.0 : 0.0);
+    }
+  __syncthreads();
+  if (t == 0)
+    for (int col = 0; col < ni; ++col)
+      {
+        int piv = col;
+        for (int r = col + 1; r < ni; ++r)
+          if (fabs(a[r][col]) > fabs(a[piv][col]))
+            piv = r;
+        if (piv != col)
+          for (int q = 0; q < 2 * ni; ++q)
+            {
+              const double x = a[col][q];
+              a[col][q]      = a[piv][q];
+              a[piv][q]      = x;
+            }
+        const double d = 1.0 / a[col][col];
+        for (int q = 0; q < 2 * ni; ++q)
+          a[col][q] *= d;
+        for (int r = 0; r < ni; ++r)
+          if (r != col)
+            {
+              const double m = a[r][col];
+              for (int q = 0; q < 2 * ni; ++q)
+                a[r][q] -= m * a[col][q];
+            }
+      }
+  __syncthreads();
+  double *Cc = Cm + (size_t)c * ni * ni, *Fc = F + (size_t)c * nb * ni, *Gc = G + (size_t)c * ni * nb;
+  for (int k = t; k < ni * ni; k += blockDim.x)
+    Cc[k] = a[k / ni][ni + k % ni];
+  // F[b][k] = sum_m E_BI(b, m) C(m, k); G[k][b] = sum_m C(k, m) E_IB(m, b)
+  for (int k = t; k < nb * ni; k += blockDim.x)
+    {
+      const int b = k / ni, kk = k % ni;
+      double    sf = 0, sg = 0;
+      if (fr[b])
+        for (int m = 0; m < ni; ++m)
+          {
+            sf += e(lbnd[b], lint[m]) * a[m][ni + kk];
+            sg += a[kk][ni + m] * e(lint[m], lbnd[b]);
+          }
+      Fc[(size_t)b * ni + kk] = sf;
+      f[b * ni + kk]          = sf;
+      Gc[(size_t)kk * nb + b] = sg;
+    }
+  __syncthreads();
+  // S[b2][b1] = E_BB(b1, b2) - sum_k F[b1][k] E_IB(k, b2)
+  double *Sc = S + (size_t)c * nb * nb;
+  for (int k = t; k < nb * nb; k += blockDim.x)
+    {
+      const int b2 = k / nb, b1 = k % nb;
+      double    v  = e(lbnd[b1], lbnd[b2]);
+      if (fr[b2])
+        for (int m = 0; m < ni; ++m)
+          v -= f[b1 * ni + m] * e(lint[m], lbnd[b2]);
+      Sc[k] = v;
+    }
+}
+
+// y[c][k] = sum_m C[c][k][m] def[int[c][m]] (FP64), one thread per (cell, k)
+template <typename T>
+__global__ void
+k_cond_y(double *__restrict__ y, const double *__restrict__ Cm, const T *__restrict__ def,
+         const int32_t *__restrict__ cint, int ni, int64_t n_cells)
+{
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_cells * ni)
+    return;
+  const int64_t c = g / ni;
+  const int     k = (int)(g - c * ni);
+  double        v = 0;
+  for (int m = 0; m < ni; ++m)
+    v += Cm[((size_t)c * ni + k) * ni + m] * (double)def[cint[(size_t)c * ni + m]];
+  y[g] = v;
+}
+
+// the condensed right-hand side of GEMV column i: b_S[rin[i]] = def[rin[i]]
+// - sum over its (cell, slot) pairs of F[c][slot] . b_I[c] (F = E_BI C
+// already holds C, so the cell's interior right-hand side enters as is);
+// sol = def on every dof (the constrained rows keep it); out padded to ld
+// with zeros
+template <typename T, typename O>
+__global__ void
+k_cond_rhs(T *__restrict__ sol, const T *__restrict__ def, O *__restrict__ out,
+           const int32_t *__restrict__ rin, const int32_t *__restrict__ off,
+           const int32_t *__restrict__ ent, const double *__restrict__ F,
+           const int32_t *__restrict__ cint, int ni, int nb, int64_t n, int64_t nr, int64_t ld)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    sol[i] = def[i];
+  if (i >= ld)
+    return;
+  if (i >= nr)
+    {
+      out[i] = O(0);
+      return;
+    }
+  double v = (double)def[rin[i]];
+  for (int32_t e = off[i]; e < off[i + 1]; ++e)
+    {
+      const int32_t cs = ent[e]; // cell * nb + slot
+      const int64_t c  = cs / nb;
+      const double  *f  = F + (size_t)cs * ni;
+      const int32_t *ic = cint + (size_t)c * ni;
+      for (int m = 0; m < ni; ++m)
+        v -= f[m] * (double)def[ic[m]];
+    }
+  out[i] = (O)v;
+}
+
+// the interior dofs from the boundary solution: x_I = y - G x_B
+template <typename T>
+__global__ void
+k_cond_post(T *__restrict__ sol, const double *__restrict__ y, const double *__restrict__ G,
+            const int32_t *__restrict__ cint, const int32_t *__restrict__ cbnd, int ni, int nb,
+            int64_t n_cells)
+{
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_cells * ni)
+    return;
+  const int64_t c  = g / ni;
+  const int     k  = (int)(g - c * ni);
+  const double *gr = G + ((size_t)c * ni + k) * nb;
+  double        v  = y[g];
+  for (int b = 0; b < nb; ++b)
+    {
+      const int32_t d = cbnd[(size_t)c * nb + b];
+      if (d >= 0)
+        v -= gr[b] * (double)sol[d];
+    }
+  sol[cint[g]] = (T)v;
+}
+
 // A_ff[fj][fi] += E[c][j][i] over the cells of one colour (no two of them
 // share a node, so no two threads of a launch touch the same entry): the
 // element matrices scattered into the column-major free-dof block, the
@@ -1028,15 +1261,78 @@ assemble_free_block(glsMG_ *mg, const std::vector<int32_t> &freel, hipStream_t s
                            hipMemcpyHostToDevice, s));
   gls::op_element_matrices_device(op, E, 0, nc_, s);
   HIP_THROW(hipMemsetAsync(mg->d_lu, 0, (size_t)nf * nf * sizeof(double), s));
-  const int64_t per = (int64_t)ndof * ndof;
-  for (int k = 0; k < n_colors; ++k)
+  if (!mg->cond)
     {
-      const int64_t cnt = cbeg[(size_t)k + 1] - cbeg[(size_t)k];
-      hipLaunchKernelGGL(k_scatter_emat<T>, g1(cnt * per), dim3(256), 0, s, mg->d_lu, nf,
-                         (const T *)E, (const int32_t *)d_cdof,
-                         (const int32_t *)d_order + cbeg[(size_t)k], cnt, ndof);
+      const int64_t per = (int64_t)ndof * ndof;
+      for (int k = 0; k < n_colors; ++k)
+        {
+          const int64_t cnt = cbeg[(size_t)k + 1] - cbeg[(size_t)k];
+          hipLaunchKernelGGL(k_scatter_emat<T>, g1(cnt * per), dim3(256), 0, s, mg->d_lu, nf,
+                             (const T *)E, (const int32_t *)d_cdof,
+                             (const int32_t *)d_order + cbeg[(size_t)k], cnt, ndof);
+        }
+      HIP_THROW(hipGetLastError());
     }
-  HIP_THROW(hipGetLastError());
+  else
+    {
+      // element Schur complements over the boundary dofs (k_condense), then
+      // assembled like the element matrices
+      const int ni = mg->cond_ni, nb = mg->cond_nb;
+      std::vector<int32_t> cdb((size_t)nc_ * nb), bfree((size_t)nc_ * nb), cint((size_t)nc_ * ni),
+        cbnd((size_t)nc_ * nb);
+      for (int64_t c = 0; c < nc_; ++c)
+        {
+          const uint32_t *cn = &op->h_cell_nodes[(size_t)gls::ext_cell(op, c) * nq];
+          for (int b = 0; b < nb; ++b)
+            {
+              const int     l = mg->cond_lbnd[(size_t)b];
+              const int32_t f = cdof[(size_t)c * ndof + l];
+              cdb[(size_t)c * nb + b]   = f;
+              bfree[(size_t)c * nb + b] = f >= 0 ? 1 : 0;
+              cbnd[(size_t)c * nb + b]  = f >= 0 ? (int32_t)(cn[l / nc] * nc + l % nc) : -1;
+            }
+          for (int m = 0; m < ni; ++m)
+            {
+              const int l = mg->cond_lint[(size_t)m];
+              cint[(size_t)c * ni + m] = (int32_t)(cn[l / nc] * nc + l % nc);
+            }
+        }
+      if (!mg->d_cC)
+        {
+          HIP_THROW(hipMalloc((void **)&mg->d_cC, (size_t)nc_ * ni * ni * 8));
+          HIP_THROW(hipMalloc((void **)&mg->d_cF, (size_t)nc_ * nb * ni * 8));
+          HIP_THROW(hipMalloc((void **)&mg->d_cG, (size_t)nc_ * ni * nb * 8));
+          HIP_THROW(hipMalloc((void **)&mg->d_cy, (size_t)nc_ * ni * 8));
+          HIP_THROW(hipMalloc((void **)&mg->d_cint, (size_t)nc_ * ni * 4));
+          HIP_THROW(hipMalloc((void **)&mg->d_cbnd, (size_t)nc_ * nb * 4));
+        }
+      HIP_THROW(hipMemcpyAsync(mg->d_cint, cint.data(), cint.size() * 4, hipMemcpyHostToDevice, s));
+      HIP_THROW(hipMemcpyAsync(mg->d_cbnd, cbnd.data(), cbnd.size() * 4, hipMemcpyHostToDevice, s));
+      void *Sd = nullptr, *d_lint = nullptr, *d_lbnd = nullptr, *d_bfree = nullptr, *d_cdb = nullptr;
+      HIP_THROW(hipMallocAsync(&Sd, (size_t)nc_ * nb * nb * 8, s));
+      HIP_THROW(hipMallocAsync(&d_lint, (size_t)ni * 4, s));
+      HIP_THROW(hipMallocAsync(&d_lbnd, (size_t)nb * 4, s));
+      HIP_THROW(hipMallocAsync(&d_bfree, bfree.size() * 4, s));
+      HIP_THROW(hipMallocAsync(&d_cdb, cdb.size() * 4, s));
+      HIP_THROW(hipMemcpyAsync(d_lint, mg->cond_lint.data(), (size_t)ni * 4, hipMemcpyHostToDevice, s));
+      HIP_THROW(hipMemcpyAsync(d_lbnd, mg->cond_lbnd.data(), (size_t)nb * 4, hipMemcpyHostToDevice, s));
+      HIP_THROW(hipMemcpyAsync(d_bfree, bfree.data(), bfree.size() * 4, hipMemcpyHostToDevice, s));
+      HIP_THROW(hipMemcpyAsync(d_cdb, cdb.data(), cdb.size() * 4, hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(k_condense<T>, dim3((unsigned)nc_), dim3(256), 0, s, (const T *)E, ndof,
+                         (const int32_t *)d_lint, ni, (const int32_t *)d_lbnd, nb,
+                         (const int32_t *)d_bfree, (double *)Sd, mg->d_cC, mg->d_cF, mg->d_cG);
+      const int64_t per = (int64_t)nb * nb;
+      for (int k = 0; k < n_colors; ++k)
+        {
+          const int64_t cnt = cbeg[(size_t)k + 1] - cbeg[(size_t)k];
+          hipLaunchKernelGGL(k_scatter_emat<double>, g1(cnt * per), dim3(256), 0, s, mg->d_lu, nf,
+                             (const double *)Sd, (const int32_t *)d_cdb,
+                             (const int32_t *)d_order + cbeg[(size_t)k], cnt, nb);
+        }
+      HIP_THROW(hipGetLastError());
+      for (void *q : {Sd, d_lint, d_lbnd, d_bfree, d_cdb})
+        HIP_THROW(hipFreeAsync(q, s));
+    }
   HIP_THROW(hipFreeAsync(E, s));
   HIP_THROW(hipFreeAsync(d_cdof, s));
   HIP_THROW(hipFreeAsync(d_order, s));
@@ -1066,6 +1362,55 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
   for (int64_t d = 0; d < n; ++d)
     if (!((op->h_cmask[(size_t)(d / nc)] >> (d % nc)) & 1))
       freel.push_back((int32_t)d);
+  // static condensation of the cells' interior dofs (default with the
+  // element-matrix assembly; GLS_COARSE_CONDENSE=0 off): a node with every
+  // lattice coordinate inside (0, k) belongs to one cell only, so its dofs
+  // are eliminated cell by cell (Schur complement of the element matrix) and
+  // the dense inverse covers the other free dofs (Re3900 r0: 12,606 of
+  // 14,206, 0.70x the factorisation flops, 0.79x the GEMV's bytes); the
+  // coarse solve adds y = C b_I, the condensed right-hand side and
+  // x_I = y - G x_B (k_cond_y / k_cond_rhs / k_cond_post)
+  const char *ca      = getenv("GLS_COARSE_ASSEMBLY");
+  const bool  columns = ca && std::string(ca) == "columns";
+  {
+    const char *cc = getenv("GLS_COARSE_CONDENSE");
+    const int   k  = op->degree, dim = op->dim, nq = op->nq;
+    mg->cond_lint.clear(), mg->cond_lbnd.clear();
+    for (int p = 0; p < nq; ++p)
+      {
+        const int  co[3] = {p % (k + 1), (p / (k + 1)) % (k + 1), dim == 3 ? p / ((k + 1) * (k + 1)) : 1};
+        const bool in    = co[0] > 0 && co[0] < k && co[1] > 0 && co[1] < k && co[2] > 0 && co[2] < k;
+        for (int q = 0; q < nc; ++q)
+          (in ? mg->cond_lint : mg->cond_lbnd).push_back(p * nc + q);
+      }
+    const int ni = (int)mg->cond_lint.size(), nb = (int)mg->cond_lbnd.size();
+    bool      cond = !columns && !(cc && cc[0] == '0') && ni > 0 && ni <= COND_MAXI &&
+                nb <= 128 && nb * ni <= 1024;
+    std::vector<char> is_int((size_t)n, 0);
+    for (int64_t c = 0; cond && c < op->n_cells; ++c)
+      {
+        const uint32_t *cn = &op->h_cell_nodes[(size_t)gls::ext_cell(op, c) * nq];
+        for (int m = 0; m < ni && cond; ++m)
+          {
+            const int     l = mg->cond_lint[(size_t)m];
+            const int64_t d = (int64_t)cn[l / nc] * nc + l % nc;
+            // every interior dof free and in this cell alone
+            if (((op->h_cmask[(size_t)cn[l / nc]] >> (l % nc)) & 1) || is_int[(size_t)d])
+              cond = false;
+            is_int[(size_t)d] = 1;
+          }
+      }
+    mg->cond = cond, mg->cond_ni = ni, mg->cond_nb = nb;
+    if (cond)
+      {
+        std::vector<int32_t> rl;
+        rl.reserve(freel.size());
+        for (int32_t d : freel)
+          if (!is_int[(size_t)d])
+            rl.push_back(d);
+        freel.swap(rl);
+      }
+  }
   const int64_t nf = (int64_t)freel.size();
   if (nf == 0)
     throw std::runtime_error("dense LU coarse solver: no free coarse dofs");
@@ -1093,9 +1438,8 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
     throw std::runtime_error("dense LU coarse solver: constrained dofs changed");
   HIP_THROW(hipMemcpyAsync(mg->d_free, freel.data(), (size_t)nf * sizeof(int32_t),
                            hipMemcpyHostToDevice, s));
-  const char *ca = getenv("GLS_COARSE_ASSEMBLY");
   const auto  t0 = std::chrono::steady_clock::now();
-  if (ca && std::string(ca) == "columns")
+  if (columns)
     {
       // reference path of the assembly test: A_ff column by column from
       // unit-vector vmults (nf vmults of the level operator)
@@ -1224,6 +1568,42 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
     }
   HIP_THROW(hipMemcpyAsync(mg->d_free_in, fin.data(), (size_t)nf * sizeof(int32_t),
                            hipMemcpyHostToDevice, s));
+  if (mg->cond)
+    {
+      // per GEMV column i: the (cell, boundary slot) pairs of dof fin[i]
+      const int     nb = mg->cond_nb, nq = op->nq;
+      std::vector<std::vector<int32_t>> at((size_t)n);
+      for (int64_t c = 0; c < op->n_cells; ++c)
+        {
+          const uint32_t *cn = &op->h_cell_nodes[(size_t)gls::ext_cell(op, c) * nq];
+          for (int b = 0; b < nb; ++b)
+            {
+              const int     l = mg->cond_lbnd[(size_t)b];
+              const int64_t d = (int64_t)cn[l / nc] * nc + l % nc;
+              if (!((op->h_cmask[(size_t)cn[l / nc]] >> (l % nc)) & 1))
+                at[(size_t)d].push_back((int32_t)(c * nb + b));
+            }
+        }
+      std::vector<int32_t> off(1, 0), ent;
+      for (int64_t i = 0; i < nf; ++i)
+        {
+          for (int32_t e : at[(size_t)fin[(size_t)i]])
+            ent.push_back(e);
+          off.push_back((int32_t)ent.size());
+        }
+      for (int32_t **q : {&mg->d_rg_off, &mg->d_rg_ent})
+        if (*q)
+          {
+            HIP_THROW(hipStreamSynchronize(s));
+            HIP_THROW(hipFree(*q));
+            *q = nullptr;
+          }
+      HIP_THROW(hipMalloc((void **)&mg->d_rg_off, off.size() * 4));
+      HIP_THROW(hipMalloc((void **)&mg->d_rg_ent, std::max<size_t>(1, ent.size()) * 4));
+      HIP_THROW(hipMemcpy(mg->d_rg_off, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+      if (!ent.empty())
+        HIP_THROW(hipMemcpy(mg->d_rg_ent, ent.data(), ent.size() * 4, hipMemcpyHostToDevice));
+    }
   const auto t3 = std::chrono::steady_clock::now();
   auto       ms = [](auto a, auto b) {
     return std::chrono::duration<double, std::milli>(b - a).count();
@@ -1255,6 +1635,37 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
     }
 }
 
+// the condensed coarse right-hand side into out (GEMV column order, padded
+// to ld_free) and sol = def; then, after the GEMV, the interior dofs
+template <typename T, typename O>
+void
+cond_rhs_t(glsMG_ *mg, O *out, hipStream_t s)
+{
+  const int64_t n = mg->ops[0]->n_dofs, nc_ = mg->ops[0]->n_cells;
+  hipLaunchKernelGGL(k_cond_y<T>, g1(nc_ * mg->cond_ni), dim3(256), 0, s, mg->d_cy,
+                     (const double *)mg->d_cC, (const T *)mg->def[0],
+                     (const int32_t *)mg->d_cint, mg->cond_ni, nc_);
+  hipLaunchKernelGGL((k_cond_rhs<T, O>), g1(std::max(n, mg->ld_free)), dim3(256), 0, s,
+                     (T *)mg->sol[0], (const T *)mg->def[0], out,
+                     (const int32_t *)mg->d_free_in, (const int32_t *)mg->d_rg_off,
+                     (const int32_t *)mg->d_rg_ent, (const double *)mg->d_cF,
+                     (const int32_t *)mg->d_cint, mg->cond_ni, mg->cond_nb, n, mg->n_free,
+                     mg->ld_free);
+  HIP_THROW(hipGetLastError());
+}
+
+template <typename T>
+void
+cond_post_t(glsMG_ *mg, hipStream_t s)
+{
+  const int64_t nc_ = mg->ops[0]->n_cells;
+  hipLaunchKernelGGL(k_cond_post<T>, g1(nc_ * mg->cond_ni), dim3(256), 0, s, (T *)mg->sol[0],
+                     (const double *)mg->d_cy, (const double *)mg->d_cG,
+                     (const int32_t *)mg->d_cint, (const int32_t *)mg->d_cbnd, mg->cond_ni,
+                     mg->cond_nb, nc_);
+  HIP_THROW(hipGetLastError());
+}
+
 template <typename T>
 void
 coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
@@ -1265,8 +1676,12 @@ coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
       // sol = def (constrained dofs: x_c = b_c, their rows of A are the
       // identity), then sol[free] = A_ff^{-1} def[free], one wave per row
       float *xf = reinterpret_cast<float *>(mg->d_rhs);
-      hipLaunchKernelGGL(k_coarse_prep<T>, g1(std::max(n, ld)), dim3(256), 0, s, (T *)mg->sol[0],
-                         (const T *)mg->def[0], xf, (const int32_t *)mg->d_free_in, n, nf, ld);
+      if (mg->cond)
+        cond_rhs_t<T, float>(mg, xf, s);
+      else
+        hipLaunchKernelGGL(k_coarse_prep<T>, g1(std::max(n, ld)), dim3(256), 0, s,
+                           (T *)mg->sol[0], (const T *)mg->def[0], xf,
+                           (const int32_t *)mg->d_free_in, n, nf, ld);
       // the inverse is read once per solve and is larger than the MALL:
       // non-temporal row loads (GLS_GEMV_NT=0: default policy)
       static const bool nt = [] {
@@ -1282,12 +1697,19 @@ coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
                            0, s, (const float4 *)mg->d_inv32, (const float4 *)xf, (T *)mg->sol[0],
                            (const int32_t *)mg->d_free, nf, ld);
       HIP_THROW(hipGetLastError());
+      if (mg->cond)
+        cond_post_t<T>(mg, s);
       return;
     }
   // constrained dofs: x_c = b_c (their rows of A are the identity)
-  copy_words(mg->sol[0], mg->def[0], n * (int64_t)sizeof(T) / 4, s);
-  hipLaunchKernelGGL(k_gather_free<T>, g1(nf), dim3(256), 0, s, mg->d_rhs,
-                     (const T *)mg->def[0], (const int32_t *)mg->d_free_in, nf);
+  if (mg->cond)
+    cond_rhs_t<T, double>(mg, mg->d_rhs, s);
+  else
+    {
+      copy_words(mg->sol[0], mg->def[0], n * (int64_t)sizeof(T) / 4, s);
+      hipLaunchKernelGGL(k_gather_free<T>, g1(nf), dim3(256), 0, s, mg->d_rhs,
+                         (const T *)mg->def[0], (const int32_t *)mg->d_free_in, nf);
+    }
   double *part = mg->d_rhs + 2 * ld;
   hipLaunchKernelGGL(k_gemv_part<double>, dim3((unsigned)((nf + 255) / 256), GEMV_CHUNKS),
                      dim3(256), 0, s, (const double *)mg->d_lu, (const double *)mg->d_rhs, part,
@@ -1295,6 +1717,8 @@ coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
   hipLaunchKernelGGL(k_gemv_sum<T>, g1(nf), dim3(256), 0, s, (const double *)part,
                      (T *)mg->sol[0], (const int32_t *)mg->d_free, nf, ld);
   HIP_THROW(hipGetLastError());
+  if (mg->cond)
+    cond_post_t<T>(mg, s);
 }
 
 void v_step(glsMG_ *mg, int l, hipStream_t s);
@@ -1576,7 +2000,8 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
   fr.zero       = (uint32_t *)mg->def[l - 1];
   fr.zero_words = (int64_t)((size_t)mg->ops[l - 1]->n_dofs * mg->ts() / 4);
   fr.b64        = l == (int)mg->ops.size() - 1 ? mg->top_b64 : nullptr;
-  const bool folded = smooth(mg, l, mg->sol[l], mg->def[l], true, nit, s, false, &fr);
+  PendingReduce pend;
+  const bool folded = smooth(mg, l, mg->sol[l], mg->def[l], true, nit, s, false, &fr, &pend);
   if (!folded && fr.b64)
     {
       const int64_t n = mg->ops[l]->n_dofs;
@@ -1592,6 +2017,11 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
       rs.b     = mg->def[l];
       rs.omega = 1.0;
       rs.keep  = false;
+      if (pend.valid) // the pre-smoothing's last reduction, rebuilt in this gather
+        {
+          rs.prev_partial = pend.slots, rs.prev_src = pend.src;
+          rs.prev_b = pend.b, rs.prev_d = pend.d, rs.prev_omega = pend.omega;
+        }
       gls::brick_launch(mg->ops[l], gls::op_vmult_mode(mg->ops[l]), mg->tmp[l], mg->sol[l], 0,
                         mg->ops[l]->n_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE, s, &rs);
     }
@@ -1890,7 +2320,7 @@ gls_mg_destroy(glsMG mg)
   for (auto *p : mg->d_weight)
     if (p)
       (void)hipFree(p);
-  for (auto *v : {&mg->invdiag, &mg->sol, &mg->def, &mg->tmp})
+  for (auto *v : {&mg->invdiag, &mg->sol, &mg->def, &mg->tmp, &mg->qslot[0], &mg->qslot[1]})
     for (void *p : *v)
       if (p)
         (void)hipFree(p);
@@ -1902,7 +2332,9 @@ gls_mg_destroy(glsMG mg)
     (void)hipEventDestroy(ev);
   for (void *p : {(void *)mg->d_lu, (void *)mg->d_ipiv, (void *)mg->d_info, (void *)mg->d_rhs,
                   (void *)mg->d_free, (void *)mg->d_free_in, (void *)mg->d_inv32,
-                  (void *)mg->cg_ws, mg->cg_lvl})
+                  (void *)mg->cg_ws, mg->cg_lvl, (void *)mg->d_cC, (void *)mg->d_cF,
+                  (void *)mg->d_cG, (void *)mg->d_cy, (void *)mg->d_cint, (void *)mg->d_cbnd,
+                  (void *)mg->d_rg_off, (void *)mg->d_rg_ent})
     if (p)
       (void)hipFree(p);
   if (mg->cg_host)
@@ -1944,6 +2376,15 @@ gls_mg_setup(glsMG mg, void *stream)
   gls::DeviceScope dev(mg->ops[0]->device);
   hipStream_t      s  = (hipStream_t)stream;
   const size_t     nl = mg->ops.size();
+  // the smoother's slot buffers for deferred reductions (smooth)
+  for (int q = 0; q < 2; ++q)
+    {
+      mg->qslot[q].resize(nl, nullptr);
+      for (size_t l = 0; l < nl; ++l)
+        if (!mg->qslot[q][l] && gls::deferred_reduce_ok(mg->ops[l]))
+          HIP_THROW(hipMalloc(&mg->qslot[q][l], std::max<size_t>(16, (size_t)mg->ops[l]->n_slots *
+                                                                        (mg->dim + 1) * mg->ts())));
+    }
   // the levels are independent here: each level's diagonal and power
   // iteration run on a stream of its own (forked from and joined back into
   // s by events), so the small levels' launch-bound steps overlap the fine

@@ -184,7 +184,28 @@ struct RelaxStep
   double      omega = 0.0;
   bool        keep  = true;    // false: omega d (b - A x) (with d null, omega 1: the
                                // multigrid residual b - A x)
+  // deferred shared-node reduction (FP32 3D brick levels, mg.hip smooth):
+  // partial: this apply's slot buffer (null: the operator's); prev_partial:
+  // the previous apply's slots, whose reduction this apply's gather rebuilds
+  // from prev_src (the iterate before src) with the previous step's b, d,
+  // omega and writes into src; defer: skip this apply's own reduction
+  void       *partial      = nullptr;
+  const void *prev_partial = nullptr;
+  const void *prev_src     = nullptr;
+  const void *prev_b       = nullptr;
+  const void *prev_d       = nullptr;
+  double      prev_omega   = 0.0;
+  bool        defer        = false;
 };
+
+// a brick operator whose smoother can defer its shared-node reductions
+// (the gather rebuilds them: one 16-byte pack per node, FP32 3D)
+inline bool
+deferred_reduce_ok(const glsOp_ *op)
+{
+  return op->use_brick && op->n_owned_dofs == op->n_dofs && op->faces.n == 0 &&
+         op->prec == GLS_F32 && op->dim == 3 && op->reduce_classes.n > 0;
+}
 
 // the pieces of vmult that dist.hip / mg.hip orchestrate (gls_op.hip):
 // brick kernel over work units [b0, b1) (what & BRICK_RUN) and the

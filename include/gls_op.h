@@ -372,8 +372,9 @@ glsStatus gls_mg_coarse_statistics(glsMG mg, int *n_iterations, int *converged);
  * and the wall ms of its last setup (system matrix + hierarchy) */
 glsStatus gls_mg_coarse_amg(glsMG mg, glsAMG *amg, double *setup_ms);
 /* the last dense-coarse setup (coarse_n_iterations < 0): wall ms of the
- * free-block assembly (element matrices of the coarse level scattered per
- * cell colour), of getrf and of getri, and the number of cell colours */
+ * free-block assembly (element matrices of the coarse level, the cells'
+ * interior dofs statically condensed, scattered per cell colour), of getrf
+ * and of the inverse (trtri + trsm), and the number of cell colours */
 glsStatus gls_mg_coarse_setup_times(glsMG mg, double *ms3, int *n_colors);
 /* one V-cycle on the finest level: dst = V(src) (PreconditionMG::vmult) */
 glsStatus gls_mg_vcycle(glsMG mg, void *dst, const void *src, void *stream);

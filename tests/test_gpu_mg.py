@@ -329,3 +329,66 @@ def test_coarse_inverse_trtri_vs_getrs(prec, monkeypatch):
     # already differs from the oracle's numpy LU by ~4e-12 in the V-cycle
     # (test_vcycle_re3900_f64_levels_tight[-1]); measured 1.15e-12
     assert err < (5e-12 if prec == "f64" else 1e-6)
+
+
+@pytest.mark.parametrize("coarse", [10, -1])
+def test_vcycle_deferred_reductions(coarse, monkeypatch):
+    """The smoother's deferred shared-node reductions (FP32 3D brick levels:
+    each apply's boundary rows rebuilt in the next apply's gather from its
+    partial slots, k_shared_reduce_cls's arithmetic; one explicit reduction
+    per smoothing sequence, the pre-smoothing's rebuilt by the residual
+    apply) against a reduction after every apply (GLS_MG_DEFER=0, read once
+    per process: the reference cycle runs in a child process) on the headline
+    hierarchy r0..r2.  Same tolerance rule as the graph test: the eager
+    cycle's own run-to-run difference (LDS-atomic order) times 20, at least
+    1e-6; and the GMRES iteration count."""
+    import subprocess
+    import sys
+    import torch
+    import glsamd
+    meshes, mg, A = _re3900_gmg(coarse)
+    b = gi.rnd(41, meshes[-1].n_dofs)
+
+    def cycle():
+        x = torch.zeros(meshes[-1].n_dofs, dtype=torch.float64, device="cuda")
+        mg.vcycle(x, torch.from_numpy(b).cuda())
+        torch.cuda.synchronize()
+        return _np(x)
+
+    y1, y2 = cycle(), cycle()
+    x = torch.zeros_like(torch.from_numpy(b)).cuda()
+    s = glsamd.LinearSolverGMRES(A, mg, relative_tolerance=1e-8, absolute_tolerance=0.0)
+    s.solve(x, torch.from_numpy(b).cuda())
+    it = s.last["n_iterations"]
+    code = f"""
+import sys, numpy as np, torch
+sys.path[:0] = {sys.path!r}
+import glsamd, glsinputs as gi
+from test_gpu_mg import _re3900_gmg
+meshes, mg, A = _re3900_gmg({coarse})
+b = gi.rnd(41, meshes[-1].n_dofs)
+x = torch.zeros(meshes[-1].n_dofs, dtype=torch.float64, device="cuda")
+mg.vcycle(x, torch.from_numpy(b).cuda())
+s = glsamd.LinearSolverGMRES(A, mg, relative_tolerance=1e-8, absolute_tolerance=0.0)
+x2 = torch.zeros_like(x)
+s.solve(x2, torch.from_numpy(b).cuda())
+torch.cuda.synchronize()
+np.save(sys.argv[1], x.cpu().numpy())
+print(s.last["n_iterations"])
+"""
+    import os
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        f = os.path.join(td, "ref.npy")
+        env = dict(os.environ, GLS_MG_DEFER="0")
+        r = subprocess.run([sys.executable, "-c", code, f], env=env, capture_output=True,
+                           text=True, timeout=180, cwd=os.path.dirname(__file__))
+        assert r.returncode == 0, r.stderr[-2000:]
+        ref = np.load(f)
+        it_ref = int(r.stdout.strip().splitlines()[-1])
+    d_ee = rel_err(y2, y1)
+    d = rel_err(y1, ref)
+    print(f"coarse {coarse}: deferred vs per-apply reductions {d:.1e} (eager vs eager {d_ee:.1e}),"
+          f" GMRES {it} vs {it_ref} iterations")
+    assert d < max(1e-6, 20 * d_ee)
+    assert abs(it - it_ref) <= 1
