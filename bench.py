@@ -416,9 +416,18 @@ def amg_companions(reps=5):
         line = {"finest_dofs": meshes[-1].n_dofs, "levels": n_ref + 1}
         # the AMG with deal.II's "smoother: Chebyshev alpha" 10 (the default)
         # and with ML's own default 30
+        # the coarse iteration count per AMG level count (a smaller "coarse:
+        # max size" forces a third level) and with the near-null space split
+        # per component (dim + 1 constant modes, node blocks: what
+        # extract_constant_modes hands ML when the deck does not ask for the
+        # default parameters), to show where the AMG's weakness comes from
         variants = [("amg", dict(coarse_amg=d.amg_parameters())),
                     ("amg_alpha30", dict(coarse_amg=dict(d.amg_parameters(),
-                                                         chebyshev_alpha=30.0)))]
+                                                         chebyshev_alpha=30.0))),
+                    ("amg_3levels", dict(coarse_amg=dict(d.amg_parameters(),
+                                                         coarse_max_size=100))),
+                    ("amg_component_modes", dict(coarse_amg=dict(d.amg_parameters(),
+                                                                 block_size=d.dim + 1)))]
         if relax:
             variants.append(("relax10", dict(coarse_n_iterations=10)))
         for key, kw in variants:

@@ -24,8 +24,9 @@
 //     coarse_max_size dofs (deal.II's "coarse: max size" 2000), solved there
 //     by a dense inverse (the reference: Amesos-KLU);
 //   * Chebyshev smoothing of degree smoother_sweeps on D^-1 A over
-//     [1.1 lambda / 30, 1.1 lambda] (ML's default smoother for the elliptic
-//     defaults; the decks' ILU smoother is sequential and substituted by it).
+//     [1.1 lambda / alpha, 1.1 lambda], alpha = chebyshev_alpha (deal.II's
+//     10; ML's own default 30) -- ML's default smoother for the elliptic
+//     defaults; the decks' ILU smoother is sequential and substituted by it.
 // Setup on the host (as ML's); the V-cycle on the device: CSR SpMV kernels
 // with the Chebyshev update fused, one launch per sweep.  tests/amg_ref.py
 // restates the same algorithm with scipy for the parity tests.
@@ -445,6 +446,9 @@ to_device(const HostCSR &A)
   // lanes per row: the smallest power of two >= 8 covering half a mean row
   const double mean = A.n > 0 ? (double)D.nnz / (double)A.n : 0.0;
   D.g               = mean > 96 ? 64 : mean > 48 ? 32 : mean > 24 ? 16 : 8;
+  // (sphere r3 coarse level, 87 entries per row: 32 lanes 16.9-17.0 ms per
+  // V-cycle, 8 / 16 / 64 lanes 20.0 / 18.1 / 18.0 ms;
+  // profiles/r04/amg/ab_amg_rows_per_lane_group.txt)
   std::vector<int32_t> rp(A.rp.begin(), A.rp.end());
   upload_vec(&D.rp, rp);
   upload_vec(&D.ci, A.ci);

@@ -526,7 +526,7 @@ struct glsMG_
   bool           cond = false;
   int            cond_ni = 0, cond_nb = 0;
   std::vector<int32_t> cond_lint, cond_lbnd; // local interior / boundary dofs of a cell
-  double        *d_cC = nullptr, *d_cF = nullptr, *d_cG = nullptr, *d_cy = nullptr;
+  double        *d_cC = nullptr, *d_cF = nullptr, *d_cG = nullptr;
   int32_t       *d_cint = nullptr, *d_cbnd = nullptr, *d_rg_off = nullptr, *d_rg_ent = nullptr;
   float         *d_inv32 = nullptr; // [nf][nf] FP32 copy of the inverse (inv_f32)
   bool           inv_f32 = false;
@@ -1095,79 +1095,82 @@ __global__ void __launch_bounds__(256)
     }
 }
 
-// y[c][k] = sum_m C[c][k][m] def[int[c][m]] (FP64), one thread per (cell, k)
-template <typename T>
-__global__ void
-k_cond_y(double *__restrict__ y, const double *__restrict__ Cm, const T *__restrict__ def,
-         const int32_t *__restrict__ cint, int ni, int64_t n_cells)
+// sum over the 64 lanes of a wavefront (butterfly, every lane gets it)
+__device__ __forceinline__ double
+cond_wave_sum(double v)
 {
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n_cells * ni)
-    return;
-  const int64_t c = g / ni;
-  const int     k = (int)(g - c * ni);
-  double        v = 0;
-  for (int m = 0; m < ni; ++m)
-    v += Cm[((size_t)c * ni + k) * ni + m] * (double)def[cint[(size_t)c * ni + m]];
-  y[g] = v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    v += __shfl_xor(v, o);
+  return v;
 }
 
 // the condensed right-hand side of GEMV column i: b_S[rin[i]] = def[rin[i]]
 // - sum over its (cell, slot) pairs of F[c][slot] . b_I[c] (F = E_BI C
-// already holds C, so the cell's interior right-hand side enters as is);
-// sol = def on every dof (the constrained rows keep it); out padded to ld
-// with zeros
+// already holds C, so the cell's interior right-hand side enters as is).
+// Eight lanes per column, one (cell, slot) pair each (a vertex of a hex mesh
+// usually has at most 8 cells; more loop), summed by a butterfly; sol = def
+// on every dof (the constrained rows keep it); out padded to ld with zeros
 template <typename T, typename O>
-__global__ void
-k_cond_rhs(T *__restrict__ sol, const T *__restrict__ def, O *__restrict__ out,
-           const int32_t *__restrict__ rin, const int32_t *__restrict__ off,
-           const int32_t *__restrict__ ent, const double *__restrict__ F,
-           const int32_t *__restrict__ cint, int ni, int nb, int64_t n, int64_t nr, int64_t ld)
-{
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n)
-    sol[i] = def[i];
-  if (i >= ld)
-    return;
-  if (i >= nr)
-    {
-      out[i] = O(0);
-      return;
-    }
-  double v = (double)def[rin[i]];
-  for (int32_t e = off[i]; e < off[i + 1]; ++e)
-    {
-      const int32_t cs = ent[e]; // cell * nb + slot
-      const int64_t c  = cs / nb;
-      const double  *f  = F + (size_t)cs * ni;
-      const int32_t *ic = cint + (size_t)c * ni;
-      for (int m = 0; m < ni; ++m)
-        v -= f[m] * (double)def[ic[m]];
-    }
-  out[i] = (O)v;
-}
-
-// the interior dofs from the boundary solution: x_I = y - G x_B
-template <typename T>
-__global__ void
-k_cond_post(T *__restrict__ sol, const double *__restrict__ y, const double *__restrict__ G,
-            const int32_t *__restrict__ cint, const int32_t *__restrict__ cbnd, int ni, int nb,
-            int64_t n_cells)
+__global__ void __launch_bounds__(256)
+  k_cond_rhs(T *__restrict__ sol, const T *__restrict__ def, O *__restrict__ out,
+             const int32_t *__restrict__ rin, const int32_t *__restrict__ off,
+             const int32_t *__restrict__ ent, const double *__restrict__ F,
+             const int32_t *__restrict__ cint, int ni, int nb, int64_t n, int64_t nr,
+             int64_t ld)
 {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n_cells * ni)
+  if (g < n)
+    sol[g] = def[g];
+  const int64_t i  = g >> 3;
+  const int     l8 = (int)(g & 7);
+  double        v  = 0;
+  if (i < nr)
+    for (int32_t e = off[i] + l8; e < off[i + 1]; e += 8)
+      {
+        const int32_t  cs = ent[e]; // cell * nb + slot
+        const int64_t  c  = cs / nb;
+        const double  *f  = F + (size_t)cs * ni;
+        const int32_t *ic = cint + (size_t)c * ni;
+        for (int m = 0; m < ni; ++m)
+          v += f[m] * (double)def[ic[m]];
+      }
+#pragma unroll
+  for (int o = 4; o > 0; o >>= 1)
+    v += __shfl_xor(v, o);
+  if (l8 != 0 || i >= ld)
     return;
-  const int64_t c  = g / ni;
-  const int     k  = (int)(g - c * ni);
-  const double *gr = G + ((size_t)c * ni + k) * nb;
-  double        v  = y[g];
-  for (int b = 0; b < nb; ++b)
+  out[i] = i < nr ? (O)((double)def[rin[i]] - v) : O(0);
+}
+
+// the interior dofs from the boundary solution: x_I = C b_I - G x_B, one
+// wavefront per (cell, interior dof k): the lanes stride G's row (nb
+// entries) and the first ni lanes add C's row times b_I
+template <typename T>
+__global__ void __launch_bounds__(256)
+  k_cond_post(T *__restrict__ sol, const T *__restrict__ def, const double *__restrict__ Cm,
+              const double *__restrict__ G, const int32_t *__restrict__ cint,
+              const int32_t *__restrict__ cbnd, int ni, int nb, int64_t n_cells)
+{
+  const int64_t row  = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int     lane = threadIdx.x & 63;
+  if (row >= n_cells * ni)
+    return;
+  const int64_t  c  = row / ni;
+  const double  *gr = G + (size_t)row * nb;
+  const int32_t *cb = cbnd + (size_t)c * nb;
+  double         v  = 0;
+  for (int b = lane; b < nb; b += 64)
     {
-      const int32_t d = cbnd[(size_t)c * nb + b];
+      const int32_t d = cb[b];
       if (d >= 0)
         v -= gr[b] * (double)sol[d];
     }
-  sol[cint[g]] = (T)v;
+  if (lane < ni)
+    v += Cm[(size_t)row * ni + lane] * (double)def[cint[(size_t)c * ni + lane]];
+  v = cond_wave_sum(v);
+  if (lane == 0)
+    sol[cint[row]] = (T)v;
 }
 
 // A_ff[fj][fi] += E[c][j][i] over the cells of one colour (no two of them
@@ -1302,7 +1305,6 @@ assemble_free_block(glsMG_ *mg, const std::vector<int32_t> &freel, hipStream_t s
           HIP_THROW(hipMalloc((void **)&mg->d_cC, (size_t)nc_ * ni * ni * 8));
           HIP_THROW(hipMalloc((void **)&mg->d_cF, (size_t)nc_ * nb * ni * 8));
           HIP_THROW(hipMalloc((void **)&mg->d_cG, (size_t)nc_ * ni * nb * 8));
-          HIP_THROW(hipMalloc((void **)&mg->d_cy, (size_t)nc_ * ni * 8));
           HIP_THROW(hipMalloc((void **)&mg->d_cint, (size_t)nc_ * ni * 4));
           HIP_THROW(hipMalloc((void **)&mg->d_cbnd, (size_t)nc_ * nb * 4));
         }
@@ -1368,8 +1370,8 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
   // are eliminated cell by cell (Schur complement of the element matrix) and
   // the dense inverse covers the other free dofs (Re3900 r0: 12,606 of
   // 14,206, 0.70x the factorisation flops, 0.79x the GEMV's bytes); the
-  // coarse solve adds y = C b_I, the condensed right-hand side and
-  // x_I = y - G x_B (k_cond_y / k_cond_rhs / k_cond_post)
+  // coarse solve adds the condensed right-hand side b_B - F b_I before the
+  // GEMV and x_I = C b_I - G x_B after it (k_cond_rhs / k_cond_post)
   const char *ca      = getenv("GLS_COARSE_ASSEMBLY");
   const bool  columns = ca && std::string(ca) == "columns";
   {
@@ -1641,11 +1643,8 @@ template <typename T, typename O>
 void
 cond_rhs_t(glsMG_ *mg, O *out, hipStream_t s)
 {
-  const int64_t n = mg->ops[0]->n_dofs, nc_ = mg->ops[0]->n_cells;
-  hipLaunchKernelGGL(k_cond_y<T>, g1(nc_ * mg->cond_ni), dim3(256), 0, s, mg->d_cy,
-                     (const double *)mg->d_cC, (const T *)mg->def[0],
-                     (const int32_t *)mg->d_cint, mg->cond_ni, nc_);
-  hipLaunchKernelGGL((k_cond_rhs<T, O>), g1(std::max(n, mg->ld_free)), dim3(256), 0, s,
+  const int64_t n = mg->ops[0]->n_dofs;
+  hipLaunchKernelGGL((k_cond_rhs<T, O>), g1(std::max(n, 8 * mg->ld_free)), dim3(256), 0, s,
                      (T *)mg->sol[0], (const T *)mg->def[0], out,
                      (const int32_t *)mg->d_free_in, (const int32_t *)mg->d_rg_off,
                      (const int32_t *)mg->d_rg_ent, (const double *)mg->d_cF,
@@ -1659,10 +1658,10 @@ void
 cond_post_t(glsMG_ *mg, hipStream_t s)
 {
   const int64_t nc_ = mg->ops[0]->n_cells;
-  hipLaunchKernelGGL(k_cond_post<T>, g1(nc_ * mg->cond_ni), dim3(256), 0, s, (T *)mg->sol[0],
-                     (const double *)mg->d_cy, (const double *)mg->d_cG,
-                     (const int32_t *)mg->d_cint, (const int32_t *)mg->d_cbnd, mg->cond_ni,
-                     mg->cond_nb, nc_);
+  hipLaunchKernelGGL(k_cond_post<T>, g1(64 * nc_ * mg->cond_ni), dim3(256), 0, s,
+                     (T *)mg->sol[0], (const T *)mg->def[0], (const double *)mg->d_cC,
+                     (const double *)mg->d_cG, (const int32_t *)mg->d_cint,
+                     (const int32_t *)mg->d_cbnd, mg->cond_ni, mg->cond_nb, nc_);
   HIP_THROW(hipGetLastError());
 }
 
@@ -2333,7 +2332,7 @@ gls_mg_destroy(glsMG mg)
   for (void *p : {(void *)mg->d_lu, (void *)mg->d_ipiv, (void *)mg->d_info, (void *)mg->d_rhs,
                   (void *)mg->d_free, (void *)mg->d_free_in, (void *)mg->d_inv32,
                   (void *)mg->cg_ws, mg->cg_lvl, (void *)mg->d_cC, (void *)mg->d_cF,
-                  (void *)mg->d_cG, (void *)mg->d_cy, (void *)mg->d_cint, (void *)mg->d_cbnd,
+                  (void *)mg->d_cG, (void *)mg->d_cint, (void *)mg->d_cbnd,
                   (void *)mg->d_rg_off, (void *)mg->d_rg_ent})
     if (p)
       (void)hipFree(p);
