@@ -227,6 +227,11 @@ def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src,
     torch.cuda.empty_cache()
     out.update(amg_companions())
     torch.cuda.empty_cache()
+    try:
+        out.update(turek3d_mg_companion())
+    except Exception as e:  # reported beside the headline, never fatal
+        out["turek3d_mg_f32_direct"] = {"error": str(e)}
+    torch.cuda.empty_cache()
     return out
 
 
@@ -276,6 +281,22 @@ def mg_companions(d, params, weights, n_ref, reps=20):
             torch.cuda.synchronize()
             t.append(e0.elapsed_time(e1))
         return float(np.median(t))
+
+    def gmres_iteration(m):
+        # fixed 28 iterations (one restart cycle), wall time per iteration
+        solver = glsamd.LinearSolverGMRES(A, m, n_max_iterations=28, relative_tolerance=1e-30,
+                                          absolute_tolerance=0.0)
+        times = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            try:
+                solver.solve(x, b)
+            except glsamd.GlsError:
+                pass  # no convergence at tolerance 0 is the point: 28 iterations
+            torch.cuda.synchronize()
+            times.append((time.perf_counter() - t0) / max(1, solver.last["n_iterations"]))
+        return float(np.median(times)) * 1e3
 
     vc = vcycles()
     os.environ["GLS_MG_GRAPH"] = "1"
@@ -327,9 +348,14 @@ def mg_companions(d, params, weights, n_ref, reps=20):
             lu["ms_hipgraph_replay"] = float(np.median(t))
         finally:
             os.environ.pop("GLS_MG_GRAPH")
+        lu["gmres_iteration_ms"] = gmres_iteration(mg_lu)
         lu["coarse_dofs"] = meshes[0].n_dofs
         lu["coarse_free_dofs"] = int(sum(((c >> k) & 1 == 0).sum() for c in [cm[0]]
                                          for k in range(4)))
+        # the dense inverse's size after the static condensation of the
+        # cells' interior dofs (one interior Q2 node per 3D cell, never
+        # constrained): free dofs - cells x (dim + 1)
+        lu["inverse_dofs"] = lu["coarse_free_dofs"] - meshes[0].n_cells * (meshes[0].dim + 1)
         lu["inverse_storage"] = "f32 (FP64 sums), free dofs only"
         y32 = torch.zeros_like(x)
         mg_lu.vcycle(y32, b)
@@ -363,19 +389,7 @@ def mg_companions(d, params, weights, n_ref, reps=20):
             os.environ.pop("GLS_COARSE_INV_F32")
     except Exception as e:  # reported, never fatal
         lu = {"error": str(e)}
-    # GMRES: fixed 28 iterations (one restart cycle), wall time per iteration
-    solver = glsamd.LinearSolverGMRES(A, mg, n_max_iterations=28, relative_tolerance=1e-30,
-                                      absolute_tolerance=0.0)
-    times = []
-    for _ in range(3):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        try:
-            solver.solve(x, b)
-        except glsamd.GlsError:
-            pass  # no convergence at tolerance 0 is the point: 28 iterations
-        torch.cuda.synchronize()
-        times.append((time.perf_counter() - t0) / max(1, solver.last["n_iterations"]))
+    git = gmres_iteration(mg)
     return {f"r{n_ref}_mg_setup_f32": {"ms": float(np.median(setup)), "levels": n_ref + 1,
                                        "note": "gls_mg_setup: inverse diagonals (direct "
                                                "element-diagonal kernel) + power iteration "
@@ -385,9 +399,71 @@ def mg_companions(d, params, weights, n_ref, reps=20):
                                                     "finest_dofs": meshes[-1].n_dofs,
                                                     "vcycles_per_s": 1e3 / vc},
             f"r{n_ref}_vcycle_f32_coarse_direct_lu": lu,
-            f"r{n_ref}_gmres_iteration": {"ms": float(np.median(times)) * 1e3,
-                                          "note": "V-cycle + FP64 vmult + CGS2 + host "
-                                                  "Hessenberg step, wall clock"}}
+            f"r{n_ref}_gmres_iteration": {"ms": git,
+                                          "note": "V-cycle (coarse: 10 relaxation sweeps) + "
+                                                  "FP64 vmult + CGS2 + host Hessenberg step, "
+                                                  "wall clock; with the deck's direct coarse "
+                                                  "solve: r{}_vcycle_f32_coarse_direct_lu."
+                                                  "gmres_iteration_ms".format(n_ref)}}
+
+
+def turek3d_mg_companion(reps=10):
+    """Config 3's own multigrid at its configured size (input_turek_3D_Re100
+    .json: GMG over r0..r3, 6.8 M DoFs on the finest level, the HBM-bound
+    size; deck coarse solver "direct", not iterated): FP32 levels, setup,
+    one V-cycle (event-timed median) and one right-preconditioned GMRES
+    iteration with the FP64 vmult (wall, 28 iterations of one restart)."""
+    import torch
+    import glsamd
+    d = gm.read_deck(os.path.join(gm.DECK_DIR, "input_turek_3D_Re100.json"))
+    params, w = d.operator_parameters(2.5e-4)
+    n_ref = d.n_refinements
+    meshes = [d.mesh(r) for r in range(n_ref + 1)]
+    vel, p, slip = d.boundary_descriptor()
+    cm = [m.constraint_mask(vel, p, slip) for m in meshes]
+    u = gi.linearization_point(meshes[-1].n_nodes, meshes[-1].dim, d.u_max)
+    hist = gi.history(u, params["order"])
+    mg, _ = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f32",
+                             coarse_n_iterations=-1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    mg.setup()
+    torch.cuda.synchronize()
+    setup_ms = (time.perf_counter() - t0) * 1e3
+    A = glsamd.NavierStokesOperator(meshes[-1], cm[-1], "f64")
+    A.set_parameters(**params)
+    A.set_linearization_point(u)
+    if params["order"] > 0:
+        A.set_previous_solution(hist, w)
+    b = A._dev(gi.src_vector(meshes[-1].n_dofs))
+    x = A.initialize_dof_vector()
+    for _ in range(3):
+        mg.vcycle(x, b)
+    torch.cuda.synchronize()
+    t = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        mg.vcycle(x, b)
+        e1.record()
+        torch.cuda.synchronize()
+        t.append(e0.elapsed_time(e1))
+    solver = glsamd.LinearSolverGMRES(A, mg, n_max_iterations=28, relative_tolerance=1e-30,
+                                      absolute_tolerance=0.0)
+    times = []
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        try:
+            solver.solve(x, b)
+        except glsamd.GlsError:
+            pass  # 28 iterations at tolerance 0
+        torch.cuda.synchronize()
+        times.append((time.perf_counter() - t0) / max(1, solver.last["n_iterations"]))
+    return {f"turek3d_r{n_ref}_mg_f32_direct": {
+        "levels": n_ref + 1, "finest_dofs": meshes[-1].n_dofs, "coarse_dofs": meshes[0].n_dofs,
+        "setup_ms": setup_ms, "coarse_setup": mg.coarse_setup_times(),
+        "vcycle_ms": float(np.median(t)), "gmres_iteration_ms": float(np.median(times)) * 1e3}}
 
 
 def amg_companions(reps=5):
@@ -869,7 +945,7 @@ def main():
         # HBM bytes per vmult from the committed rocprofv3 PMC passes of this
         # workload (scripts/pmc.sh + scripts/pmc_summary.py), when they match
         traffic = None
-        tf = os.environ.get("GLS_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r03", "pmc_r2",
+        tf = os.environ.get("GLS_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r04", "pmc_r2",
                                                              "traffic.json"))
         if tf and os.path.exists(tf) and world == 1:
             with open(tf) as f:
