@@ -130,6 +130,7 @@ struct BrickArgs
   const T        *qd;
   T               qomega;
   T              *qsrc_w;
+  double         *out64; // FP32: the written rows also as FP64 (null: none)
   ReduceClasses   rc;
   int64_t         brick_begin, brick_end;
   int             bx, by, bz;
@@ -1031,6 +1032,15 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
               r[c]              = base + a.romega * (a.rd ? a.rd[j] : T(1)) * (a.rb[j] - r[c]);
             }
       store_node<T, nc>(a.dst, tgt, r);
+      if constexpr (sizeof(T) == 4 && !R)
+        if (a.out64)
+          {
+            double r64[nc];
+#pragma unroll
+            for (int c = 0; c < nc; ++c)
+              r64[c] = (double)r[c];
+            store_node<double, nc>(a.out64, tgt, r64);
+          }
     }
 }
 
@@ -1094,7 +1104,8 @@ __global__ void __launch_bounds__(256)
                       const T *__restrict__ partial, const uint32_t *__restrict__ nodes,
                       const ReduceClasses rc, int64_t n_shared,
                       const T *__restrict__ rb = nullptr, const T *__restrict__ rd = nullptr,
-                      T romega = T(0), int keep = 1, uint32_t n_relax = 0xFFFFFFFFu)
+                      T romega = T(0), int keep = 1, uint32_t n_relax = 0xFFFFFFFFu,
+                      double *__restrict__ out64 = nullptr)
 {
   // 16-byte packs when a node's row is whole packs (nc = 4): one thread per
   // (node, pack), vector loads and stores
@@ -1147,6 +1158,10 @@ __global__ void __launch_bounds__(256)
           sum = xs + romega * dj * (reinterpret_cast<const V *>(rb)[j] - sum);
         }
       reinterpret_cast<V *>(dst)[(size_t)node * NPK + kp] = sum;
+      if (out64)
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          out64[(size_t)node * nc + kp * W + w] = (double)sum[w];
       return;
     }
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1188,6 +1203,8 @@ __global__ void __launch_bounds__(256)
       sum            = (keep ? src[j] : T(0)) + romega * (rd ? rd[j] : T(1)) * (rb[j] - sum);
     }
   dst[(size_t)node * nc + c] = sum;
+  if (out64)
+    out64[(size_t)node * nc + c] = (double)sum;
 }
 
 } // namespace gls

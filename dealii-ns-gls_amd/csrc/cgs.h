@@ -83,14 +83,16 @@ __global__ void __launch_bounds__(256)
 }
 
 // w -= V h (h on the device) over rows [0, n); then the dots of the updated w
-// with the basis (norm = 0) or its squared norm into partial 0 (norm = 1),
-// over rows [0, n_dot) (a partitioned vector: its owned rows)
+// with the basis (norm = 0), its squared norm into partial 0 (norm = 1), or
+// both: the dots into partials [0, J) and the squared norm into partial J
+// (norm = 2, J < CGS_MAXJ), over rows [0, n_dot) (a partitioned vector: its
+// owned rows)
 __global__ void __launch_bounds__(256)
   k_cgs_update(const double *__restrict__ V, int J, const double *__restrict__ h,
                double *__restrict__ w, double *__restrict__ part, int64_t n, int64_t n_dot,
                int64_t ld, int norm)
 {
-  double acc[CGS_MAXJ], hc[CGS_MAXJ];
+  double acc[CGS_MAXJ], hc[CGS_MAXJ], nrm = 0;
 #pragma unroll
   for (int c = 0; c < CGS_MAXJ; ++c)
     {
@@ -113,14 +115,64 @@ __global__ void __launch_bounds__(256)
       w[i] = wi;
       if (i >= n_dot)
         continue;
-      if (norm)
+      if (norm == 1)
         acc[0] += wi * wi;
       else
+        {
 #pragma unroll
-        for (int c = 0; c < CGS_MAXJ; ++c)
-          acc[c] += v[c] * wi;
+          for (int c = 0; c < CGS_MAXJ; ++c)
+            acc[c] += v[c] * wi; // v[c] = 0 for c >= J
+          if (norm == 2)
+            nrm += wi * wi;
+        }
     }
-  cgs_block_store(acc, norm ? 1 : J, part);
+  if (norm == 2)
+#pragma unroll
+    for (int c = 0; c < CGS_MAXJ; ++c)
+      if (c == J)
+        acc[c] = nrm;
+  cgs_block_store(acc, norm == 1 ? 1 : norm == 2 ? J + 1 : J, part);
+}
+
+// The second CGS pass's update folded into the normalisation: v = (w - V h)
+// / |w - V h| with h = V^T w (the re-orthogonalisation coefficients) and the
+// norm from Pythagoras, |w - V h|^2 = |w|^2 - |h|^2 (V orthonormal; h is
+// O(eps |w|), so the subtraction loses nothing): one pass over the basis
+// instead of an update pass, a norm reduction and a scaling pass.  h[0, J)
+// and |w|^2 = h[J] on the device (k_cgs_update norm = 2 + k_cgs_finish);
+// block 0 writes the norm to *hn for the Hessenberg column.
+__global__ void __launch_bounds__(256)
+  k_cgs_unit(const double *__restrict__ V, int J, const double *__restrict__ h,
+             const double *__restrict__ w, double *__restrict__ v, double *__restrict__ hn,
+             int64_t n, int64_t ld)
+{
+  double hc[CGS_MAXJ];
+  double h2 = 0;
+#pragma unroll
+  for (int c = 0; c < CGS_MAXJ; ++c)
+    {
+      hc[c] = c < J ? h[c] : 0.0;
+      h2 += hc[c] * hc[c];
+    }
+  const double nw = h[J] - h2;
+  const double nn = sqrt(nw > 0 ? nw : 0.0);
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    *hn = nn;
+  const double  sc  = nn > 0 ? 1.0 / nn : 0.0;
+  const int64_t per = (n + CGS_BLOCKS - 1) / CGS_BLOCKS;
+  const int64_t r0 = blockIdx.x * per, r1 = r0 + per < n ? r0 + per : n;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x)
+    {
+      double vr[CGS_MAXJ];
+#pragma unroll
+      for (int c = 0; c < CGS_MAXJ; ++c)
+        vr[c] = c < J ? V[(size_t)c * ld + i] : 0.0;
+      double t = 0;
+#pragma unroll
+      for (int c = 0; c < CGS_MAXJ; ++c)
+        t += vr[c] * hc[c];
+      v[i] = (w[i] - t) * sc;
+    }
 }
 
 // out[c] = sum over blocks of part[b][c] in a fixed order: one workgroup

@@ -717,6 +717,9 @@ struct Impl
         a.qd            = rx ? (const T *)rx->prev_d : nullptr;
         a.qomega        = rx ? (T)rx->prev_omega : T(0);
         a.qsrc_w        = (T *)src;
+        a.out64         = rx ? rx->out64 : nullptr;
+        if (a.out64 && (sizeof(T) != 4 || op->reduce_classes.n == 0 || mode == MODE_RESIDUAL))
+          throw std::runtime_error("fused FP64 output: FP32 brick operators with class reductions");
         a.rc            = op->reduce_classes;
         if (a.qslots && !(sizeof(T) == 4 && dim == 3 && op->reduce_classes.n > 0))
           throw std::runtime_error("deferred shared-node reduction: FP32 3D brick levels only");
@@ -814,7 +817,7 @@ struct Impl
               hipLaunchKernelGGL((k_shared_reduce_cls<T, dim + 1, false>), g3, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)a.partial, nods, rc,
                                  nr, a.rb, a.rd, a.romega, a.rkeep,
-                                 (uint32_t)op->n_owned_nodes);
+                                 (uint32_t)op->n_owned_nodes, a.out64);
             else if (mode == MODE_RESIDUAL)
               hipLaunchKernelGGL((k_shared_reduce<T, dim + 1, true>), g2, dim3(256), 0, s,
                                  (T *)dst, (const T *)src, (const T *)a.partial, nods, offs,

@@ -6,12 +6,15 @@
 // solution) stays in HBM; per iteration only the j+1 Hessenberg entries and a
 // norm cross to the host (what deal.II's MPI_Allreduce of the dots returns on
 // every rank), and the next Arnoldi step is already enqueued while the host
-// waits for them (the device does not idle through the round trip).  Orthogonalisation is classical Gram-Schmidt with one
-// re-orthogonalisation (CGS2): two GEMVs over the contiguous basis per
-// iteration instead of j+1 dependent dot/axpy pairs — the same projector as
-// deal.II's modified Gram-Schmidt in exact arithmetic, and the stable choice
-// for a streaming device.  The basis GEMVs are plain library GEMVs (rocBLAS);
-// the operator apply and the V-cycle are this library's own kernels.
+// waits for them (the device does not idle through the round trip).
+// Orthogonalisation is classical Gram-Schmidt with one re-orthogonalisation
+// (CGS2): passes over the contiguous basis per iteration instead of j+1
+// dependent dot/axpy pairs — the same projector as deal.II's modified
+// Gram-Schmidt in exact arithmetic, and the stable choice for a streaming
+// device.  Up to 31 basis columns the passes are this file's fused kernels
+// (cgs.h: dots; update + dots + norm; the second update folded into the
+// normalisation), beyond that rocBLAS GEMVs; the operator apply and the
+// V-cycle are this library's own kernels.
 #include "../../include/gls_op.h"
 #include "cgs.h"
 #include "common.h"
@@ -207,11 +210,34 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
     HIP_THROW(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
   // GLS_GMRES_ROCBLAS=1: the rocBLAS GEMV orthogonalisation at every length
   static const bool force_rocblas = getenv_flag("GLS_GMRES_ROCBLAS");
+  // GLS_GMRES_CGS3=1: the three explicit CGS2 passes (the second update and
+  // the norm as their own pass) instead of the Pythagorean normalisation
+  static const bool force_three_pass = getenv_flag("GLS_GMRES_CGS3");
   auto              arnoldi       = [&](int j) {
     precondition(z.d(), vcol(j));
     gls::op_vmult_device(op, w.d(), z.d(), s);
-    double *hn = dh.d() + 2 * (m + 1);
-    if (j + 1 <= CGS_MAXJ && !force_rocblas)
+    double *hn        = dh.d() + 2 * (m + 1);
+    bool    unit_done = false;
+    if (j + 1 < CGS_MAXJ && !force_rocblas && !force_three_pass)
+      {
+        // fused CGS2: dots; update + dots + |w|^2; the second update folded
+        // into the normalisation (k_cgs_unit, norm by Pythagoras)
+        const int J = j + 1;
+        hipLaunchKernelGGL(k_cgs_dots, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(), J,
+                           (const double *)w.d(), cpart.d(), n, n);
+        hipLaunchKernelGGL(k_cgs_finish, dim3(J), dim3(256), 0, s, (const double *)cpart.d(),
+                           dh.d(), 0);
+        hipLaunchKernelGGL(k_cgs_update, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(),
+                           J, (const double *)dh.d(), w.d(), cpart.d(), n, n, n, 2);
+        hipLaunchKernelGGL(k_cgs_finish, dim3(J + 1), dim3(256), 0, s, (const double *)cpart.d(),
+                           dh.d() + (m + 1), 0);
+        hipLaunchKernelGGL(k_cgs_unit, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(), J,
+                           (const double *)(dh.d() + (m + 1)), (const double *)w.d(), vcol(j + 1),
+                           hn, n, n);
+        HIP_THROW(hipGetLastError());
+        unit_done = true;
+      }
+    else if (j + 1 <= CGS_MAXJ && !force_rocblas)
       {
         // fused CGS2: dots, update + dots, update + norm (three basis passes)
         const int J = j + 1;
@@ -246,8 +272,9 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
     HIP_THROW(hipMemcpyAsync(op->gmres_host + (j % 2) * HC, dh.d(), HC * sizeof(double),
                              hipMemcpyDeviceToHost, s));
     HIP_THROW(hipEventRecord(ev[j % 2], s));
-    hipLaunchKernelGGL(k_unit_col, grid1(n), dim3(256), 0, s, vcol(j + 1), (const double *)w.d(),
-                       (const double *)hn, n);
+    if (!unit_done)
+      hipLaunchKernelGGL(k_unit_col, grid1(n), dim3(256), 0, s, vcol(j + 1),
+                         (const double *)w.d(), (const double *)hn, n);
     HIP_THROW(hipGetLastError());
   };
   // r (in column 0 of V) = b - A x

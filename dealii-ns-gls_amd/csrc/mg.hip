@@ -538,6 +538,10 @@ struct glsMG_
   // finest-level FP64 defect for the fused copy_to_mg (mg_vcycle_device; null:
   // def[top] already holds the defect)
   const double *top_b64 = nullptr;
+  // its FP64 result for the fused copy_from_mg (null: none), and whether the
+  // last post-smoothing step wrote it
+  double *top_out64      = nullptr;
+  bool    top_out64_done = false;
   double *cg_ws    = nullptr;
   void   *cg_lvl   = nullptr;
   double *cg_host  = nullptr; // pinned: two Hessenberg columns (software pipeline)
@@ -692,10 +696,12 @@ defer_reduce(const glsMG_ *mg, int level)
 // instead of x (the multigrid's out-of-place prolongation put it there).
 // fr (zero start only): folded into the first relaxation; false when there
 // was none (iters == 0), so the caller does that work itself
+// out64 (deferred-reduction levels only): the last step's result also
+// written as FP64 by its brick write-out and reduction (*wrote64 = true)
 bool
 smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int iters,
        hipStream_t s, bool start_in_tmp = false, const FirstRelax *fr = nullptr,
-       PendingReduce *pend = nullptr)
+       PendingReduce *pend = nullptr, double *out64 = nullptr, bool *wrote64 = nullptr)
 {
   auto  relax = mg->prec == GLS_F64 ? relax_t<double> : relax_t<float>;
   auto  first = [&](void *xx) {
@@ -750,11 +756,15 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
   // runs explicitly below, or is handed to the caller (pend), whose next
   // apply of the operator to x rebuilds it the same way
   const bool    defer = defer_reduce(mg, level);
+  if (!defer || pend || it >= iters)
+    out64 = nullptr;
   PendingReduce pr;
   for (; it < iters; ++it)
     {
       void          *oth = cur == x ? tmp : x;
       gls::RelaxStep r   = rx;
+      if (it + 1 == iters)
+        r.out64 = out64;
       if (defer)
         {
           r.defer   = true;
@@ -779,6 +789,7 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
         {
           gls::RelaxStep r = rx;
           r.partial        = const_cast<void *>(pr.slots);
+          r.out64          = out64;
           gls::brick_launch(op, gls::op_vmult_mode(op), cur, pr.src, 0, 0, gls::BRICK_REDUCE, s,
                             &r);
         }
@@ -788,6 +799,8 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
       const int64_t w = (int64_t)((size_t)op->n_dofs * mg->ts() / 4);
       copy_words(x, cur, w, s);
     }
+  if (wrote64)
+    *wrote64 = out64 != nullptr && pr.valid;
   return zero_start && iters > 0;
 }
 
@@ -2045,8 +2058,13 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
     transfer(mg, 0, l, mg->tmp[l], mg->sol[l - 1], s, mg->sol[l]);
   else
     transfer(mg, 0, l, mg->sol[l], mg->sol[l - 1], s);
-  // post-smoothing (MGSmootherPrecondition::smooth -> step)
-  smooth(mg, l, mg->sol[l], mg->def[l], false, nit, s, odd);
+  // post-smoothing (MGSmootherPrecondition::smooth -> step); on the finest
+  // level its last step also writes the FP64 result (copy_from_mg folded)
+  bool wrote = false;
+  smooth(mg, l, mg->sol[l], mg->def[l], false, nit, s, odd, nullptr, nullptr,
+         l == (int)mg->ops.size() - 1 ? mg->top_out64 : nullptr, &wrote);
+  if (l == (int)mg->ops.size() - 1)
+    mg->top_out64_done = wrote;
 }
 
 // Relaxation-factor estimate of PreconditionRelaxation with relaxation = 0
@@ -2591,7 +2609,10 @@ mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s)
   const bool  graph  = ge && std::atoi(ge) != 0;
   const bool  folded = cvt && top > 0 && !graph && mg->desc.smoothing_n_iterations > 0;
   if (folded)
-    mg->top_b64 = (const double *)src;
+    {
+      mg->top_b64   = (const double *)src;
+      mg->top_out64 = (double *)dst;
+    }
   else if (cvt)
     hipLaunchKernelGGL((k_convert<double, float>), g1(n), dim3(256), 0, s,
                        (float *)mg->def[top], (const double *)src, n);
@@ -2604,12 +2625,18 @@ mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s)
     }
   catch (...)
     {
-      mg->top_b64 = nullptr;
+      mg->top_b64   = nullptr;
+      mg->top_out64 = nullptr;
       throw;
     }
-  mg->top_b64 = nullptr;
-  // copy_from_mg
-  if (cvt)
+  const bool done = mg->top_out64 != nullptr && mg->top_out64_done;
+  mg->top_b64        = nullptr;
+  mg->top_out64      = nullptr;
+  mg->top_out64_done = false;
+  // copy_from_mg (unless the last post-smoothing step wrote dst itself)
+  if (done)
+    ;
+  else if (cvt)
     hipLaunchKernelGGL((k_convert<float, double>), g1(n), dim3(256), 0, s, (double *)dst,
                        (const float *)mg->sol[top], n);
   else

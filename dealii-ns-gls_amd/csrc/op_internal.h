@@ -196,6 +196,9 @@ struct RelaxStep
   const void *prev_d       = nullptr;
   double      prev_omega   = 0.0;
   bool        defer        = false;
+  // the result also converted to FP64 here (the V-cycle's copy_from_mg fused
+  // into its last apply; brick write-out and class reduce, FP32 levels)
+  double     *out64        = nullptr;
 };
 
 // a brick operator whose smoother can defer its shared-node reductions
