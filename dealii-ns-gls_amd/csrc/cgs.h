@@ -142,9 +142,8 @@ __global__ void __launch_bounds__(256)
 // and |w|^2 = h[J] on the device (k_cgs_update norm = 2 + k_cgs_finish);
 // block 0 writes the norm to *hn for the Hessenberg column.
 __global__ void __launch_bounds__(256)
-  k_cgs_unit(const double *__restrict__ V, int J, const double *__restrict__ h,
-             const double *__restrict__ w, double *__restrict__ v, double *__restrict__ hn,
-             int64_t n, int64_t ld)
+  k_cgs_unit(const double *__restrict__ V, int J, const double *__restrict__ h, const double *w,
+             double *v, double *__restrict__ hn, int64_t n, int64_t ld) // v may be w
 {
   double hc[CGS_MAXJ];
   double h2 = 0;

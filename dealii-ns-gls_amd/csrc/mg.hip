@@ -1865,8 +1865,25 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
     double *wv = vc(j + 1);
     prec(wv, w);
     double *hn = dh + 2 * (m + 1);
-    const int J = j + 1;
-    if (J <= CGS_MAXJ)
+    const int J         = j + 1;
+    bool      unit_done = false;
+    if (J < CGS_MAXJ)
+      {
+        // CGS2 with the second update folded into the normalisation
+        // (krylov.hip, cgs.h k_cgs_unit)
+        hipLaunchKernelGGL(k_cgs_dots, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V, J,
+                           (const double *)wv, cpart, n, n);
+        hipLaunchKernelGGL(k_cgs_finish, dim3(J), dim3(256), 0, s, (const double *)cpart, dh, 0);
+        hipLaunchKernelGGL(k_cgs_update, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V, J,
+                           (const double *)dh, wv, cpart, n, n, n, 2);
+        hipLaunchKernelGGL(k_cgs_finish, dim3(J + 1), dim3(256), 0, s, (const double *)cpart,
+                           dh + (m + 1), 0);
+        hipLaunchKernelGGL(k_cgs_unit, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V, J,
+                           (const double *)(dh + (m + 1)), (const double *)wv, wv, hn, n, n);
+        HIP_THROW(hipGetLastError());
+        unit_done = true;
+      }
+    else if (J <= CGS_MAXJ)
       {
         hipLaunchKernelGGL(k_cgs_dots, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V, J,
                            (const double *)wv, cpart, n, n);
@@ -1899,8 +1916,9 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
       }
     HIP_THROW(hipMemcpyAsync(mg->cg_host + (j % 2) * HC, dh, HC * 8, hipMemcpyDeviceToHost, s));
     HIP_THROW(hipEventRecord(mg->cg_ev[j % 2], s));
-    hipLaunchKernelGGL(k_unit_col, g1(n), dim3(256), 0, s, wv, (const double *)wv,
-                       (const double *)hn, n);
+    if (!unit_done)
+      hipLaunchKernelGGL(k_unit_col, g1(n), dim3(256), 0, s, wv, (const double *)wv,
+                         (const double *)hn, n);
     HIP_THROW(hipGetLastError());
   };
   cvt_out(b, (const T *)mg->def[0]);

@@ -177,3 +177,57 @@ def test_gmres_error_convention():
     with pytest.raises(glsamd.GlsError, match="FP64"):
         glsamd.LinearSolverGMRES(op32).solve(op32.initialize_dof_vector(),
                                              op32.initialize_dof_vector())
+
+
+def test_gmres_pythagorean_vs_three_pass_cgs2():
+    """The default orthogonalisation (CGS2 with the second update folded into
+    the normalisation, |w - V h|^2 = |w|^2 - |h|^2) against the three explicit
+    passes (GLS_GMRES_CGS3=1, read once per process: a child process) on the
+    Re3900 r1 Newton system with the FP64-level V-cycle: the same iteration
+    count and solutions within the solver tolerance's class."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    import torch
+    code = r'''
+import sys, numpy as np, torch
+import glsamd, glsinputs as gi
+from helpers import deck
+d = deck("input_hoffmann_3D_Re3900.json")
+meshes = [d.mesh(r) for r in range(2)]
+vel, p, slip = d.boundary_descriptor()
+cm = [m.constraint_mask(vel, p, slip) for m in meshes]
+params, w = d.operator_parameters(2.5e-4)
+u = gi.linearization_point(meshes[-1].n_nodes, meshes[-1].dim, d.u_max)
+hist = gi.history(u, params["order"])
+mg, _ = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f64", coarse_n_iterations=10)
+A = glsamd.NavierStokesOperator(meshes[-1], cm[-1], "f64")
+A.set_parameters(**params)
+A.set_linearization_point(u)
+A.set_previous_solution(hist, w)
+b = gi.rnd(5, meshes[-1].n_dofs)
+s = glsamd.LinearSolverGMRES(A, mg, n_max_iterations=400, relative_tolerance=1e-10,
+                             absolute_tolerance=0.0)
+x = A.initialize_dof_vector()
+s.solve(x, A._dev(b))
+torch.cuda.synchronize()
+np.save(sys.argv[1], x.cpu().numpy())
+print(s.last["n_iterations"])
+'''
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([here] + sys.path)
+    res = {}
+    with tempfile.TemporaryDirectory() as td:
+        for tag, extra in (("pyth", {}), ("cgs3", {"GLS_GMRES_CGS3": "1"})):
+            f = os.path.join(td, tag + ".npy")
+            out = subprocess.run([sys.executable, "-c", code, f], env=dict(env, **extra),
+                                 capture_output=True, text=True, timeout=300)
+            assert out.returncode == 0, out.stderr[-2000:]
+            res[tag] = (int(out.stdout.strip().splitlines()[-1]), np.load(f))
+    (ip, xp), (i3, x3) = res["pyth"], res["cgs3"]
+    diff = np.linalg.norm(xp - x3) / np.linalg.norm(x3)
+    print(f"GMRES iterations Pythagorean {ip} / three-pass {i3}, solution rel diff {diff:.2e}")
+    assert abs(ip - i3) <= 1
+    assert diff < 1e-7
