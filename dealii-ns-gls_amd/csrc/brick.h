@@ -307,8 +307,8 @@ group_ut_only(int g, int W)
   return MODE == MODE_NEWTON && any && !other;
 }
 
-// Geometry of a launch's bricks (build_bricks orders the Cartesian and the
-// curved bricks of each segment into separate runs): GEO_CART bricks hold
+// Geometry of a launch's bricks (build_bricks spreads the curved bricks
+// evenly over the XCD runs of each segment): GEO_CART bricks hold
 // one diagonal J^{-1} and det J per cell, GEO_GEN bricks J^{-1} and JxW per
 // q point, GEO_ANY reads the type per brick (brick_geo bit 0).
 enum

@@ -126,7 +126,7 @@ host_qindex(int dim, int n, int64_t cell, int p, int64_t ncell)
 // Brick decomposition: node lattice per brick, exclusive vs shared nodes,
 // partial slots and the CSR that k_shared_reduce walks.
 void
-build_bricks(glsOp_ *op, const glsOpDesc *d)
+build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
 {
   const int dim = op->dim, k = op->degree, n = k + 1;
   const int bx = d->brick[0], by = d->brick[1];
@@ -227,6 +227,49 @@ build_bricks(glsOp_ *op, const glsOpDesc *d)
           order[b0 + i] = seg[x * q + std::min<int64_t>(x, r) + j];
         }
     };
+    // curved bricks (per-q geometry: longer lives) spread evenly over the
+    // XCD runs of a segment, and first within each run: the generator's
+    // order puts all of them (the cells around the cylinder) into one or two
+    // XCDs' runs (Re3900 r2: 80 and 48 of 128), whose last bricks then end
+    // the launch.  Each run takes a contiguous share of the curved bricks and
+    // of the Cartesian ones in mesh order (lattice-plane sharing kept).
+    // GLS_CURVED_BALANCE=0 disables it.
+    const char *cb      = getenv("GLS_CURVED_BALANCE");
+    const bool  balance = remap && !(cb && cb[0] == '0') && cell_curved;
+    auto        spread  = [&](int64_t b0, int64_t b1) {
+      const int64_t G = b1 - b0, q = G / 8, r = G % 8;
+      if (G < 16)
+        return;
+      std::vector<int64_t> K, C;
+      for (int64_t i = b0; i < b1; ++i)
+        {
+          bool cv = false;
+          for (int64_t lc = 0; lc < cpb && !cv; ++lc)
+            cv = cell_curved[(size_t)(order[(size_t)i] * cpb + lc)] != 0;
+          (cv ? K : C).push_back(order[(size_t)i]);
+        }
+      if (K.empty() || C.empty())
+        return;
+      // run x: positions [x q + min(x, r), +q + (x < r)) of the segment (the
+      // xcd lambda's split); curved shares as even as the counts allow
+      const int64_t nk = (int64_t)K.size();
+      size_t        ik = 0, ic = 0;
+      int64_t       pos = b0;
+      // (curved bricks first in the run measured 1-2 % faster than spread
+      // through it or last: profiles/r04/explore/ab_curved_balance.txt)
+      for (int x = 0; x < 8; ++x)
+        {
+          const int64_t len = q + (x < r ? 1 : 0);
+          const int64_t kx  = nk * (x + 1) / 8 - nk * x / 8;
+          for (int64_t t = 0; t < len; ++t)
+            order[(size_t)pos++] = (t < kx && ik < K.size()) || ic >= C.size() ? K[ik++] : C[ic++];
+        }
+    };
+    if (balance)
+      {
+        spread(0, n_interior);
+        spread(n_interior, nb_full - n_split);
+      }
     if (remap)
       {
         xcd(0, n_interior);
@@ -1540,7 +1583,12 @@ gls_op_create(const glsOpDesc *d, glsOp *out)
         gen[(size_t)f * n_gen * nq + host_qindex(dim, n, g, q, n_gen)] =
           gen_rows[((size_t)g * nq + q) * ngf + f];
   upload((void **)&op->d_cell_geo, cell_geo);
-  build_bricks(op, d);
+  // per-cell geometry type for the brick order (curved bricks balanced over
+  // the XCDs, build_bricks)
+  std::vector<char> cell_curved((size_t)d->n_cells);
+  for (int64_t c = 0; c < d->n_cells; ++c)
+    cell_curved[(size_t)c] = (cell_geo[(size_t)c] & GEO_GENERAL) ? 1 : 0;
+  build_bricks(op, d, cell_curved.data());
 
   std::vector<double> hq((size_t)d->n_cells), hmin((size_t)d->n_cells);
   for (int64_t c = 0; c < d->n_cells; ++c)
