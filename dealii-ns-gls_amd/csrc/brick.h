@@ -41,13 +41,14 @@ struct BrickMax
   static constexpr int cells = dim == 3 ? 4 : 8; // cells per direction
 };
 
-template <int dim, int k>
+template <int dim, int k, int ZL = 1>
 struct BrickLattice
 {
-  // largest lattice the brick kernel takes: 3D bricks of up to 4x4x1 cells
-  // (build_bricks runs 3D bricks as one-cell layers), 2D up to 8x8 cells
+  // largest lattice the brick kernel takes: 3D bricks of up to 4x4xZL cells
+  // (build_bricks runs 3D bricks as one-cell layers, ZL = 1, except the
+  // two-layer FP32 bricks, ZL = 2), 2D up to 8x8 cells
   static constexpr int side = k * BrickMax<dim>::cells + 1;
-  static constexpr int L    = dim == 3 ? side * side * (k + 1) : side * side;
+  static constexpr int L    = dim == 3 ? side * side * (ZL * k + 1) : side * side;
   static constexpr bool fits = L <= 729;
 };
 
@@ -504,7 +505,7 @@ struct BrickOcc
   static constexpr bool late  = cart4; // tables issued at the start of each round
 };
 
-template <int dim, int k, typename T, int MODE, int GEO = GEO_ANY>
+template <int dim, int k, typename T, int MODE, int GEO = GEO_ANY, int ZL = 1>
 __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves))
   k_brick(BrickArgs<T, dim, k + 1> a)
 {
@@ -579,7 +580,7 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
   // ---- prologue: every load that does not depend on another is issued
   // up front (lattice node ids, write-out targets, round 0's geometry and
   // tables), so the block pays one HBM latency before its first sweep
-  constexpr int   NI = (BrickLattice<dim, k>::L + BLOCK - 1) / BLOCK;
+  constexpr int   NI = (BrickLattice<dim, k, ZL>::L + BLOCK - 1) / BLOCK;
   const uint32_t *bn = a.brick_nodes + brick * (int64_t)L;
   const uint32_t *bt = a.brick_target + brick * (int64_t)L;
   uint32_t        pk[NI], tg[NI];
@@ -659,7 +660,9 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
   // unmodified src of the exclusive nodes are loaded here, behind the
   // gather, instead of after the cell rounds (one memory round trip less at
   // the end of every brick; FP64 has no registers to spare for them)
-  constexpr bool PRE = sizeof(T) == 4 && !R;
+  // (two-layer bricks: two lattice chunks per thread; the operands' 24
+  // registers would spill, so they are read at the write-out)
+  constexpr bool PRE = sizeof(T) == 4 && !R && ZL == 1;
   constexpr int  NPR = PRE ? NI : 1;
   T              xb[NPR][nc], xd[NPR][nc], xs[NPR][nc];
   if constexpr (PRE)

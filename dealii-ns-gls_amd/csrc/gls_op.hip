@@ -142,12 +142,32 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
   // Small bricks (bx by <= 4: the r1 level of a 2x2x2-refined coarse mesh)
   // keep up to 8 cells (bz layers) per brick: one round of the workgroup's
   // 4 waves x 2 cells instead of a 4-cell layer with two idle waves
+  // FP32 3D Q2 levels with many bricks: 4x4x2 bricks, 32 cells and 4 rounds
+  // per workgroup (fewer shared nodes per cell, half the partial slots; the
+  // relaxation operands read at the write-out).  They pay where the launch
+  // runs several dispatch generations of the FP32 kernel (4 workgroups per
+  // CU): Re3900 r3 173 -> 162 us per FP32 vmult, but r2 (800 two-layer
+  // bricks, one generation of 4-round lives) 26.8 -> 29.5 us
+  // (profiles/r04/explore/ab_two_layer.txt).  Default: at least 4 generations
+  // of two-layer bricks; GLS_F32_TWO_LAYER=0 / 1 forces them off / on.
+  bool two_layer = dim == 3 && k == 2 && op->prec == GLS_F32 && bx * by == 16 && bz % 2 == 0;
+  if (two_layer)
+    {
+      int dev = 0, n_cu = 0;
+      const int64_t nb2 = d->n_cells / (2 * bx * by);
+      two_layer = hipGetDevice(&dev) == hipSuccess &&
+                  hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) ==
+                    hipSuccess &&
+                  n_cu > 0 && nb2 >= 4 * 4 * (int64_t)n_cu;
+      if (const char *tl = getenv("GLS_F32_TWO_LAYER"))
+        two_layer = tl[0] == '1';
+    }
   if (dim == 3)
     {
       int z = 1;
       while (bx * by * z * 2 <= 8 && bz % (z * 2) == 0)
         z *= 2;
-      bz = z;
+      bz = two_layer ? 2 : z;
     }
   const int64_t cpb = (int64_t)bx * by * bz;
   if (d->n_cells % cpb != 0)
@@ -155,8 +175,9 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
   const int Lx = k * bx + 1, Ly = k * by + 1, Lz = dim == 3 ? k * bz + 1 : 1;
   const int L  = Lx * Ly * Lz;
   const int side_max = k * (dim == 3 ? 4 : 8) + 1;
-  const int lmax     = dim == 3 ? side_max * side_max * (k + 1) : side_max * side_max;
-  if (L > lmax || lmax > 729 || (dim == 3 && (bx > 4 || by > 4 || bx * by * bz > 16)) ||
+  const int zl       = two_layer ? 2 : 1;
+  const int lmax     = dim == 3 ? side_max * side_max * (zl * k + 1) : side_max * side_max;
+  if (L > lmax || lmax > 729 || (dim == 3 && (bx > 4 || by > 4 || bx * by * bz > 16 * zl)) ||
       (dim == 2 && (bx > 8 || by > 8)))
     return; // lattice does not fit the brick kernel's LDS: per-cell path
   const int64_t nb_full = d->n_cells / cpb;
@@ -182,6 +203,8 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
           n_split = 2 * rem;
       }
   }
+  if (two_layer)
+    n_split = 0; // (one dispatch generation: no tail to split)
   if (const char *e = getenv("GLS_BRICK_SPLIT"))
     n_split = std::atoll(e);
   if (by % 2 != 0)
@@ -715,6 +738,22 @@ struct Impl
   static void
   launch_brick(int64_t n_units, size_t lds, int geo, hipStream_t s, const BrickArgs<T, dim, n> &a)
   {
+    // two-layer bricks (FP32 3D Q2 levels, build_bricks): two lattice chunks
+    // per thread
+    if constexpr (sizeof(T) == 4 && dim == 3 && k == 2)
+      if (a.L > BrickLattice<dim, k, 1>::L)
+        {
+          if (geo == GEO_GEN)
+            hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_GEN, 2>), dim3((unsigned)n_units),
+                               dim3(BLOCK), lds, s, a);
+          else if (geo == GEO_CART)
+            hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_CART, 2>), dim3((unsigned)n_units),
+                               dim3(BLOCK), lds, s, a);
+          else
+            hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_ANY, 2>), dim3((unsigned)n_units),
+                               dim3(BLOCK), lds, s, a);
+          return;
+        }
     if (geo == GEO_GEN)
       hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_GEN>), dim3((unsigned)n_units), dim3(BLOCK),
                          lds, s, a);
