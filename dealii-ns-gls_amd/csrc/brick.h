@@ -496,17 +496,17 @@ to_packs(const T (&x)[nc], V (&v)[NP])
 // forced to 4 waves it spills 140 B/lane inside the round loop and takes
 // 63.7 instead of 40.2 us at r2, 517 instead of 276 us at r3: round 4,
 // profiles/r04/explore/ab_any4_spill.txt.)
-template <int dim, int k, typename T, int MODE, int GEO>
+template <int dim, int k, typename T, int MODE, int GEO, int ZL = 1>
 struct BrickOcc
 {
   static constexpr bool cart4 = GEO == GEO_CART && sizeof(T) == 8 && dim == 3 && k == 2 &&
-                                MODE != MODE_RESIDUAL;
+                                MODE != MODE_RESIDUAL && ZL == 1;
   static constexpr int  waves = cart4 || sizeof(T) == 4 ? 4 : 3;
   static constexpr bool late  = cart4; // tables issued at the start of each round
 };
 
 template <int dim, int k, typename T, int MODE, int GEO = GEO_ANY, int ZL = 1>
-__global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves))
+__global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO, ZL>::waves))
   k_brick(BrickArgs<T, dim, k + 1> a)
 {
   using LDS          = BrickLDS<dim, k, T>;
@@ -520,7 +520,7 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO>::waves)
   constexpr int WPB  = LDS::WPB;
   constexpr int WB   = LDS::WB;
   constexpr bool R   = MODE == MODE_RESIDUAL;
-  constexpr bool LATE = BrickOcc<dim, k, T, MODE, GEO>::late;
+  constexpr bool LATE = BrickOcc<dim, k, T, MODE, GEO, ZL>::late;
   static_assert(nq <= 64, "one cell must fit a wavefront");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

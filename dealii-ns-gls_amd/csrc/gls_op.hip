@@ -142,7 +142,7 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
   // Small bricks (bx by <= 4: the r1 level of a 2x2x2-refined coarse mesh)
   // keep up to 8 cells (bz layers) per brick: one round of the workgroup's
   // 4 waves x 2 cells instead of a 4-cell layer with two idle waves
-  // FP32 3D Q2 levels with many bricks: 4x4x2 bricks, 32 cells and 4 rounds
+  // 3D Q2 operators with many bricks: 4x4x2 bricks, 32 cells and 4 rounds
   // per workgroup (fewer shared nodes per cell, half the partial slots; the
   // relaxation operands read at the write-out).  They pay where the launch
   // runs several dispatch generations of the FP32 kernel (4 workgroups per
@@ -150,15 +150,23 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
   // bricks, one generation of 4-round lives) 26.8 -> 29.5 us
   // (profiles/r04/explore/ab_two_layer.txt).  Default: at least 4 generations
   // of two-layer bricks; GLS_F32_TWO_LAYER=0 / 1 forces them off / on.
-  bool two_layer = dim == 3 && k == 2 && op->prec == GLS_F32 && bx * by == 16 && bz % 2 == 0;
+  // FP64 likewise on meshes with curved cells (the 3-wave kernels: 168
+  // VGPRs two-layer; the all-Cartesian FP64 kernel keeps its 4 waves with
+  // one-layer bricks), from 4 generations of 3 workgroups per CU
+  bool any_curved = false;
+  for (int64_t c = 0; cell_curved && c < d->n_cells && !any_curved; ++c)
+    any_curved = cell_curved[(size_t)c] != 0;
+  bool two_layer = dim == 3 && k == 2 && (op->prec == GLS_F32 || any_curved) && bx * by == 16 &&
+                   bz % 2 == 0;
   if (two_layer)
     {
-      int dev = 0, n_cu = 0;
+      int           dev = 0, n_cu = 0;
       const int64_t nb2 = d->n_cells / (2 * bx * by);
+      const int     wgs = op->prec == GLS_F32 ? 4 : 3; // workgroups per CU
       two_layer = hipGetDevice(&dev) == hipSuccess &&
                   hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) ==
                     hipSuccess &&
-                  n_cu > 0 && nb2 >= 4 * 4 * (int64_t)n_cu;
+                  n_cu > 0 && nb2 >= 4 * wgs * (int64_t)n_cu;
       if (const char *tl = getenv("GLS_F32_TWO_LAYER"))
         two_layer = tl[0] == '1';
     }
@@ -738,9 +746,8 @@ struct Impl
   static void
   launch_brick(int64_t n_units, size_t lds, int geo, hipStream_t s, const BrickArgs<T, dim, n> &a)
   {
-    // two-layer bricks (FP32 3D Q2 levels, build_bricks): two lattice chunks
-    // per thread
-    if constexpr (sizeof(T) == 4 && dim == 3 && k == 2)
+    // two-layer bricks (3D Q2, build_bricks): two lattice chunks per thread
+    if constexpr (dim == 3 && k == 2)
       if (a.L > BrickLattice<dim, k, 1>::L)
         {
           if (geo == GEO_GEN)
