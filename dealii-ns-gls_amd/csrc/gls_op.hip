@@ -149,7 +149,7 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
   // CU): Re3900 r3 173 -> 162 us per FP32 vmult, but r2 (800 two-layer
   // bricks, one generation of 4-round lives) 26.8 -> 29.5 us
   // (profiles/r04/explore/ab_two_layer.txt).  Default: at least 4 generations
-  // of two-layer bricks; GLS_F32_TWO_LAYER=0 / 1 forces them off / on.
+  // of two-layer bricks; GLS_TWO_LAYER=0 / 1 forces them off / on.
   // FP64 likewise on meshes with curved cells (the 3-wave kernels: 168
   // VGPRs two-layer; the all-Cartesian FP64 kernel keeps its 4 waves with
   // one-layer bricks), from 4 generations of 3 workgroups per CU
@@ -167,7 +167,7 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
                   hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) ==
                     hipSuccess &&
                   n_cu > 0 && nb2 >= 4 * wgs * (int64_t)n_cu;
-      if (const char *tl = getenv("GLS_F32_TWO_LAYER"))
+      if (const char *tl = getenv("GLS_TWO_LAYER"))
         two_layer = tl[0] == '1';
     }
   if (dim == 3)

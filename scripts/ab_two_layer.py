@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B of the two-layer FP32 bricks (GLS_F32_TWO_LAYER, read at operator
+"""A/B of the two-layer FP32 bricks (GLS_TWO_LAYER, read at operator
 creation): FP32 vmult back to back on the sphere r3 and Re3900 r3 meshes, and
 the Turek-3D r0..r3 multigrid companion; alternating, twice."""
 import json
@@ -46,7 +46,7 @@ def vmult_us(deck, n_ref, reps=50):
 res = {}
 for rep in range(2):
     for v in ("0", "1"):
-        os.environ["GLS_F32_TWO_LAYER"] = v
+        os.environ["GLS_TWO_LAYER"] = v
         r = {"sphere_r3": vmult_us("input_sphere_amg.json", 3),
              "re3900_r3": vmult_us("input_hoffmann_3D_Re3900.json", 3)}
         t = bench.turek3d_mg_companion()
