@@ -132,7 +132,18 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   rocblas_handle h  = blas_handle(op->device, s);
   // dh: the two CGS passes' coefficients and |w| (HC values, one D2H copy)
   const int      HC = 2 * (m + 1) + 1;
-  const size_t   ws = ((size_t)(m + 3) * n + HC + (size_t)CGS_BLOCKS * CGS_MAXJ) * sizeof(double);
+  // the preconditioned directions z_j = M^{-1} v_j are kept (Z, m columns):
+  // the cycle's update is then x += Z y, the same iterate as deal.II's
+  // x += M^{-1} (V y) for a linear preconditioner, without the V-cycle per
+  // restart (GLS_GMRES_ZKEEP=0: the M^{-1} (V y) form)
+  static const bool zkeep = [] {
+    const char *e = getenv("GLS_GMRES_ZKEEP");
+    return !(e && e[0] == '0');
+  }();
+  const size_t nz = zkeep ? (size_t)m * n : 0;
+  // Z starts 256-byte aligned (the operator's 16-byte pack loads read it)
+  const size_t z_off = ((size_t)(m + 3) * n + HC + (size_t)CGS_BLOCKS * CGS_MAXJ + 31) / 32 * 32;
+  const size_t ws    = (z_off + nz) * sizeof(double);
   if (op->gmres_ws_bytes < ws)
     {
       if (op->gmres_ws)
@@ -168,6 +179,9 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   const View V{wsd}, w{wsd + (size_t)(m + 1) * n}, z{wsd + (size_t)(m + 2) * n},
     dh{wsd + (size_t)(m + 3) * n}, cpart{wsd + (size_t)(m + 3) * n + HC};
   auto vcol = [&](int j) { return V.d() + (size_t)j * n; };
+  // Z after the CGS partials (ws layout [V | w | z | dh | cpart | Z])
+  double *Zd   = wsd + z_off;
+  auto    zcol = [&](int j) { return zkeep ? Zd + (size_t)j * n : z.d(); };
   auto precondition = [&](double *dst, const double *src) {
     if (mg)
       gls::mg_vcycle_device(mg, dst, src, s);
@@ -214,8 +228,8 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   // the norm as their own pass) instead of the Pythagorean normalisation
   static const bool force_three_pass = getenv_flag("GLS_GMRES_CGS3");
   auto              arnoldi       = [&](int j) {
-    precondition(z.d(), vcol(j));
-    gls::op_vmult_device(op, w.d(), z.d(), s);
+    precondition(zcol(j), vcol(j));
+    gls::op_vmult_device(op, w.d(), zcol(j), s);
     double *hn        = dh.d() + 2 * (m + 1);
     bool    unit_done = false;
     if (j + 1 < CGS_MAXJ && !force_rocblas && !force_three_pass)
@@ -337,13 +351,20 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
           y[i] = t / H[(size_t)i * (m + 1) + i];
         }
       HIP_THROW(hipMemcpyAsync(dh.d(), y.data(), jd * sizeof(double), hipMemcpyHostToDevice, s));
-      {
-        const double one = 1.0, zero = 0.0;
-        RB_THROW(rocblas_dgemv(h, rocblas_operation_none, (rocblas_int)n, jd, &one, V.d(),
-                               (rocblas_int)n, dh.d(), 1, &zero, w.d(), 1));
-        precondition(z.d(), w.d());
-        RB_THROW(rocblas_daxpy(h, (rocblas_int)n, &one, z.d(), 1, x, 1));
-      }
+      if (jd > 0)
+        {
+          const double one = 1.0, zero = 0.0;
+          if (zkeep)
+            RB_THROW(rocblas_dgemv(h, rocblas_operation_none, (rocblas_int)n, jd, &one, Zd,
+                                   (rocblas_int)n, dh.d(), 1, &one, x, 1));
+          else
+            {
+              RB_THROW(rocblas_dgemv(h, rocblas_operation_none, (rocblas_int)n, jd, &one, V.d(),
+                                     (rocblas_int)n, dh.d(), 1, &zero, w.d(), 1));
+              precondition(z.d(), w.d());
+              RB_THROW(rocblas_daxpy(h, (rocblas_int)n, &one, z.d(), 1, x, 1));
+            }
+        }
       conv = res <= tol;
       if (conv || it >= desc->max_iterations)
         break;
