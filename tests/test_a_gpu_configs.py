@@ -356,3 +356,39 @@ def test_vcycle_sphere_iso_q1():
           f"{ref.coarse_gmres_iterations}")
     assert conv and abs(it - ref.coarse_gmres_iterations) <= 3
     assert err < 2e-3
+
+
+def test_vcycle_sphere_iso_q1_f64_tight():
+    """The sphere multigrid algorithm at FP64 levels with a tight coarse
+    tolerance (coarse GMRES to 1e-10 on both sides): the GPU V-cycle against
+    the oracle multigrid beyond FP32 round-off, so that the 2e-3 of the FP32
+    test above bounds only the FP32-vs-FP64 difference."""
+    import torch
+    import glsamd
+    import glsmesh as gm
+    d = deck("input_sphere_amg.json")
+    meshes = [d.mesh(r) for r in range(N_REF_SPHERE_MG + 1)]
+    vel, p, slip = d.boundary_descriptor()
+    cm = [m.constraint_mask(vel, p, slip) for m in meshes]
+    params, w = d.operator_parameters(2.5e-4)
+    u = gi.linearization_point(meshes[-1].n_nodes, 3, d.u_max)
+    hist = gi.history(u, params["order"])
+    mg, _ = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f64",
+                             coarse_n_iterations=10, coarse_iso_q1=True,
+                             coarse_iterate=True, coarse_reltol=1e-10, coarse_maxiter=5000)
+    ref = OracleGMG([gm.IsoQ1Mesh(meshes[0])] + meshes[1:], cm, params, u, hist, w,
+                    coarse_iters=10, coarse_gmres_reltol=1e-10)
+    ref.set_omega([mg.relaxation(l)[0] for l in range(len(meshes))])
+    b = gi.rnd(11, meshes[-1].n_dofs)
+    src = torch.from_numpy(b).cuda()
+    dst = torch.zeros_like(src)
+    mg.vcycle(dst, src)
+    torch.cuda.synchronize()
+    it, conv = mg.coarse_statistics()
+    xr = ref.vcycle(b)
+    err = rel_err(_np(dst), xr)
+    print(f"sphere r{N_REF_SPHERE_MG} iso-Q1 FP64-level V-cycle (coarse 1e-10) rel err {err:.2e}, "
+          f"coarse GMRES {it} vs {ref.coarse_gmres_iterations}")
+    # measured 1.5e-15, 134 vs 134 coarse iterations
+    assert conv and abs(it - ref.coarse_gmres_iterations) <= 1
+    assert err < 1e-10
