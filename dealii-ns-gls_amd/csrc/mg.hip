@@ -55,6 +55,19 @@ struct TransferArgs
 // compile-time constant of the unrolled sweeps (a dense (2k+1)^dim x
 // (k+1)^dim loop indexing the kernel-argument array at run time went
 // through scratch: 28.7 us per r2 -> r1 restriction).
+// threads per transfer workgroup (one coarse cell): the fine lattice's
+// (2k+1)^dim points rounded up to whole waves, at least the coarse cell's
+// dofs, at most 256 (3D Q2: 125 points -> 128 threads, twice the resident
+// workgroups of a 256-thread block that idles half its lanes)
+template <int dim, int k>
+constexpr int
+transfer_block()
+{
+  constexpr int nl = ipow(2 * k + 1, dim), nd = ipow(k + 1, dim) * (dim + 1);
+  constexpr int m  = nl > nd ? nl : nd;
+  return m <= 64 ? 64 : m <= 128 ? 128 : 256;
+}
+
 template <int dim, int k, typename T>
 __global__ void __launch_bounds__(256)
   k_prolongate(TransferArgs<T> a, T *__restrict__ dst_f, const T *__restrict__ src_c,
@@ -62,7 +75,8 @@ __global__ void __launch_bounds__(256)
 {
   constexpr int n = k + 1, nq = ipow(n, dim), nc = dim + 1, L = 2 * k + 1;
   constexpr int nl = ipow(L, dim);
-  constexpr int NIT = (nl + 255) / 256; // lattice points per thread (blockDim 256)
+  constexpr int TB  = transfer_block<dim, k>();
+  constexpr int NIT = (nl + TB - 1) / TB; // lattice points per thread
   __shared__ T  u[nc][nq];
   __shared__ T  sP[L][n];
   const int64_t c = blockIdx.x;
@@ -75,7 +89,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int r = 0; r < NIT; ++r)
     {
-      const int I = t + r * 256;
+      const int I = t + r * TB;
       fe[r]       = I < nl ? a.child[c * nl + I] : NOT_OWNER;
     }
 #pragma unroll
@@ -102,7 +116,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int r = 0; r < NIT; ++r)
     {
-      const int I = t + r * 256;
+      const int I = t + r * TB;
       if (I >= nl)
         break;
       const int Ix = I % L, Iy = (I / L) % L, Iz = dim == 3 ? I / (L * L) : 0;
@@ -160,8 +174,8 @@ __global__ void __launch_bounds__(256)
   const int64_t c = blockIdx.x;
   const int     t = threadIdx.x;
   // this thread's coarse dof (node id, constraint bits) is independent of
-  // the fine gather: loaded up front (blockDim 256 >= nq * nc, k <= 2 in 3D)
-  constexpr bool ONE = nq * nc <= 256;
+  // the fine gather: loaded up front (blockDim >= nq * nc, k <= 2 in 3D)
+  constexpr bool ONE = nq * nc <= transfer_block<dim, k>();
   const uint32_t pk0 = ONE && t < nq * nc ? a.coarse_nodes[c * nq + t % nq] : 0u;
   if (t < L * n)
     sP[t / n][t % n] = a.P[t / n][t % n];
@@ -589,12 +603,12 @@ transfer_t(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hi
   constexpr int nq = ipow(k + 1, dim);
   const auto    a  = targs<T>(mg, level);
   const dim3    grid((unsigned)a.n_cells_c);
+  const dim3    tb(transfer_block<dim, k>());
   if (kind == 0)
-    hipLaunchKernelGGL((k_prolongate<dim, k, T>), grid, dim3(256), 0, s, a, (T *)dst,
-                       (const T *)src, (const T *)base);
+    hipLaunchKernelGGL((k_prolongate<dim, k, T>), grid, tb, 0, s, a, (T *)dst, (const T *)src,
+                       (const T *)base);
   else if (kind == 1)
-    hipLaunchKernelGGL((k_restrict<dim, k, T>), grid, dim3(256), 0, s, a, (T *)dst,
-                       (const T *)src);
+    hipLaunchKernelGGL((k_restrict<dim, k, T>), grid, tb, 0, s, a, (T *)dst, (const T *)src);
   else
     hipLaunchKernelGGL((k_interpolate<dim, k, T>), g1(a.n_cells_c * nq), dim3(256), 0, s, a,
                        (T *)dst, (const T *)src);
