@@ -88,4 +88,21 @@ struct Basis1D
   explicit Basis1D(int k);
 };
 
+// 16-byte vector of solution components (4 FP32 or 2 FP64): the brick
+// kernels' LDS packs and node loads, the reduction's slot sums
+template <typename T>
+struct Pack;
+template <>
+struct Pack<double>
+{
+  typedef double V __attribute__((ext_vector_type(2)));
+  static constexpr int W = 2;
+};
+template <>
+struct Pack<float>
+{
+  typedef float V __attribute__((ext_vector_type(4)));
+  static constexpr int W = 4;
+};
+
 } // namespace gls

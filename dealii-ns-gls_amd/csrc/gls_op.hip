@@ -458,6 +458,14 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
   upload((void **)&op->d_brick_target, target);
   upload((void **)&op->d_shared_nodes, shared_nodes);
   upload((void **)&op->d_shared_off, off);
+  {
+    // node -> its index in the shared-node order (-1: exclusive to one brick),
+    // for consumers that rebuild a deferred reduction (mg.hip k_restrict)
+    std::vector<int32_t> si((size_t)d->n_nodes);
+    for (size_t i = 0; i < si.size(); ++i)
+      si[i] = (int32_t)shared_index[i];
+    upload((void **)&op->d_shared_index, si);
+  }
   HIP_THROW(hipMalloc(&op->d_partial,
                       std::max<size_t>(1, (size_t)slot * (dim + 1) * op->tsize())));
 }
@@ -1755,7 +1763,7 @@ gls_op_destroy(glsOp op)
                   op->d_tab,          op->d_cellwise,     op->d_old_grad,     op->d_hq,
                   op->d_hmin,         op->d_tmp,          op->d_cbits,        op->d_brick_nodes,
                   op->d_brick_target, op->d_shared_nodes, op->d_shared_off,
-                  op->d_partial,      op->d_bgeo_cart,    op->d_bgeo_gen,
+                  op->d_shared_index, op->d_partial,      op->d_bgeo_cart,    op->d_bgeo_gen,
                   op->d_brick_geo,    op->d_brick_cell0,  op->d_brick_chunk0, op->d_tab_cbase,
                   op->d_node_cmask,   op->d_inhom,        op->gmres_ws};
   for (void *b : bufs)

@@ -47,7 +47,60 @@ struct TransferArgs
   const T        *weight;       // [n_dofs_f]
   int64_t         n_cells_c;
   T               P[MAXP][MAXN];
+  // restriction of a residual whose shared-node reduction is still pending
+  // (v_step, FP32 3D brick levels; null: src complete): the fine node's
+  // shared index, the residual apply's slots and classes, its src x and b
+  const int32_t  *q_index   = nullptr;
+  const uint32_t *q_nodes   = nullptr; // shared node | cmask << 28
+  const T        *q_slots   = nullptr;
+  const T        *q_x       = nullptr;
+  const T        *q_b       = nullptr;
+  gls::ReduceClasses q_rc{};
 };
+
+// the residual b - A x of shared fine node s from the residual apply's
+// partial slots, in k_shared_reduce_cls's order and arithmetic (bitwise its
+// result: keep 0, omega 1, d 1; constrained components b - x)
+template <typename T>
+__device__ __forceinline__ typename gls::Pack<T>::V
+rebuild_residual(const TransferArgs<T> &a, uint32_t s)
+{
+  using V        = typename gls::Pack<T>::V;
+  constexpr int W = gls::Pack<T>::W;
+  int           k = 0;
+#pragma unroll
+  for (int j = 1; j < gls::ReduceClasses::MAX; ++j)
+    if (j < a.q_rc.n && s >= a.q_rc.first[j])
+      k = j;
+  const uint32_t m      = a.q_rc.mult[k];
+  const uint32_t b0     = a.q_rc.slot0[k] + (s - a.q_rc.first[k]) * m;
+  const uint32_t packed = a.q_nodes[s];
+  const V       *pp     = reinterpret_cast<const V *>(a.q_slots);
+  V              sum    = {};
+  uint32_t       i      = 0;
+  for (; i + 4 <= m; i += 4)
+    {
+      const V x0 = pp[b0 + i], x1 = pp[b0 + i + 1], x2 = pp[b0 + i + 2], x3 = pp[b0 + i + 3];
+      sum += (x0 + x1) + (x2 + x3);
+    }
+  if (i + 2 <= m)
+    {
+      const V x0 = pp[b0 + i], x1 = pp[b0 + i + 1];
+      sum += x0 + x1;
+      i += 2;
+    }
+  if (i < m)
+    sum += pp[b0 + i];
+  const uint32_t node = packed & gls::NODE_MASK, cm = packed >> 28;
+  const V        xs   = reinterpret_cast<const V *>(a.q_x)[node];
+  if (cm)
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      if ((cm >> w) & 1)
+        sum[w] = xs[w];
+  const V dj = V{} + T(1);
+  return V{} + T(1) * dj * (reinterpret_cast<const V *>(a.q_b)[node] - sum);
+}
 
 // Transfers as sum factorisation over the (2k+1)^dim child lattice of one
 // coarse cell: the 1-D interpolation matrix P [(2k+1) x (k+1)] is staged in
@@ -187,6 +240,20 @@ __global__ void __launch_bounds__(256)
       const uint32_t fe    = a.child[c * nl + I];
       const bool     owner = !(fe & NOT_OWNER);
       const uint32_t fn    = fe & ~NOT_OWNER;
+      if constexpr (sizeof(T) == 4 && nc == 4)
+        if (a.q_index)
+          {
+            // pending residual: shared rows rebuilt from the slots
+            using V     = typename gls::Pack<T>::V;
+            const int32_t si = owner ? a.q_index[fn] : -1;
+            const V       r  = si >= 0 ? rebuild_residual(a, (uint32_t)si) :
+                               owner  ? reinterpret_cast<const V *>(src_f)[fn] : V{};
+            const V       wv = owner ? reinterpret_cast<const V *>(a.weight)[fn] : V{};
+#pragma unroll
+            for (int comp = 0; comp < nc; ++comp)
+              v[comp][I] = wv[comp] * r[comp];
+            continue;
+          }
 #pragma unroll
       for (int comp = 0; comp < nc; ++comp)
         v[comp][I] = owner ? a.weight[(size_t)fn * nc + comp] * src_f[(size_t)fn * nc + comp]
@@ -556,6 +623,11 @@ struct glsMG_
   // last post-smoothing step wrote it
   double *top_out64      = nullptr;
   bool    top_out64_done = false;
+  // the residual of level rq_level whose shared-node reduction the next
+  // restriction rebuilds (v_step; rq_level < 0: none): its slots, x and b
+  mutable int   rq_level = -1;
+  mutable void *rq_slots = nullptr;
+  mutable const void *rq_x = nullptr, *rq_b = nullptr;
   double *cg_ws    = nullptr;
   void   *cg_lvl   = nullptr;
   double *cg_host  = nullptr; // pinned: two Hessenberg columns (software pipeline)
@@ -590,6 +662,16 @@ targs(const glsMG_ *mg, int level)
   for (int i = 0; i < MAXP; ++i)
     for (int j = 0; j < MAXN; ++j)
       a.P[i][j] = (T)mg->P[kc][i][j];
+  if (mg->rq_level == level)
+    {
+      const glsOp op = mg->ops[level];
+      a.q_index      = op->d_shared_index;
+      a.q_nodes      = op->d_shared_nodes;
+      a.q_slots      = (const T *)mg->rq_slots;
+      a.q_x          = (const T *)mg->rq_x;
+      a.q_b          = (const T *)mg->rq_b;
+      a.q_rc         = op->reduce_classes;
+    }
   return a;
 }
 
@@ -2066,6 +2148,21 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
           rs.prev_partial = pend.slots, rs.prev_src = pend.src;
           rs.prev_b = pend.b, rs.prev_d = pend.d, rs.prev_omega = pend.omega;
         }
+      // the residual's own reduction deferred into the restriction's gather
+      // (its only reader: the prolongation overwrites tmp afterwards), into
+      // the slot buffer the pre-smoothing's pending slots do not occupy
+      static const bool defer_res = [] {
+        const char *e = getenv("GLS_MG_DEFER_RESIDUAL");
+        return !(e && e[0] == '0');
+      }();
+      if (defer_res && defer_reduce(mg, l) && mg->prec == GLS_F32 && mg->ops[l]->dim == 3)
+        {
+          void *q0   = mg->qslot[0][(size_t)l], *q1 = mg->qslot[1][(size_t)l];
+          rs.defer   = true;
+          rs.partial = pend.valid && pend.slots == q0 ? q1 : q0;
+          mg->rq_level = l, mg->rq_slots = rs.partial;
+          mg->rq_x = mg->sol[l], mg->rq_b = mg->def[l];
+        }
       gls::brick_launch(mg->ops[l], gls::op_vmult_mode(mg->ops[l]), mg->tmp[l], mg->sol[l], 0,
                         mg->ops[l]->n_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE, s, &rs);
     }
@@ -2080,7 +2177,16 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
       const int64_t w = (int64_t)((size_t)mg->ops[l - 1]->n_dofs * mg->ts() / 4);
       zero_words(mg->def[l - 1], w, s);
     }
-  transfer(mg, 1, l, mg->def[l - 1], mg->tmp[l], s);
+  try
+    {
+      transfer(mg, 1, l, mg->def[l - 1], mg->tmp[l], s);
+    }
+  catch (...)
+    {
+      mg->rq_level = -1;
+      throw;
+    }
+  mg->rq_level = -1;
   v_step(mg, l - 1, s);
   // prolongate and add the coarse correction; with an odd number of fused
   // smoothing steps to follow it goes out of place into tmp, so the

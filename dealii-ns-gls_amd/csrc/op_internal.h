@@ -124,6 +124,7 @@ struct glsOp_
   uint32_t *d_brick_target = nullptr;
   uint32_t *d_shared_nodes = nullptr;
   uint32_t *d_shared_off   = nullptr;
+  int32_t  *d_shared_index = nullptr; // node -> shared index (-1: exclusive)
   gls::ReduceClasses reduce_classes{}; // multiplicity classes of the shared nodes
   // the shared nodes are ordered [owned | ghost]: the first n_shared_owned
   // are owned rows; classes of each part on its own (first[] relative to the
