@@ -56,7 +56,59 @@ struct TransferArgs
   const T        *q_x       = nullptr;
   const T        *q_b       = nullptr;
   gls::ReduceClasses q_rc{};
+  // prolongation of a coarse solution whose last smoothing step's reduction
+  // is pending: the coarse node's shared index, that step's slots, its src
+  // (the iterate before), b, d (null: 1) and omega
+  const int32_t  *p_index   = nullptr;
+  const T        *p_slots   = nullptr;
+  const T        *p_prev    = nullptr;
+  const T        *p_b       = nullptr;
+  const T        *p_d       = nullptr;
+  T               p_omega   = T(0);
+  gls::ReduceClasses p_rc{};
 };
+
+// the relaxation step x_prev + omega d (b - A x_prev) at shared coarse node s
+// from the step's partial slots, in k_shared_reduce_cls's order and
+// arithmetic (bitwise its result; constrained components keep x_prev)
+template <typename T>
+__device__ __forceinline__ typename gls::Pack<T>::V
+rebuild_relax(const TransferArgs<T> &a, uint32_t s, uint32_t node, uint32_t cm)
+{
+  using V        = typename gls::Pack<T>::V;
+  constexpr int W = gls::Pack<T>::W;
+  int           k = 0;
+#pragma unroll
+  for (int j = 1; j < gls::ReduceClasses::MAX; ++j)
+    if (j < a.p_rc.n && s >= a.p_rc.first[j])
+      k = j;
+  const uint32_t m   = a.p_rc.mult[k];
+  const uint32_t b0  = a.p_rc.slot0[k] + (s - a.p_rc.first[k]) * m;
+  const V       *pp  = reinterpret_cast<const V *>(a.p_slots);
+  V              sum = {};
+  uint32_t       i   = 0;
+  for (; i + 4 <= m; i += 4)
+    {
+      const V x0 = pp[b0 + i], x1 = pp[b0 + i + 1], x2 = pp[b0 + i + 2], x3 = pp[b0 + i + 3];
+      sum += (x0 + x1) + (x2 + x3);
+    }
+  if (i + 2 <= m)
+    {
+      const V x0 = pp[b0 + i], x1 = pp[b0 + i + 1];
+      sum += x0 + x1;
+      i += 2;
+    }
+  if (i < m)
+    sum += pp[b0 + i];
+  const V xs = reinterpret_cast<const V *>(a.p_prev)[node];
+  if (cm)
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      if ((cm >> w) & 1)
+        sum[w] = xs[w];
+  const V dj = a.p_d ? reinterpret_cast<const V *>(a.p_d)[node] : V{} + T(1);
+  return xs + a.p_omega * dj * (reinterpret_cast<const V *>(a.p_b)[node] - sum);
+}
 
 // the residual b - A x of shared fine node s from the residual apply's
 // partial slots, in k_shared_reduce_cls's order and arithmetic (bitwise its
@@ -161,9 +213,24 @@ __global__ void __launch_bounds__(256)
     {
       const uint32_t packed = a.coarse_nodes[c * nq + t];
       const uint32_t node = packed & NODE_MASK, cm = packed >> 28;
+      bool           done = false;
+      if constexpr (sizeof(T) == 4 && nc == 4)
+        if (a.p_index)
+          {
+            // pending last smoothing step: shared coarse rows rebuilt
+            using V          = typename gls::Pack<T>::V;
+            const int32_t si = a.p_index[node];
+            const V       x  = si >= 0 ? rebuild_relax(a, (uint32_t)si, node, cm) :
+                                         reinterpret_cast<const V *>(src_c)[node];
 #pragma unroll
-      for (int comp = 0; comp < nc; ++comp)
-        u[comp][t] = ((cm >> comp) & 1) ? T(0) : src_c[(size_t)node * nc + comp];
+            for (int comp = 0; comp < nc; ++comp)
+              u[comp][t] = ((cm >> comp) & 1) ? T(0) : x[comp];
+            done = true;
+          }
+      if (!done)
+#pragma unroll
+        for (int comp = 0; comp < nc; ++comp)
+          u[comp][t] = ((cm >> comp) & 1) ? T(0) : src_c[(size_t)node * nc + comp];
     }
   __syncthreads();
 #pragma unroll
@@ -628,6 +695,12 @@ struct glsMG_
   mutable int   rq_level = -1;
   mutable void *rq_slots = nullptr;
   mutable const void *rq_x = nullptr, *rq_b = nullptr;
+  // the coarse solution of level pp_level - 1 whose last smoothing step's
+  // reduction the next prolongation into level pp_level rebuilds
+  mutable int         pp_level = -1;
+  mutable const void *pp_slots = nullptr, *pp_prev = nullptr, *pp_b = nullptr,
+                     *pp_d = nullptr;
+  mutable double      pp_omega = 0.0;
   double *cg_ws    = nullptr;
   void   *cg_lvl   = nullptr;
   double *cg_host  = nullptr; // pinned: two Hessenberg columns (software pipeline)
@@ -671,6 +744,17 @@ targs(const glsMG_ *mg, int level)
       a.q_x          = (const T *)mg->rq_x;
       a.q_b          = (const T *)mg->rq_b;
       a.q_rc         = op->reduce_classes;
+    }
+  if (mg->pp_level == level)
+    {
+      const glsOp oc = mg->ops[level - 1];
+      a.p_index      = oc->d_shared_index;
+      a.p_slots      = (const T *)mg->pp_slots;
+      a.p_prev       = (const T *)mg->pp_prev;
+      a.p_b          = (const T *)mg->pp_b;
+      a.p_d          = (const T *)mg->pp_d;
+      a.p_omega      = (T)mg->pp_omega;
+      a.p_rc         = oc->reduce_classes;
     }
   return a;
 }
@@ -1841,7 +1925,7 @@ check_amg(glsStatus st)
 // the coarse "preconditioner" once: sol[0] from def[0] (multigrid.cc:465-489):
 // dense LU (< 0), identity (0) or relaxation sweeps (> 0)
 void
-coarse_apply(glsMG_ *mg, hipStream_t s)
+coarse_apply(glsMG_ *mg, hipStream_t s, PendingReduce *pend = nullptr)
 {
   const size_t bytes = (size_t)mg->ops[0]->n_dofs * mg->ts();
   if (mg->desc.coarse_amg)
@@ -1872,7 +1956,8 @@ coarse_apply(glsMG_ *mg, hipStream_t s)
       copy_words(mg->sol[0], mg->def[0], (int64_t)(bytes / 4), s);
     }
   else
-    smooth(mg, 0, mg->sol[0], mg->def[0], true, mg->desc.coarse_n_iterations, s);
+    smooth(mg, 0, mg->sol[0], mg->def[0], true, mg->desc.coarse_n_iterations, s, false, nullptr,
+           pend);
 }
 
 // r = b - r (the coarse GMRES restart residual)
@@ -2113,9 +2198,27 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
         coarse_gmres_t<float>(mg, s);
       return;
     }
+  // the last smoothing step's reduction of a level below the finest handed
+  // to the prolongation that reads its result (GLS_MG_DEFER_PROLONG=0: off)
+  static const bool defer_pro = [] {
+    const char *e = getenv("GLS_MG_DEFER_PROLONG");
+    return !(e && e[0] == '0');
+  }();
+  auto hand_over = [&](int lc, const PendingReduce &p) {
+    if (!p.valid)
+      return;
+    mg->pp_level = lc + 1, mg->pp_slots = p.slots, mg->pp_prev = p.src;
+    mg->pp_b = p.b, mg->pp_d = p.d, mg->pp_omega = p.omega;
+  };
+  const bool pro_ok = [&](int lc) {
+    return defer_pro && mg->prec == GLS_F32 && mg->dim == 3 && lc + 1 < (int)mg->ops.size() &&
+           defer_reduce(mg, lc);
+  }(l);
   if (l == 0)
     {
-      coarse_apply(mg, s);
+      PendingReduce pc;
+      coarse_apply(mg, s, pro_ok ? &pc : nullptr);
+      hand_over(0, pc);
       return;
     }
   const int nit = mg->desc.smoothing_n_iterations;
@@ -2192,17 +2295,28 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
   // smoothing steps to follow it goes out of place into tmp, so the
   // ping-pong ends in sol without a copy
   const bool odd = gls::fused_relax_ok(mg->ops[l]) && nit % 2 == 1;
-  if (odd)
-    transfer(mg, 0, l, mg->tmp[l], mg->sol[l - 1], s, mg->sol[l]);
-  else
-    transfer(mg, 0, l, mg->sol[l], mg->sol[l - 1], s);
+  try
+    {
+      if (odd)
+        transfer(mg, 0, l, mg->tmp[l], mg->sol[l - 1], s, mg->sol[l]);
+      else
+        transfer(mg, 0, l, mg->sol[l], mg->sol[l - 1], s);
+    }
+  catch (...)
+    {
+      mg->pp_level = -1;
+      throw;
+    }
+  mg->pp_level = -1;
   // post-smoothing (MGSmootherPrecondition::smooth -> step); on the finest
   // level its last step also writes the FP64 result (copy_from_mg folded)
-  bool wrote = false;
-  smooth(mg, l, mg->sol[l], mg->def[l], false, nit, s, odd, nullptr, nullptr,
+  bool          wrote = false;
+  PendingReduce pp;
+  smooth(mg, l, mg->sol[l], mg->def[l], false, nit, s, odd, nullptr, pro_ok ? &pp : nullptr,
          l == (int)mg->ops.size() - 1 ? mg->top_out64 : nullptr, &wrote);
   if (l == (int)mg->ops.size() - 1)
     mg->top_out64_done = wrote;
+  hand_over(l, pp);
 }
 
 // Relaxation-factor estimate of PreconditionRelaxation with relaxation = 0
