@@ -193,3 +193,28 @@ def test_sphere_r3_partition_balance():
     assert np.abs(owned / owned.mean() - 1).max() < 0.05
     assert (ghost < 0.10 * owned).all()
     assert max(len(p.recv_nodes) for p in parts) <= 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_local_group_gpu_two_layer(world, monkeypatch):
+    """The partitioned native vmult with two-layer bricks forced
+    (GLS_TWO_LAYER=1: 4x4x2 bricks, the default only from 4 dispatch
+    generations, e.g. a rank's r3 slab at 2 ranks): interior / boundary
+    segments, curved-brick balance and the ghost-row reduce on 32-cell
+    bricks, against the single-domain oracle (FP64 1e-12)."""
+    import torch
+    monkeypatch.setenv("GLS_TWO_LAYER", "1")
+    c = deck_case("input_hoffmann_3D_Re3900.json", 1)
+    g = glsdist.LocalGroup(c.mesh, c.cmask, world, engine="gpu", native=True)
+    g.setup(c.params, c.u_star, c.hist, c.weights)
+    assert all(list(r.eng.op.brick_shape)[2] == 2 for r in g.ranks), \
+        [list(r.eng.op.brick_shape) for r in g.ranks]
+    srcs = g.scatter(c.src)
+    dsts = [r.new_vector() for r in g.ranks]
+    for r, sv in zip(g.ranks, srcs):  # ghosts must come from the import
+        sv[r.n_owned_dofs:].zero_()
+    g.vmult(dsts, srcs)
+    torch.cuda.synchronize()
+    out = g.gather(dsts).cpu().numpy()
+    assert rel_err(out, _oracle_ref(c)) < 1e-12
