@@ -143,7 +143,9 @@ __global__ void __launch_bounds__(256)
 // block 0 writes the norm to *hn for the Hessenberg column.
 __global__ void __launch_bounds__(256)
   k_cgs_unit(const double *__restrict__ V, int J, const double *__restrict__ h, const double *w,
-             double *v, double *__restrict__ hn, int64_t n, int64_t ld) // v may be w
+             double *v, double *__restrict__ hn, int64_t n, int64_t ld, // v may be w
+             const double *__restrict__ col = nullptr, double *__restrict__ host = nullptr,
+             int n_col = 0, int hn_at = 0)
 {
   double hc[CGS_MAXJ];
   double h2 = 0;
@@ -157,6 +159,11 @@ __global__ void __launch_bounds__(256)
   const double nn = sqrt(nw > 0 ? nw : 0.0);
   if (blockIdx.x == 0 && threadIdx.x == 0)
     *hn = nn;
+  // the Hessenberg column (col[0, n_col), the norm at hn_at) stored straight
+  // into mapped pinned host memory: no device-to-host copy on the stream
+  if (host && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < n_col; i += blockDim.x)
+      host[i] = i == hn_at ? nn : col[i];
   const double  sc  = nn > 0 ? 1.0 / nn : 0.0;
   const int64_t per = (n + CGS_BLOCKS - 1) / CGS_BLOCKS;
   const int64_t r0 = blockIdx.x * per, r1 = r0 + per < n ? r0 + per : n;

@@ -163,7 +163,8 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
           HIP_THROW(hipHostFree(op->gmres_host));
           op->gmres_host = nullptr;
         }
-      HIP_THROW(hipHostMalloc((void **)&op->gmres_host, 2 * HC * sizeof(double)));
+      HIP_THROW(hipHostMalloc((void **)&op->gmres_host, 2 * HC * sizeof(double),
+                              hipHostMallocMapped | hipHostMallocCoherent));
       op->gmres_host_count = 2 * HC;
     }
   struct View
@@ -176,6 +177,10 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
     }
   };
   double    *wsd = (double *)op->gmres_ws;
+  // the pinned Hessenberg buffers as the device sees them (k_cgs_unit writes
+  // them directly)
+  double *host_dev = nullptr;
+  HIP_THROW(hipHostGetDevicePointer((void **)&host_dev, op->gmres_host, 0));
   const View V{wsd}, w{wsd + (size_t)(m + 1) * n}, z{wsd + (size_t)(m + 2) * n},
     dh{wsd + (size_t)(m + 3) * n}, cpart{wsd + (size_t)(m + 3) * n + HC};
   auto vcol = [&](int j) { return V.d() + (size_t)j * n; };
@@ -247,7 +252,8 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
                            dh.d() + (m + 1), 0);
         hipLaunchKernelGGL(k_cgs_unit, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(), J,
                            (const double *)(dh.d() + (m + 1)), (const double *)w.d(), vcol(j + 1),
-                           hn, n, n);
+                           hn, n, n, (const double *)dh.d(), host_dev + (j % 2) * HC, HC,
+                           2 * (m + 1));
         HIP_THROW(hipGetLastError());
         unit_done = true;
       }
@@ -283,8 +289,9 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
         RB_THROW(rocblas_dnrm2(h, (rocblas_int)n, w.d(), 1, hn));
         RB_THROW(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host));
       }
-    HIP_THROW(hipMemcpyAsync(op->gmres_host + (j % 2) * HC, dh.d(), HC * sizeof(double),
-                             hipMemcpyDeviceToHost, s));
+    if (!unit_done)
+      HIP_THROW(hipMemcpyAsync(op->gmres_host + (j % 2) * HC, dh.d(), HC * sizeof(double),
+                               hipMemcpyDeviceToHost, s));
     HIP_THROW(hipEventRecord(ev[j % 2], s));
     if (!unit_done)
       hipLaunchKernelGGL(k_unit_col, grid1(n), dim3(256), 0, s, vcol(j + 1),

@@ -2002,12 +2002,15 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
       HIP_THROW(hipMalloc((void **)&mg->cg_ws,
                           ((size_t)(m + 4) * n + HC + (size_t)CGS_PART) * 8));
       HIP_THROW(hipMalloc(&mg->cg_lvl, (size_t)2 * n * sizeof(T)));
-      HIP_THROW(hipHostMalloc((void **)&mg->cg_host, (size_t)2 * HC * 8));
+      HIP_THROW(hipHostMalloc((void **)&mg->cg_host, (size_t)2 * HC * 8,
+                              hipHostMallocMapped | hipHostMallocCoherent));
       for (hipEvent_t &e : mg->cg_ev)
         HIP_THROW(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
   double *V = mg->cg_ws, *w = V + (size_t)(m + 1) * n, *x = w + n, *b = x + n,
          *dh = b + n, *cpart = dh + HC;
+  double *host_dev = nullptr; // cg_host as the device sees it (k_cgs_unit writes it)
+  HIP_THROW(hipHostGetDevicePointer((void **)&host_dev, mg->cg_host, 0));
   T *la = (T *)mg->cg_lvl, *lb = la + n;
   auto cvt_in = [&](T *dst, const double *src) {
     hipLaunchKernelGGL((k_convert<double, T>), g1(n), dim3(256), 0, s, dst, src, n);
@@ -2060,7 +2063,8 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
         hipLaunchKernelGGL(k_cgs_finish, dim3(J + 1), dim3(256), 0, s, (const double *)cpart,
                            dh + (m + 1), 0);
         hipLaunchKernelGGL(k_cgs_unit, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V, J,
-                           (const double *)(dh + (m + 1)), (const double *)wv, wv, hn, n, n);
+                           (const double *)(dh + (m + 1)), (const double *)wv, wv, hn, n, n,
+                           (const double *)dh, host_dev + (j % 2) * HC, HC, 2 * (m + 1));
         HIP_THROW(hipGetLastError());
         unit_done = true;
       }
@@ -2095,7 +2099,8 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
         check_blas(rocblas_dnrm2(h, (rocblas_int)n, wv, 1, hn), "rocblas_dnrm2");
         check_blas(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host), "pointer mode");
       }
-    HIP_THROW(hipMemcpyAsync(mg->cg_host + (j % 2) * HC, dh, HC * 8, hipMemcpyDeviceToHost, s));
+    if (!unit_done)
+      HIP_THROW(hipMemcpyAsync(mg->cg_host + (j % 2) * HC, dh, HC * 8, hipMemcpyDeviceToHost, s));
     HIP_THROW(hipEventRecord(mg->cg_ev[j % 2], s));
     if (!unit_done)
       hipLaunchKernelGGL(k_unit_col, g1(n), dim3(256), 0, s, wv, (const double *)wv,
