@@ -801,8 +801,20 @@ gls_amg_vmult(glsAMG amg, double *dst, const double *src, void *stream)
   const hipStream_t   st = (hipStream_t)stream;
   AmgLevel           &L0 = amg->lv[0];
   const int64_t       n  = L0.A.n;
-  HIP_THROW(hipMemcpyAsync(L0.f, src, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
-  vcycle_level(amg, 0, st);
+  // the finest level reads its right-hand side only (Chebyshev steps,
+  // residual): the caller's src serves as f for this cycle, no copy
+  double *const f0 = L0.f;
+  L0.f             = const_cast<double *>(src);
+  try
+    {
+      vcycle_level(amg, 0, st);
+    }
+  catch (...)
+    {
+      L0.f = f0;
+      throw;
+    }
+  L0.f = f0;
   if (amg->lv.size() > 1)
     hipLaunchKernelGGL(k_add2, elem_grid(n), dim3(256), 0, st, L0.x, L0.d, dst, n);
   else
