@@ -25,9 +25,11 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 using namespace gls;
@@ -2030,10 +2032,23 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
     coarse_apply(mg, s);
     cvt_out(dst, (const T *)mg->sol[0]);
   };
+  // FP32 brick levels: the FP64 result written by the brick write-out and
+  // the reduction themselves (RelaxStep.out64), no conversion pass
+  const bool fused_out = std::is_same<T, float>::value && gls::deferred_reduce_ok(op);
   auto apply_A = [&](double *dst, const double *src) {
     cvt_in(la, src);
-    gls::op_vmult_device(op, lb, la, s);
-    cvt_out(dst, lb);
+    if (fused_out)
+      {
+        gls::RelaxStep r;
+        r.out64 = dst;
+        gls::brick_launch(op, gls::op_vmult_mode(op), lb, la, 0, op->n_bricks,
+                          gls::BRICK_RUN | gls::BRICK_REDUCE, s, &r);
+      }
+    else
+      {
+        gls::op_vmult_device(op, lb, la, s);
+        cvt_out(dst, lb);
+      }
   };
   auto nrm2 = [&](const double *v) {
     double r = 0;
