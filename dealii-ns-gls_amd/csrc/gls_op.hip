@@ -123,6 +123,19 @@ host_qindex(int dim, int n, int64_t cell, int p, int64_t ncell)
   return ((int64_t)(p / lpc) * ncell + cell) * lpc + (p % lpc);
 }
 
+// compute units of the operator's device (not the caller's current one):
+// the brick layout, and with it the summation order, follows the device the
+// operator lives on
+int
+op_cu_count(const glsOp_ *op)
+{
+  int n_cu = 0;
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, op->device) !=
+      hipSuccess)
+    return 0;
+  return n_cu;
+}
+
 // Brick decomposition: node lattice per brick, exclusive vs shared nodes,
 // partial slots and the CSR that k_shared_reduce walks.
 void
@@ -160,13 +173,10 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
                    bz % 2 == 0;
   if (two_layer)
     {
-      int           dev = 0, n_cu = 0;
       const int64_t nb2 = d->n_cells / (2 * bx * by);
       const int     wgs = op->prec == GLS_F32 ? 4 : 3; // workgroups per CU
-      two_layer = hipGetDevice(&dev) == hipSuccess &&
-                  hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) ==
-                    hipSuccess &&
-                  n_cu > 0 && nb2 >= 4 * wgs * (int64_t)n_cu;
+      const int     n_cu = op_cu_count(op);
+      two_layer = n_cu > 0 && nb2 >= 4 * wgs * (int64_t)n_cu;
       if (const char *tl = getenv("GLS_TWO_LAYER"))
         two_layer = tl[0] == '1';
     }
@@ -200,10 +210,8 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
   // measured 46.3 -> 45.1 us; splitting 0/256/512 was slower).
   int64_t n_split = 0;
   {
-    int dev = 0, n_cu = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        n_cu > 0)
+    const int n_cu = op_cu_count(op);
+    if (n_cu > 0)
       {
         const int64_t slots = 3 * (int64_t)n_cu;
         const int64_t rem   = nb_full % slots;

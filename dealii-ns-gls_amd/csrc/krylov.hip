@@ -134,12 +134,24 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   const int      HC = 2 * (m + 1) + 1;
   // the preconditioned directions z_j = M^{-1} v_j are kept (Z, m columns):
   // the cycle's update is then x += Z y, the same iterate as deal.II's
-  // x += M^{-1} (V y) for a linear preconditioner, without the V-cycle per
-  // restart (GLS_GMRES_ZKEEP=0: the M^{-1} (V y) form)
-  static const bool zkeep = [] {
-    const char *e = getenv("GLS_GMRES_ZKEEP");
-    return !(e && e[0] == '0');
-  }();
+  // x += M^{-1} (V y) (SolverGMRES, right preconditioning: solver_l.cc:62)
+  // without the V-cycle per restart -- but only for a LINEAR preconditioner.
+  // A V-cycle whose coarse solve iterates to a tolerance (coarse_iterate,
+  // the reference's default coarse_grid_iterate, multigrid.h:36) is not
+  // linear, so x += Z y would leave deal.II's iterate; there, and when the m
+  // extra columns would take more than a quarter of the free device memory,
+  // the M^{-1} (V y) form runs.  GLS_GMRES_ZKEEP=0 / 1 forces it off / on
+  // (1: tests pinning the deviation of the kept form).
+  bool zkeep = !mg || gls::mg_is_linear(mg);
+  {
+    const size_t zbytes = (size_t)m * n * sizeof(double);
+    const bool   have_z = op->gmres_ws_bytes >= (size_t)(2 * m + 3) * n * sizeof(double);
+    size_t       fr = 0, tot = 0;
+    if (zkeep && !have_z && hipMemGetInfo(&fr, &tot) == hipSuccess && zbytes > fr / 4)
+      zkeep = false;
+    if (const char *e = getenv("GLS_GMRES_ZKEEP"))
+      zkeep = e[0] != '0';
+  }
   const size_t nz = zkeep ? (size_t)m * n : 0;
   // Z starts 256-byte aligned (the operator's 16-byte pack loads read it)
   const size_t z_off = ((size_t)(m + 3) * n + HC + (size_t)CGS_BLOCKS * CGS_MAXJ + 31) / 32 * 32;

@@ -674,6 +674,7 @@ struct glsMG_
   // dofs' global indices (-1: constrained), y = C b_I per solve, and per GEMV
   // column i the (cell, boundary slot) pairs of its dof (CSR)
   bool           cond = false;
+  bool           cond_failed = false; // a cell's E_II was (numerically) singular: no condensation
   int            cond_ni = 0, cond_nb = 0;
   std::vector<int32_t> cond_lint, cond_lbnd; // local interior / boundary dofs of a cell
   double        *d_cC = nullptr, *d_cF = nullptr, *d_cG = nullptr;
@@ -1215,7 +1216,7 @@ __global__ void __launch_bounds__(256)
   k_condense(const T *__restrict__ E, int ndof, const int32_t *__restrict__ lint, int ni,
              const int32_t *__restrict__ lbnd, int nb, const int32_t *__restrict__ bfree,
              double *__restrict__ S, double *__restrict__ Cm, double *__restrict__ F,
-             double *__restrict__ G)
+             double *__restrict__ G, int32_t *__restrict__ bad)
 {
   __shared__ double a[COND_MAXI][2 * COND_MAXI];
   __shared__ double f[128 * COND_MAXI / 4]; // F rows of this cell (nb <= 128, ni <= 8)
@@ -1233,30 +1234,47 @@ __global__ void __launch_bounds__(256)
     }
   __syncthreads();
   if (t == 0)
-    for (int col = 0; col < ni; ++col)
-      {
-        int piv = col;
-        for (int r = col + 1; r < ni; ++r)
-          if (fabs(a[r][col]) > fabs(a[piv][col]))
-            piv = r;
-        if (piv != col)
+    {
+      // a pivot below 1e-12 of E_II's largest entry (or a non-finite one)
+      // marks the cell: the host then assembles without condensation, where
+      // getrf's info check covers a singular coarse matrix
+      double scale = 0;
+      for (int r = 0; r < ni; ++r)
+        for (int q = 0; q < ni; ++q)
+          scale = fmax(scale, fabs(a[r][q]));
+      bool sing = !(scale > 0) || !isfinite(scale);
+      for (int col = 0; col < ni && !sing; ++col)
+        {
+          int piv = col;
+          for (int r = col + 1; r < ni; ++r)
+            if (fabs(a[r][col]) > fabs(a[piv][col]))
+              piv = r;
+          if (!(fabs(a[piv][col]) > 1e-12 * scale))
+            {
+              sing = true;
+              break;
+            }
+          if (piv != col)
+            for (int q = 0; q < 2 * ni; ++q)
+              {
+                const double x = a[col][q];
+                a[col][q]      = a[piv][q];
+                a[piv][q]      = x;
+              }
+          const double d = 1.0 / a[col][col];
           for (int q = 0; q < 2 * ni; ++q)
-            {
-              const double x = a[col][q];
-              a[col][q]      = a[piv][q];
-              a[piv][q]      = x;
-            }
-        const double d = 1.0 / a[col][col];
-        for (int q = 0; q < 2 * ni; ++q)
-          a[col][q] *= d;
-        for (int r = 0; r < ni; ++r)
-          if (r != col)
-            {
-              const double m = a[r][col];
-              for (int q = 0; q < 2 * ni; ++q)
-                a[r][q] -= m * a[col][q];
-            }
-      }
+            a[col][q] *= d;
+          for (int r = 0; r < ni; ++r)
+            if (r != col)
+              {
+                const double m = a[r][col];
+                for (int q = 0; q < 2 * ni; ++q)
+                  a[r][q] -= m * a[col][q];
+              }
+        }
+      if (sing)
+        bad[c] = 1;
+    }
   __syncthreads();
   double *Cc = Cm + (size_t)c * ni * ni, *Fc = F + (size_t)c * nb * ni, *Gc = G + (size_t)c * ni * nb;
   for (int k = t; k < ni * ni; k += blockDim.x)
@@ -1399,9 +1417,10 @@ k_scatter_emat(double *__restrict__ A, int64_t nf, const T *__restrict__ E,
 // all coarse cells, then one scatter launch per cell colour (greedy colouring
 // on the host, cells of a colour share no node), summed in FP64
 template <typename T>
-void
+bool
 assemble_free_block(glsMG_ *mg, const std::vector<int32_t> &freel, hipStream_t s)
 {
+  bool ok = true; // false: a condensed cell's interior block is singular
   glsOp         op   = mg->ops[0];
   const int64_t n    = op->n_dofs, nf = (int64_t)freel.size(), nc_ = op->n_cells;
   const int     nc   = op->dim + 1, nq = op->nq, ndof = nq * nc;
@@ -1515,9 +1534,19 @@ assemble_free_block(glsMG_ *mg, const std::vector<int32_t> &freel, hipStream_t s
       HIP_THROW(hipMemcpyAsync(d_lbnd, mg->cond_lbnd.data(), (size_t)nb * 4, hipMemcpyHostToDevice, s));
       HIP_THROW(hipMemcpyAsync(d_bfree, bfree.data(), bfree.size() * 4, hipMemcpyHostToDevice, s));
       HIP_THROW(hipMemcpyAsync(d_cdb, cdb.data(), cdb.size() * 4, hipMemcpyHostToDevice, s));
+      int32_t *d_bad = nullptr;
+      HIP_THROW(hipMallocAsync((void **)&d_bad, (size_t)nc_ * 4, s));
+      HIP_THROW(hipMemsetAsync(d_bad, 0, (size_t)nc_ * 4, s));
       hipLaunchKernelGGL(k_condense<T>, dim3((unsigned)nc_), dim3(256), 0, s, (const T *)E, ndof,
                          (const int32_t *)d_lint, ni, (const int32_t *)d_lbnd, nb,
-                         (const int32_t *)d_bfree, (double *)Sd, mg->d_cC, mg->d_cF, mg->d_cG);
+                         (const int32_t *)d_bfree, (double *)Sd, mg->d_cC, mg->d_cF, mg->d_cG,
+                         d_bad);
+      std::vector<int32_t> hbad((size_t)nc_);
+      HIP_THROW(hipMemcpyAsync(hbad.data(), d_bad, (size_t)nc_ * 4, hipMemcpyDeviceToHost, s));
+      HIP_THROW(hipStreamSynchronize(s));
+      HIP_THROW(hipFreeAsync(d_bad, s));
+      for (int32_t b : hbad)
+        ok = ok && b == 0;
       const int64_t per = (int64_t)nb * nb;
       for (int k = 0; k < n_colors; ++k)
         {
@@ -1535,7 +1564,7 @@ assemble_free_block(glsMG_ *mg, const std::vector<int32_t> &freel, hipStream_t s
   HIP_THROW(hipFreeAsync(d_order, s));
   mg->coarse_colors = n_colors;
   // (the synchronised setup of the caller waits for these launches)
-  (void)mg;
+  return ok;
 }
 
 // Assemble the coarse level operator into FP64 and LU-factorise it.  Only
@@ -1581,7 +1610,7 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
           (in ? mg->cond_lint : mg->cond_lbnd).push_back(p * nc + q);
       }
     const int ni = (int)mg->cond_lint.size(), nb = (int)mg->cond_lbnd.size();
-    bool      cond = !columns && !(cc && cc[0] == '0') && ni > 0 && ni <= COND_MAXI &&
+    bool      cond = !columns && !(cc && cc[0] == '0') && !mg->cond_failed && ni > 0 && ni <= COND_MAXI &&
                 nb <= 128 && nb * ni <= 1024;
     std::vector<char> is_int((size_t)n, 0);
     for (int64_t c = 0; cond && c < op->n_cells; ++c)
@@ -1654,8 +1683,24 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
         }
       HIP_THROW(hipGetLastError());
     }
-  else
-    assemble_free_block<T>(mg, freel, s);
+  else if (!assemble_free_block<T>(mg, freel, s))
+    {
+      // a cell's interior block E_II is singular: start over without the
+      // static condensation (the free-dof buffers are sized for nf)
+      HIP_THROW(hipStreamSynchronize(s));
+      for (void **q : {(void **)&mg->d_lu, (void **)&mg->d_ipiv, (void **)&mg->d_info,
+                       (void **)&mg->d_rhs, (void **)&mg->d_free, (void **)&mg->d_free_in})
+        {
+          HIP_THROW(hipFree(*q));
+          *q = nullptr;
+        }
+      mg->n_free      = 0;
+      mg->cond        = false;
+      mg->cond_failed = true;
+      fprintf(stderr, "[glsamd] coarse solver: singular interior block in a coarse cell, "
+                      "assembling without static condensation\n");
+      return coarse_lu_setup_t<T>(mg, s);
+    }
   HIP_THROW(hipStreamSynchronize(s));
   const auto t1 = std::chrono::steady_clock::now();
   // GLS_COARSE_LU=npvt (measurement switch): LU without pivoting, identity
@@ -2207,8 +2252,27 @@ coarse_gmres_t(glsMG_ *mg, hipStream_t s)
 }
 
 // Multigrid::level_v_step (deal.II default V-cycle): solution[l] from defect[l]
+void v_step_body(glsMG_ *mg, int l, hipStream_t s);
 void
 v_step(glsMG_ *mg, int l, hipStream_t s)
+{
+  // a deferred reduction handed to the next transfer (rq_level / pp_level)
+  // must not outlive a failed step: a later transfer of that level would read
+  // stale slots and vectors
+  try
+    {
+      v_step_body(mg, l, s);
+    }
+  catch (...)
+    {
+      mg->rq_level = -1;
+      mg->pp_level = -1;
+      throw;
+    }
+}
+
+void
+v_step_body(glsMG_ *mg, int l, hipStream_t s)
 {
   if (l == 0 && mg->desc.coarse_iterate)
     {
@@ -2283,11 +2347,11 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
           void *q0   = mg->qslot[0][(size_t)l], *q1 = mg->qslot[1][(size_t)l];
           rs.defer   = true;
           rs.partial = pend.valid && pend.slots == q0 ? q1 : q0;
-          mg->rq_level = l, mg->rq_slots = rs.partial;
-          mg->rq_x = mg->sol[l], mg->rq_b = mg->def[l];
         }
       gls::brick_launch(mg->ops[l], gls::op_vmult_mode(mg->ops[l]), mg->tmp[l], mg->sol[l], 0,
                         mg->ops[l]->n_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE, s, &rs);
+      if (rs.defer) // (set only once the launch went through)
+        mg->rq_level = l, mg->rq_slots = rs.partial, mg->rq_x = mg->sol[l], mg->rq_b = mg->def[l];
     }
   else
     {
@@ -2300,33 +2364,17 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
       const int64_t w = (int64_t)((size_t)mg->ops[l - 1]->n_dofs * mg->ts() / 4);
       zero_words(mg->def[l - 1], w, s);
     }
-  try
-    {
-      transfer(mg, 1, l, mg->def[l - 1], mg->tmp[l], s);
-    }
-  catch (...)
-    {
-      mg->rq_level = -1;
-      throw;
-    }
+  transfer(mg, 1, l, mg->def[l - 1], mg->tmp[l], s);
   mg->rq_level = -1;
   v_step(mg, l - 1, s);
   // prolongate and add the coarse correction; with an odd number of fused
   // smoothing steps to follow it goes out of place into tmp, so the
   // ping-pong ends in sol without a copy
   const bool odd = gls::fused_relax_ok(mg->ops[l]) && nit % 2 == 1;
-  try
-    {
-      if (odd)
-        transfer(mg, 0, l, mg->tmp[l], mg->sol[l - 1], s, mg->sol[l]);
-      else
-        transfer(mg, 0, l, mg->sol[l], mg->sol[l - 1], s);
-    }
-  catch (...)
-    {
-      mg->pp_level = -1;
-      throw;
-    }
+  if (odd)
+    transfer(mg, 0, l, mg->tmp[l], mg->sol[l - 1], s, mg->sol[l]);
+  else
+    transfer(mg, 0, l, mg->sol[l], mg->sol[l - 1], s);
   mg->pp_level = -1;
   // post-smoothing (MGSmootherPrecondition::smooth -> step); on the finest
   // level its last step also writes the FP64 result (copy_from_mg folded)
@@ -2863,6 +2911,12 @@ mg_check_outer(glsMG mg, const glsOp_ *op)
                              "operator's size");
   if (!mg->setup_done)
     throw std::runtime_error("gls_gmres_solve: the multigrid is not set up (gls_mg_setup)");
+}
+
+bool
+mg_is_linear(glsMG mg)
+{
+  return !mg->desc.coarse_iterate;
 }
 
 void

@@ -223,6 +223,9 @@ void mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s);
 // throws unless mg can precondition op's FP64 Krylov vectors in place: outer
 // precision FP64, finest level of op's size, gls_mg_setup done
 void mg_check_outer(glsMG mg, const glsOp_ *op);
+// true when one V-cycle is a linear map of its input (no coarse solve
+// iterated to a tolerance): GMRES may then keep M^{-1} v_j (krylov.hip)
+bool mg_is_linear(glsMG mg);
 // outflow boundary-face terms (faces.hip), launched after the cell kernels
 void faces_setup(glsOp_ *op, const glsOpDesc *d);
 void faces_release(glsOp_ *op);

@@ -231,3 +231,62 @@ print(s.last["n_iterations"])
     print(f"GMRES iterations Pythagorean {ip} / three-pass {i3}, solution rel diff {diff:.2e}")
     assert abs(ip - i3) <= 1
     assert diff < 1e-7
+
+
+def test_gmres_kept_directions_nonlinear_preconditioner(monkeypatch):
+    """x += Z y (the kept z_j = M^{-1} v_j) equals deal.II's x += M^{-1}(V y)
+    (solver_l.cc:62, right preconditioning) only for a LINEAR preconditioner.
+    A V-cycle whose coarse solve is GMRES to a tolerance (coarse_iterate, the
+    reference's default coarse_grid_iterate, multigrid.h:36) is not linear, so
+    the solver takes the M^{-1}(V y) form there by itself: the default solve
+    and the forced M^{-1}(V y) form (GLS_GMRES_ZKEEP=0) run the same algorithm
+    (same iteration count up to the LDS-atomic order's noise); the forced kept
+    form (GLS_GMRES_ZKEEP=1) is the deviation this pins: it converges too, to
+    a solution of the same tolerance class."""
+    import torch
+    import glsamd
+    import glsinputs as gi
+    from helpers import Case, deck
+    d = deck("input_sphere_amg.json")
+    meshes = [d.mesh(r) for r in range(2)]
+    vel, p, slip = d.boundary_descriptor()
+    cmasks = [m.constraint_mask(vel, p, slip) for m in meshes]
+    params, w = d.operator_parameters()
+    u = gi.linearization_point(meshes[-1].n_nodes, meshes[-1].dim, d.u_max)
+    hist = gi.history(u, params["order"])
+    mg, _ = glsamd.build_gmg(meshes, cmasks, params, u, hist, w, precision="f32",
+                             coarse_n_iterations=10, coarse_iterate=True, coarse_reltol=1e-4,
+                             coarse_maxiter=500)
+    A = glsamd.NavierStokesOperator(meshes[-1], cmasks[-1], "f64")
+    A.set_parameters(**params)
+    A.set_linearization_point(u)
+    A.set_previous_solution(hist, w)
+    b = gi.rnd(7, meshes[-1].n_dofs)
+    rel = 1e-8
+    out = {}
+    for tag, env in (("auto", None), ("zkeep0", "0"), ("zkeep1", "1")):
+        if env is None:
+            monkeypatch.delenv("GLS_GMRES_ZKEEP", raising=False)
+        else:
+            monkeypatch.setenv("GLS_GMRES_ZKEEP", env)
+        s = glsamd.LinearSolverGMRES(A, mg, n_max_iterations=400, relative_tolerance=rel,
+                                     max_n_tmp_vectors=12)
+        x = A.initialize_dof_vector()
+        s.solve(x, A._dev(b))
+        torch.cuda.synchronize()
+        out[tag] = (dict(s.last), _np(x))
+    monkeypatch.delenv("GLS_GMRES_ZKEEP", raising=False)
+    o = Case(meshes[-1], cmasks[-1], params, w, d.u_max).oracle()
+    res = {t: np.linalg.norm(b - o.vmult(x)) for t, (_, x) in out.items()}
+    its = {t: st["n_iterations"] for t, (st, _) in out.items()}
+    x0 = out["zkeep0"][1]
+    diff = {t: np.linalg.norm(x - x0) / np.linalg.norm(x0) for t, (_, x) in out.items()}
+    print("iterations", its, "true residuals", res, "rel diff to zkeep0", diff)
+    tol = out["auto"][0]["tolerance"]
+    for t, (st, _) in out.items():
+        assert st["converged"] == 1, (t, st)
+        assert st["n_restarts"] >= 1, (t, st)  # the restart update is exercised
+    assert abs(its["auto"] - its["zkeep0"]) <= 2, its
+    assert diff["auto"] < 1e-4, diff
+    assert res["auto"] <= 64 * tol and res["zkeep0"] <= 64 * tol, (res, tol)
+    assert res["zkeep1"] <= 64 * tol, (res, tol)
