@@ -20,7 +20,7 @@ AMD_LIBS := -L/opt/rocm/lib -lrocsolver -lrocblas -lrccl -Wl,-rpath,/opt/rocm/li
 
 MESH_SRC := $(PKG)/host/mesh.cc
 AMD_SRC  := $(wildcard $(PKG)/csrc/*.hip) $(wildcard $(PKG)/csrc/*.cc)
-AMD_HDR  := $(wildcard $(PKG)/csrc/*.h) $(wildcard $(PKG)/csrc/*.cuh) include/gls_op.h
+AMD_HDR  := $(wildcard $(PKG)/csrc/*.h) $(wildcard $(PKG)/csrc/*.inc) $(wildcard $(PKG)/csrc/*.cuh) include/gls_op.h
 
 all: mesh amd oracle cpptest
 

@@ -101,6 +101,11 @@ def cpu_baseline(o, src, n_dofs, budget_s=12.0):
                        f"agrees with the scalar oracle to {chk:.1e}")
 
 
+def _comp_get(comp, key, field):
+    v = (comp or {}).get(key)
+    return v.get(field) if isinstance(v, dict) else None
+
+
 def _timed_vmults(op, dst, src, reps, flush=None):
     """Median per-vmult duration (ms) with HIP events on the launch stream
     (torch's current stream); `flush` runs between reps, outside the events."""
@@ -998,6 +1003,7 @@ def main():
                                    f"Q2/Q2, MappingQ2, BDF2, increment form",
                        "cells": mesh.n_cells, "dofs": n_dofs, "cells_per_gpu": local_cells,
                        "general_geometry_cells": n_gen, "cartesian_cells": n_cart,
+                       "brick_shape": list(op.brick_shape) if hasattr(op, "brick_shape") else None,
                        "parallelism": f"cells x-slab partitioned over {world} GPU(s)"
                                       + (f", ghost exchange {exchange}" if exchange else "")},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
@@ -1009,7 +1015,14 @@ def main():
                          "streamed_bytes": op.vmult_bytes(),
                          # the same launch time against what the kernel reads
                          # (16 instead of SURVEY's 20 table values per q)
-                         "frac_streamed": op.vmult_bytes() / (kernel_ms * 1e-3) / HBM_PEAK},
+                         "frac_streamed": op.vmult_bytes() / (kernel_ms * 1e-3) / HBM_PEAK,
+                         # SURVEY §8d's cold r2 figure (MALL flushed by a 1 GiB
+                         # write between vmults; the warm 133 MB working set fits
+                         # the 256 MB MALL) and the HBM-bound r+1 mesh back to
+                         # back, from the companions below (null without them)
+                         "frac_cold": _comp_get(comp, f"r{n_ref}_f64_cold", "roofline_frac"),
+                         "frac_r3": _comp_get(comp, f"r{n_ref + 1}_f64_warm",
+                                              "roofline_frac_back_to_back")},
             "cpu_baseline": cpu,
             "parity": parity,
             "companions": comp if dist_comp is None else dict(comp or {}, **dist_comp),

@@ -125,6 +125,7 @@ struct BrickArgs
   int             L, Lx, Ly;
   int             PLx, PLy, LP; // padded LDS lattice strides / size (>= L)
   T               nu, w0, theta, stau;
+  T               nu4, stau2; // 4 nu, stau^2 (delta_qwise_fast)
   int             td, cw, have_prev, have_old_grad;
   Shape<T, n>     sh;
 };
@@ -375,7 +376,7 @@ load_lane(const BrickArgs<T, dim, k + 1> &a, int64_t cell0, int64_t chunk0, int 
                           i == e  ? a.geo_cart + i * a.n_cells + cell :
                                     a.geo_cart + (i * dim + e));
     }
-  else if (general)
+  else if (GEO == GEO_GEN)
     {
       const int64_t gq = qindex<dim, n>(cell, p, a.n_cells);
       r.JxW            = a.geo_gen[gq];
@@ -472,565 +473,58 @@ to_packs(const T (&x)[nc], V (&v)[NP])
       v[kp][w] = kp * W + w < nc ? x[kp * W + w] : T(0);
 }
 
-// The Cartesian FP64 3D Q2 vmult kernel (Newton, fixed point) fits 128
-// VGPRs (4 waves/SIMD) with its tables issued at the start of each round (in
-// flight during the evaluate sweeps) and an unpadded lattice (4 workgroups
-// per CU in LDS); the per-q geometry of curved bricks keeps 3 waves/SIMD and
-// the earlier prefetch (issued behind the previous round's Dq^T sweeps), as
-// do the other instantiations.
-// (A GEO_ANY kernel whose curved bricks load J^{-1} at its two points of
-// use instead of with the tables still needs 162 VGPRs: measured round 3;
-// forced to 4 waves it spills 140 B/lane inside the round loop and takes
-// 63.7 instead of 40.2 us at r2, 517 instead of 276 us at r3: round 4,
-// profiles/r04/explore/ab_any4_spill.txt.)
+// Occupancy.  The FP64 3D Q2 vmult kernels (Newton, fixed point) with
+// one-layer bricks run 4 waves/SIMD (<= 128 VGPRs, unpadded 34 KB lattice: 4
+// workgroups per CU) for Cartesian AND curved bricks: the round loop is
+// compiled once per brick geometry (a GEO_ANY launch branches per brick,
+// wave-uniformly), and
+//  * a Cartesian brick issues a round's tables and its diagonal J^{-1} / det J
+//    at the start of that round (LATE: in flight during the evaluate sweeps);
+//  * a curved brick issues its tables and per-q J^{-1} / JxW after the
+//    evaluate sweeps (AT_USE: nothing in flight across them) and parks J^{-1}
+//    in its own sweep-buffer slots (free between the evaluate and the
+//    integrate sweeps) from the real-space gradients to the test-function
+//    transform, so the physics holds no more registers than the Cartesian
+//    one's.  Scheduling barriers keep the compiler from hoisting those loads
+//    and the LDS reload back into the evaluate sweeps / the physics.
+// (Round 4 had one mixed-geometry body: 164 VGPRs, 3 waves; forced to 4 it
+// spilled 140 B/lane and took 63.7 instead of 40.2 us at r2.)  The other
+// instantiations (FP64 residual, two-layer bricks, other degrees) keep the
+// earlier prefetch (issued behind the previous round's Dq^T sweeps) at 3
+// waves; the FP32 kernels fit 4 waves with it.
 template <int dim, int k, typename T, int MODE, int GEO, int ZL = 1>
 struct BrickOcc
 {
-  static constexpr bool cart4 = GEO == GEO_CART && sizeof(T) == 8 && dim == 3 && k == 2 &&
-                                MODE != MODE_RESIDUAL && ZL == 1;
-  static constexpr int  waves = cart4 || sizeof(T) == 4 ? 4 : 3;
-  static constexpr bool late  = cart4; // tables issued at the start of each round
+  static constexpr bool four  = sizeof(T) == 8 && dim == 3 && k == 2 && MODE != MODE_RESIDUAL &&
+                               ZL == 1;
+  static constexpr int  waves = four || sizeof(T) == 4 ? 4 : 3;
 };
 
 template <int dim, int k, typename T, int MODE, int GEO = GEO_ANY, int ZL = 1>
 __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO, ZL>::waves))
   k_brick(BrickArgs<T, dim, k + 1> a)
 {
-  using LDS          = BrickLDS<dim, k, T>;
-  using V            = typename Pack<T>::V;
-  constexpr int n    = k + 1;
-  constexpr int nq   = LDS::nq;
-  constexpr int nc   = LDS::nc;
-  constexpr int W    = LDS::W;
-  constexpr int NP   = LDS::NP;
-  constexpr int CPW  = LDS::CPW;
-  constexpr int WPB  = LDS::WPB;
-  constexpr int WB   = LDS::WB;
-  constexpr bool R   = MODE == MODE_RESIDUAL;
-  constexpr bool LATE = BrickOcc<dim, k, T, MODE, GEO, ZL>::late;
-  static_assert(nq <= 64, "one cell must fit a wavefront");
-
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int L      = a.L;  // lattice nodes (global order of brick_nodes)
-  const int LP     = a.LP; // padded LDS lattice (bank-conflict-free x sweep)
-  V        *s_src  = reinterpret_cast<V *>(smem);   // [NP][LP] brick src values
-  V        *s_work = s_src + NP * LP;               // [WPB*CPW][WB]
-  // the accumulator lattice is FP64 for both precisions: ds_add_f32 costs
-  // ~10 us per FP32 vmult on gfx950 (racy plain-add ablation: 38.1 -> 28.2
-  // us), ds_add_f64 next to nothing (40.1 -> 39.7 us)
-  double   *s_acc  = reinterpret_cast<double *>(s_work + WPB * CPW * WB); // [nc][LP]
-  constexpr int RP = CoefRow<T, n>::RP;
-  T        *s_tab  = reinterpret_cast<T *>(reinterpret_cast<unsigned char *>(s_acc) +
-                                     LDS::tab_offset(LP)); // [4][n][RP]
-  const T  *sS     = s_tab + TAB_S * n * RP;
-  const T  *sST    = s_tab + TAB_ST * n * RP;
-  const T  *sD     = s_tab + TAB_D * n * RP;
-  const T  *sDT    = s_tab + TAB_DT * n * RP;
-  // lattice position of each brick cell's first node (cell-major order
-  // x, y, z): one LDS read per round instead of per-lane divisions by the
-  // runtime brick shape, which the compiler would hoist into registers
-  int      *s_org  = reinterpret_cast<int *>(s_tab + 4 * n * RP); // [ORG]
-
-  const int brick = (int)a.brick_begin + (int)blockIdx.x;
-  if (brick >= (int)a.brick_end)
-    return;
-  const int t = threadIdx.x;
-  if (t < n * RP)
+  if constexpr (GEO == GEO_ANY && BrickOcc<dim, k, T, MODE, GEO, ZL>::four)
     {
-      const int  r = t / RP, j = t % RP;
-      const bool v = j < n;
-      s_tab[TAB_S * n * RP + t]  = v ? a.sh.S[r][j] : T(0);
-      s_tab[TAB_ST * n * RP + t] = v ? a.sh.S[j][r] : T(0);
-      s_tab[TAB_D * n * RP + t]  = v ? a.sh.Dq[r][j] : T(0);
-      s_tab[TAB_DT * n * RP + t] = v ? a.sh.Dq[j][r] : T(0);
-    }
-  if (t < a.bx * a.by * a.bz && t < LDS::ORG)
-    {
-      const int cx = t % a.bx, cy = (t / a.bx) % a.by, cz = t / (a.bx * a.by);
-      s_org[t]     = cx * k + a.PLx * (cy * k + a.PLy * cz * k);
-    }
-  const int  wave    = t >> 6, lane = t & 63;
-  const int  slot    = lane / nq;
-  const int  p       = lane - slot * nq;
-  const bool in_wave = slot < CPW;
-  // left-over lanes (64 % nq) only read the first slot's buffer; every LDS
-  // store of the sweeps is guarded by in_wave
-  V         *A       = s_work + (wave * CPW + (in_wave ? slot : 0)) * WB;
-  using BL           = BufLayout<dim, n, NP>;
-  V         *B       = A + NP * BL::KS;
-  const int  pa[3]   = {p % n, (p / n) % n, dim == 3 ? p / (n * n) : 0};
-  const int  st[3]   = {1, BL::PY, BL::PZ};               // buffer strides
-  const int  q       = pa[0] + BL::PY * pa[1] + BL::PZ * pa[2]; // own slot
-  const int  lpa     = pa[0] + a.PLx * (pa[1] + a.PLy * pa[2]);  // lattice offset in a cell
-  const int  step    = CPW * WPB;
-
-  // ---- prologue: every load that does not depend on another is issued
-  // up front (lattice node ids, write-out targets, round 0's geometry and
-  // tables), so the block pays one HBM latency before its first sweep
-  constexpr int   NI = (BrickLattice<dim, k, ZL>::L + BLOCK - 1) / BLOCK;
-  const uint32_t *bn = a.brick_nodes + brick * (int64_t)L;
-  const uint32_t *bt = a.brick_target + brick * (int64_t)L;
-  uint32_t        pk[NI], tg[NI];
-#pragma unroll
-  for (int it = 0; it < NI; ++it)
-    {
-      const int i = t + it * BLOCK;
-      pk[it]      = i < L ? bn[i] : 0u;
-      tg[it]      = i < L ? bt[i] : 0u;
-    }
-  const uint32_t binfo   = a.brick_geo[brick];
-  const bool     general = GEO == GEO_GEN || (GEO == GEO_ANY && (binfo & 1u) != 0);
-  const int      ncell   = (int)(binfo >> 8);
-  const uint32_t cell0   = a.brick_cell0[brick];
-  const uint32_t chunk0  = a.brick_chunk0[brick];
-
-  // ---- stage the brick's src values once per node (read_dof_values:
-  // homogeneous constraints read as 0; the residual reads plain values).
-  // The gather is issued before round 0's loads: vmcnt retires in order, so
-  // the staging then waits for the gather only.
-  const int Lxy = a.Lx * a.Ly;
-  T         u[NI][nc];
-  // deferred reduction of the previous apply (one 16-byte pack per node)
-  constexpr bool QREC = sizeof(T) == 4 && !R && nc * sizeof(T) == 16;
-#pragma unroll
-  for (int it = 0; it < NI; ++it)
-    {
-      const int      i    = t + it * BLOCK;
-      const uint32_t node = pk[it] & NODE_MASK;
-      if (QREC && i < L && node != UNUSED_NODE && a.qslots && (tg[it] & SHARED_BIT))
+      // the round loop compiled once per brick geometry (BrickOcc)
+      const int brick = (int)a.brick_begin + (int)blockIdx.x;
+      if (brick >= (int)a.brick_end)
+        return;
+      if (a.brick_geo[brick] & 1u) // (wave-uniform: per brick)
         {
-          // the previous apply's shared-node reduction of this node, in
-          // k_shared_reduce_cls's order and arithmetic (bitwise the same)
-          const uint32_t slt = tg[it] & ~SHARED_BIT;
-          const int      kc  = slot_class(a.rc, slt);
-          const uint32_t m   = a.rc.mult[kc];
-          const uint32_t b0  = a.rc.slot0[kc] + (slt - a.rc.slot0[kc]) / m * m;
-          const V       *pp  = reinterpret_cast<const V *>(a.qslots);
-          V              sum = {};
-          uint32_t       j   = 0;
-          for (; j + 4 <= m; j += 4)
-            {
-              const V x0 = pp[b0 + j], x1 = pp[b0 + j + 1], x2 = pp[b0 + j + 2],
-                      x3 = pp[b0 + j + 3];
-              sum += (x0 + x1) + (x2 + x3);
-            }
-          if (j + 2 <= m)
-            {
-              const V x0 = pp[b0 + j], x1 = pp[b0 + j + 1];
-              sum += x0 + x1;
-              j += 2;
-            }
-          if (j < m)
-            sum += pp[b0 + j];
-          const V        xs = reinterpret_cast<const V *>(a.qprev)[node];
-          const V        bb = reinterpret_cast<const V *>(a.qb)[node];
-          const V        dd = a.qd ? reinterpret_cast<const V *>(a.qd)[node] : V{} + T(1);
-          const uint32_t cm = pk[it] >> 28;
-#pragma unroll
-          for (int w = 0; w < W; ++w)
-            if ((cm >> w) & 1)
-              sum[w] = xs[w];
-          const V v = xs + a.qomega * dd * (bb - sum);
-          reinterpret_cast<V *>(a.qsrc_w)[node] = v;
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-            u[it][c] = v[c % W];
-        }
-      else if (i < L && node != UNUSED_NODE)
-        load_node<T, nc>(a.src, node, u[it]);
-      else
-#pragma unroll
-        for (int c = 0; c < nc; ++c)
-          u[it][c] = T(0);
-    }
-  // FP32 (multigrid levels): the fused relaxation's operands b, d and the
-  // unmodified src of the exclusive nodes are loaded here, behind the
-  // gather, instead of after the cell rounds (one memory round trip less at
-  // the end of every brick; FP64 has no registers to spare for them)
-  // (two-layer bricks: two lattice chunks per thread; the operands' 24
-  // registers would spill, so they are read at the write-out)
-  constexpr bool PRE = sizeof(T) == 4 && !R && ZL == 1;
-  constexpr int  NPR = PRE ? NI : 1;
-  T              xb[NPR][nc], xd[NPR][nc], xs[NPR][nc];
-  if constexpr (PRE)
-    {
-#pragma unroll
-      for (int it = 0; it < NI; ++it)
-        {
-          const int  i    = t + it * BLOCK;
-          const bool excl = i < L && tg[it] != UNUSED_NODE && !(tg[it] & SHARED_BIT);
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-            {
-              xs[it][c] = u[it][c];
-              xb[it][c] = T(0);
-              xd[it][c] = T(1);
-            }
-          if (excl && a.rb)
-            {
-              load_node<T, nc>(a.rb, tg[it], xb[it]);
-              if (a.rd)
-                load_node<T, nc>(a.rd, tg[it], xd[it]);
-            }
-        }
-    }
-  LaneData<dim, T, MODE> cur;
-  load_lane<dim, k, T, MODE, GEO>(a, cell0, chunk0, ncell, general, wave * CPW + slot, in_wave, p,
-                                  pa, cur);
-#pragma unroll
-  for (int it = 0; it < NI; ++it)
-    {
-      const int i = t + it * BLOCK;
-      if (i >= L)
-        break;
-      const int      iz = i / Lxy, iy = (i - iz * Lxy) / a.Lx;
-      const int      ip = (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
-      const uint32_t cm = pk[it] >> 28;
-#pragma unroll
-      for (int c = 0; c < nc; ++c)
-        {
-          if (!R && ((cm >> c) & 1))
-            u[it][c] = T(0);
-          s_acc[c * LP + ip] = 0.0;
-        }
-      V v[NP];
-      to_packs<V, T, nc, NP, W>(u[it], v);
-#pragma unroll
-      for (int kp = 0; kp < NP; ++kp)
-        s_src[kp * LP + ip] = v[kp];
-    }
-  __syncthreads();
-
-  // the lane's tensor quadrature weight (Cartesian bricks: JxW = det J w_q)
-  T wq_lane = a.sh.w[pa[0]] * a.sh.w[pa[1]];
-  if (dim == 3)
-    wq_lane *= a.sh.w[pa[2]];
-  for (int base = 0; base < ncell; base += step)
-    {
-      // LATE: a round's geometry and tables are issued at the start of that
-      // round (in flight during its evaluate sweeps) instead of before the
-      // previous round's integrate sweeps: fewer registers live across the
-      // integrate sweeps
-      if (LATE && base > 0)
-        load_lane<dim, k, T, MODE, GEO>(a, cell0, chunk0, ncell, general,
-                                        base + wave * CPW + slot, in_wave, p, pa, cur);
-
-      // the lane's lattice node this round (inactive lanes: the first cell's)
-      const int li = (cur.active ? s_org[base + wave * CPW + slot] : 0) + lpa;
-      // ---- evaluate: x sweep straight from the src lattice, then y (, z).
-      // Each sweep reads its coefficient row once for every pack and issues
-      // every pack's reads before the first store (a store could alias the
-      // tables or the next pack's reads: interleaved, each pack would wait
-      // one LDS round trip of its own)
-      if (in_wave)
-        {
-          T c[n];
-          coefs<n>(sS, pa[0], c);
-          V r[NP];
-#pragma unroll
-          for (int kp = 0; kp < NP; ++kp)
-            r[kp] = contract_c<n>(s_src + kp * LP, c, li - pa[0], 1);
-#pragma unroll
-          for (int kp = 0; kp < NP; ++kp)
-            A[kp * BL::KS + q] = r[kp];
-        }
-      wave_sync();
-      V *in = A, *out = B;
-#pragma unroll
-      for (int ax = 1; ax < dim; ++ax)
-        {
-          if (in_wave)
-            {
-              T c[n];
-              coefs<n>(sS, pa[ax], c);
-              V r[NP];
-#pragma unroll
-              for (int kp = 0; kp < NP; ++kp)
-                r[kp] = contract_c<n>(in + kp * BL::KS, c, q - pa[ax] * st[ax], st[ax]);
-#pragma unroll
-              for (int kp = 0; kp < NP; ++kp)
-                out[kp * BL::KS + q] = r[kp];
-            }
-          wave_sync();
-          V *tmp = in;
-          in     = out;
-          out    = tmp;
-        }
-      // values and reference-space gradients (collocation derivative);
-      // left-over lanes stay out of the reads (they would only add bank
-      // conflicts in their ds_read_b128 lane groups)
-      T val[nc], gref[nc][dim];
-#pragma unroll
-      for (int c = 0; c < nc; ++c)
-        {
-          val[c] = T(0);
-#pragma unroll
-          for (int ax = 0; ax < dim; ++ax)
-            gref[c][ax] = T(0);
-        }
-      if (in_wave)
-#pragma unroll
-        for (int kp = 0; kp < NP; ++kp)
-          {
-            const V v = in[kp * BL::KS + q];
-            V       g[dim];
-#pragma unroll
-            for (int ax = 0; ax < dim; ++ax)
-              g[ax] = contract_v<n>(in + kp * BL::KS, sD, pa[ax], q - pa[ax] * st[ax], st[ax]);
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-              if (kp * W + w < nc)
-                {
-                  val[kp * W + w] = v[w];
-#pragma unroll
-                  for (int ax = 0; ax < dim; ++ax)
-                    gref[kp * W + w][ax] = g[ax][w];
-                }
-          }
-      wave_sync();
-
-      // ---- q-point physics (do_vmult_cell)
-      // real-space gradients J^{-T} grad_ref: Cartesian bricks (wave-uniform
-      // branch) have a diagonal J^{-1}
-      T gu[dim][dim], gp[dim];
-      if (general)
-        {
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-#pragma unroll
-            for (int e = 0; e < dim; ++e)
-              {
-                T s = 0;
-#pragma unroll
-                for (int i = 0; i < dim; ++i)
-                  s += cur.inv[i][e] * gref[c][i];
-                if (c < dim)
-                  gu[c][e] = s;
-                else
-                  gp[e] = s;
-              }
+          constexpr int G = GEO_GEN;
+#include "brick_body.inc"
         }
       else
         {
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-#pragma unroll
-            for (int e = 0; e < dim; ++e)
-              {
-                const T s = cur.inv[e][e] * gref[c][e];
-                if (c < dim)
-                  gu[c][e] = s;
-                else
-                  gp[e] = s;
-              }
+          constexpr int G = GEO_CART;
+#include "brick_body.inc"
         }
-      T vr[nc], gr[nc][dim];
-      T d1 = cur.d1, d2 = cur.d2;
-      if (delta_otf<k, MODE>() && !a.cw)
-        {
-          T u2 = 0;
-#pragma unroll
-          for (int d = 0; d < dim; ++d)
-            u2 += cur.U[d] * cur.U[d];
-          delta_qwise_fast(u2, cur.h, a.nu, a.stau, d1, d2);
-        }
-      if constexpr (MODE == MODE_NEWTON)
-        qpoint_newton_t1<dim, T>(val, val[dim], gu, gp, cur.U, cur.GU, cur.T1, d1, d2, a.nu,
-                                 a.w0, a.td, vr, gr);
-      else
-        qpoint_physics<dim, T, MODE>(val, val[dim], gu, gp, cur.U, cur.GU, cur.T1, cur.UT,
-                                     cur.oldg, d1, d2, a.nu, a.w0, a.theta, a.td,
-                                     a.have_prev, a.have_old_grad, vr, gr);
-      // submit_value / submit_gradient (JxW, J^{-T}); inactive lanes: JxW 0
-      const T JxW = general ? (cur.active ? cur.JxW : T(0))
-                            : (cur.active ? cur.JxW * wq_lane : T(0));
-      T       wq[nc], ghat[dim][nc];
-      if (general)
-        {
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-            {
-              wq[c] = vr[c] * JxW;
-#pragma unroll
-              for (int i = 0; i < dim; ++i)
-                {
-                  T s = 0;
-#pragma unroll
-                  for (int e = 0; e < dim; ++e)
-                    s += cur.inv[i][e] * gr[c][e];
-                  ghat[i][c] = s * JxW;
-                }
-            }
-        }
-      else
-        {
-          T sc[dim];
-#pragma unroll
-          for (int i = 0; i < dim; ++i)
-            sc[i] = cur.inv[i][i] * JxW;
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-            {
-              wq[c] = vr[c] * JxW;
-#pragma unroll
-              for (int i = 0; i < dim; ++i)
-                ghat[i][c] = gr[c][i] * sc[i];
-            }
-        }
-
-      // ---- integrate: Dq^T on the gradient part (two axes per exchange
-      // through the A/B halves), then S^T sweeps z (, y); the x sweep is
-      // fused with the accumulation into the brick lattice
-      V wv[NP];
-      to_packs<V, T, nc, NP, W>(wq, wv);
-#pragma unroll
-      for (int ax0 = 0; ax0 < dim; ax0 += 2)
-        {
-          if (in_wave)
-            {
-              V g0[NP];
-              to_packs<V, T, nc, NP, W>(ghat[ax0], g0);
-#pragma unroll
-              for (int kp = 0; kp < NP; ++kp)
-                A[kp * BL::KS + q] = g0[kp];
-              if (ax0 + 1 < dim)
-                {
-                  V g1[NP];
-                  to_packs<V, T, nc, NP, W>(ghat[(ax0 + 1) % dim], g1);
-#pragma unroll
-                  for (int kp = 0; kp < NP; ++kp)
-                    B[kp * BL::KS + q] = g1[kp];
-                }
-            }
-          wave_sync();
-          if (in_wave)
-#pragma unroll
-            for (int kp = 0; kp < NP; ++kp)
-              {
-                wv[kp] += contract_v<n>(A + kp * BL::KS, sDT, pa[ax0], q - pa[ax0] * st[ax0],
-                                        st[ax0]);
-                if (ax0 + 1 < dim)
-                  {
-                    const int ax1 = (ax0 + 1) % dim;
-                    wv[kp] += contract_v<n>(B + kp * BL::KS, sDT, pa[ax1],
-                                            q - pa[ax1] * st[ax1], st[ax1]);
-                  }
-              }
-          wave_sync();
-        }
-      if (in_wave)
-#pragma unroll
-        for (int kp = 0; kp < NP; ++kp)
-          A[kp * BL::KS + q] = wv[kp];
-      // the next round's geometry and tables: issued here (few registers
-      // live), in flight during the S^T sweeps and the next evaluate (this
-      // round's lattice position is kept: the prefetch overwrites cur)
-      const int  li_now     = li;
-      const bool active_now = cur.active;
-      if (!LATE && base + step < ncell)
-        load_lane<dim, k, T, MODE, GEO>(a, cell0, chunk0, ncell, general,
-                                        base + step + wave * CPW + slot, in_wave, p, pa, cur);
-      wave_sync();
-      in  = A;
-      out = B;
-#pragma unroll
-      for (int ax = dim - 1; ax >= 1; --ax)
-        {
-          if (in_wave)
-            {
-              T c[n];
-              coefs<n>(sST, pa[ax], c);
-              V r[NP];
-#pragma unroll
-              for (int kp = 0; kp < NP; ++kp)
-                r[kp] = contract_c<n>(in + kp * BL::KS, c, q - pa[ax] * st[ax], st[ax]);
-#pragma unroll
-              for (int kp = 0; kp < NP; ++kp)
-                out[kp * BL::KS + q] = r[kp];
-            }
-          wave_sync();
-          V *tmp = in;
-          in     = out;
-          out    = tmp;
-        }
-      T cx[n];
-      coefs<n>(sST, pa[0], cx);
-      if (active_now)
-#pragma unroll
-        for (int kp = 0; kp < NP; ++kp)
-          {
-            const V r = contract_c<n>(in + kp * BL::KS, cx, q - pa[0], 1);
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-              if (kp * W + w < nc)
-                lds_add(s_acc + (kp * W + w) * LP + li_now, (double)r[w]);
-          }
-      wave_sync();
     }
-  __syncthreads();
-
-  // ---- write out: exclusive nodes -> dst, boundary nodes -> partials
-#pragma unroll
-  for (int it = 0; it < NI; ++it)
+  else
     {
-      const int i = t + it * BLOCK;
-      if (i >= L)
-        break;
-      const int      iz  = i / Lxy, iy = (i - iz * Lxy) / a.Lx;
-      const int      ip  = (i - iz * Lxy - iy * a.Lx) + a.PLx * (iy + a.PLy * iz);
-      const uint32_t tgt = tg[it];
-      if (tgt == UNUSED_NODE)
-        continue;
-      double acc[nc];
-#pragma unroll
-      for (int c = 0; c < nc; ++c)
-        acc[c] = s_acc[c * LP + ip];
-      T r[nc];
-      if (tgt & SHARED_BIT)
-        {
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-            r[c] = (T)(R ? -acc[c] : acc[c]);
-          store_node<T, nc>(a.partial, tgt & ~SHARED_BIT, r);
-          continue;
-        }
-      const uint32_t cm = pk[it] >> 28;
-#pragma unroll
-      for (int c = 0; c < nc; ++c)
-        {
-          r[c] = (T)(R ? -acc[c] : acc[c]);
-          if ((cm >> c) & 1)
-            r[c] = R ? T(0) : (PRE ? xs[PRE ? it : 0][c] : a.src[(size_t)tgt * nc + c]);
-        }
-      if constexpr (PRE)
-        {
-          if (a.rb)
-#pragma unroll
-            for (int c = 0; c < nc; ++c)
-              {
-                const T base = a.rkeep ? xs[it][c] : T(0);
-                r[c]         = base + a.romega * xd[it][c] * (xb[it][c] - r[c]);
-              }
-        }
-      else if constexpr (!R)
-        if (a.rb)
-#pragma unroll
-          for (int c = 0; c < nc; ++c)
-            {
-              const size_t j    = (size_t)tgt * nc + c;
-              const T      base = a.rkeep ? a.src[j] : T(0);
-              r[c]              = base + a.romega * (a.rd ? a.rd[j] : T(1)) * (a.rb[j] - r[c]);
-            }
-      store_node<T, nc>(a.dst, tgt, r);
-      if constexpr (sizeof(T) == 4 && !R)
-        if (a.out64)
-          {
-            double r64[nc];
-#pragma unroll
-            for (int c = 0; c < nc; ++c)
-              r64[c] = (double)r[c];
-            store_node<double, nc>(a.out64, tgt, r64);
-          }
+      constexpr int G = GEO;
+#include "brick_body.inc"
     }
 }
 

@@ -838,25 +838,41 @@ struct Impl
         a.L             = op->L;
         a.Lx            = op->Lx;
         a.Ly            = op->Ly;
-        // padded LDS lattice: 3D Q2 bricks of 4x4 cells in x, y use strides
-        // 11, 12 (ds_read_b128 conflict-free x sweep, exhaustive search);
-        // the FP64 Cartesian kernel takes the unpadded lattice (4 workgroups
-        // per CU in LDS)
-        auto set_lattice = [&](bool general) {
-          // (the 4-wave Cartesian FP64 kernels: BrickOcc<...>::cart4)
-          const bool cart4 = !general && sizeof(T) == 8 && mode != MODE_RESIDUAL && dim == 3 &&
-                             k == 2;
-          const bool pad   = dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9 && op->L == 243 &&
-                           (sizeof(T) == 8 ? !cart4 : true);
-          a.PLx = pad ? 11 : op->Lx;
-          a.PLy = pad ? 12 : op->Ly;
-          a.LP  = a.PLx * a.PLy * (op->L / (op->Lx * op->Ly));
+        // LDS lattice strides of 3D Q2 bricks of 4x4 cells in x, y (9 x 9
+        // nodes per layer): the widest padding the kernel's LDS budget takes
+        // at its occupancy (160 KB / workgroups per CU, one wave per SIMD
+        // each): 11 x 12 -- the x-sweep's ds_read_b128 conflict-free and the
+        // lattice accumulation's ds_add_f64 at 7 instead of 12 LDS cycles
+        // (bank model of MI355X_MICROARCH §LDS, scripts/lds_layout_search.py
+        // --lattice) -- else 9 x 11 (the 4-wave FP64 kernels: reads 5 / adds 7
+        // cycles, 297 of the 328 lattice positions their 40 KB allow), else
+        // unpadded (reads 8 / adds 12)
+        auto set_lattice = [&](bool) {
+          const bool four  = sizeof(T) == 8 && mode != MODE_RESIDUAL && dim == 3 && k == 2 &&
+                            op->L == 243; // BrickOcc<...>::four
+          const int  waves = four || sizeof(T) == 4 ? 4 : 3;
+          const int  nz    = op->L / (op->Lx * op->Ly);
+          const size_t budget = (size_t)160 * 1024 / waves;
+          a.PLx = op->Lx, a.PLy = op->Ly;
+          if (dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9)
+            {
+              static constexpr int pads[2][2] = {{11, 12}, {9, 11}};
+              for (const auto &pl : pads)
+                if (BrickLDS<dim, k, T>::bytes(pl[0] * pl[1] * nz) <= budget)
+                  {
+                    a.PLx = pl[0], a.PLy = pl[1];
+                    break;
+                  }
+            }
+          a.LP = a.PLx * a.PLy * nz;
         };
         set_lattice(false);
         a.nu            = (T)op->prm.nu;
         a.w0            = (T)op->prm.w0;
         a.theta         = (T)op->prm.theta;
         a.stau          = (T)(op->prm.dt == 0.0 ? 0.0 : 1.0 / op->prm.dt);
+        a.nu4           = T(4) * a.nu;
+        a.stau2         = a.stau * a.stau;
         a.td            = ((op->prm.flags & GLS_CONSIDER_TIME_DERIVATIVE) && op->prm.order > 0);
         a.cw            = (op->prm.flags & GLS_CELL_WISE_STAB) ? 1 : 0;
         a.have_prev     = op->have_prev ? 1 : 0;

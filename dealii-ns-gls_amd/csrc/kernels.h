@@ -233,15 +233,19 @@ nr_rsq(float x)
   const float y = __builtin_amdgcn_rsqf(x);
   return y * fmaf(-0.5f * x * y, y, 1.5f);
 }
+// nu4 = 4 nu and stau2 = stau^2 come precomputed (bitwise the products the
+// expression forms): as kernel arguments they stay scalar registers, where
+// the products formed in the kernel became loop-invariant VGPRs that the
+// 4-wave brick kernel had to spill
 template <typename T>
 __device__ __forceinline__ void
-delta_qwise_fast(T u2, T h, T nu, T stau, T &d1, T &d2)
+delta_qwise_fast(T u2, T h, T nu4, T stau2, T &d1, T &d2)
 {
   const T umag2 = T(1e-12) + u2;
   const T ih    = nr_rcp(h);
   const T ih2   = ih * ih;
-  const T fac   = T(4) * nu * ih2;
-  d1            = nr_rsq(stau * stau + T(4) * umag2 * ih2 + T(9) * fac * fac);
+  const T fac   = nu4 * ih2;
+  d1            = nr_rsq(stau2 + T(4) * umag2 * ih2 + T(9) * fac * fac);
   d2            = umag2 * nr_rsq(umag2) * h * T(0.5);
 }
 
