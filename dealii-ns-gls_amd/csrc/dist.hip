@@ -27,9 +27,18 @@
 //             received partials (fixed order per node, constrained
 //             components skipped: their identity value stands), then the
 //             ghost block of dst is zeroed.
-// The in-process group (gls_dist_create with nccl_id NULL) runs the same
-// phases with device copies in place of RCCL, so the whole orchestration
-// is testable on one GPU (tests/test_dist.py).
+// The exchanges go through a Transport: RCCL send/recv for the ranks of a
+// communicator, device copies for the members of an in-process group
+// (gls_dist_create with nccl_id NULL: tests on one GPU).  A member of an
+// in-process group driven from its own host thread (team calls with n = 1,
+// like an RCCL rank) runs THIS function, with its own compute stream and
+// communication stream: its import copies a peer's send buffer on d->cs once
+// the peer's ev_packed has passed, its export copies a peer's ghost rows once
+// the peer's ev_ghosts has passed, and two fences keep a member from
+// rewriting its send buffer or zeroing its ghost rows before the peers'
+// copies of them are done (host barriers order the event records with the
+// waits).  gls_dist_vmult_group runs the same phases for all members of a
+// group from one thread in lockstep on one stream.
 #include "../../include/gls_op.h"
 #include "common.h"
 #include "kernels.h"
@@ -38,8 +47,11 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -112,6 +124,25 @@ struct Peer
 };
 
 struct Group; // in-process group (tests)
+
+// the data movement of one rank's exchanges (dist_vmult, update_ghost_values,
+// compress(add)) and its all-reduces
+struct Transport
+{
+  virtual ~Transport() = default;
+  // the owners' rows into this rank's ghost block of src (update_ghost_values),
+  // on d->cs behind d->ev_packed
+  virtual void import_ghosts(glsDist_ *d, void *src) = 0;
+  // this rank's ghost partial sums of dst to their owners' export buffers
+  // (compress(add)), on d->cs behind d->ev_ghosts
+  virtual void export_ghosts(glsDist_ *d, const void *dst) = 0;
+  // on s, before this rank rewrites its send buffer / zeroes its ghost rows:
+  // the peers' reads of them are done
+  virtual void fence_send(glsDist_ *, hipStream_t) {}
+  virtual void fence_ghosts(glsDist_ *, hipStream_t) {}
+  // buf[0, count) <- the sum (max) over the ranks, on s
+  virtual void allreduce(glsDist_ *d, double *buf, int64_t count, bool max, hipStream_t s) = 0;
+};
 } // namespace
 
 struct glsDist_
@@ -120,6 +151,11 @@ struct glsDist_
   int               rank = 0, world = 1;
   ncclComm_t        comm = nullptr;
   Group            *group = nullptr;
+  std::unique_ptr<Transport> tx;
+  // in-process all-reduce: this member's staged operand (peers read it)
+  double           *red_stage = nullptr;
+  int64_t           red_cap   = 0;
+  hipEvent_t        ev_red_staged = nullptr, ev_red_done = nullptr;
   hipStream_t       cs   = nullptr;
   hipEvent_t        ev_packed = nullptr, ev_imported = nullptr;
   hipEvent_t        ev_ghosts = nullptr, ev_exported = nullptr;
@@ -139,6 +175,37 @@ namespace
 struct Group
 {
   std::vector<glsDist_ *> members; // by rank
+  // host barrier of the members driven from their own threads
+  std::mutex              mu;
+  std::condition_variable cv;
+  int                     arrived = 0;
+  uint64_t                gen     = 0;
+  bool                    broken  = false;
+
+  void
+  barrier(int world)
+  {
+    std::unique_lock<std::mutex> lk(mu);
+    if (broken)
+      throw std::runtime_error("gls_dist: in-process group broken by an earlier failure");
+    const uint64_t g = gen;
+    if (++arrived == world)
+      {
+        arrived = 0;
+        ++gen;
+        cv.notify_all();
+        return;
+      }
+    if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || broken; }) ||
+        broken)
+      {
+        broken = true;
+        cv.notify_all();
+        throw std::runtime_error("gls_dist: an in-process group member waited 120 s for its "
+                                 "peers (each member driven from its own thread makes the same "
+                                 "sequence of rank calls)");
+      }
+  }
 };
 
 size_t
@@ -293,6 +360,148 @@ local_export(glsDist_ *d, hipStream_t s)
     }
 }
 
+// every member's buf[i] <- the sum (or max) of the members' staged operands,
+// in rank order
+struct StageArgs
+{
+  const double *stage[16];
+};
+__global__ void
+k_stage_reduce(double *buf, StageArgs a, int n, int64_t count, int max)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count)
+    return;
+  double v = a.stage[0][i];
+  for (int r = 1; r < n; ++r)
+    v = max ? fmax(v, a.stage[r][i]) : v + a.stage[r][i];
+  buf[i] = v;
+}
+
+struct RcclTransport : Transport
+{
+  void
+  import_ghosts(glsDist_ *d, void *src) override
+  {
+    nccl_import(d, src);
+  }
+  void
+  export_ghosts(glsDist_ *d, const void *dst) override
+  {
+    nccl_export(d, dst, d->cs);
+  }
+  void
+  allreduce(glsDist_ *d, double *buf, int64_t count, bool max, hipStream_t s) override
+  {
+    if (d->world > 1 && count > 0)
+      NCCL_THROW(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, max ? ncclMax : ncclSum,
+                               d->comm, s));
+  }
+};
+
+// a member of an in-process group driven from its own host thread: the
+// peers' buffers read by device copies on this member's streams, gated by
+// the peers' events; the barriers make every member's record of an event
+// precede the peers' waits on it (a wait on a not-yet-recorded event would
+// not wait)
+struct GroupTransport : Transport
+{
+  static void
+  wait_peers(glsDist_ *d, hipStream_t s, hipEvent_t glsDist_::*ev)
+  {
+    for (const Peer &p : d->peers)
+      HIP_THROW(hipStreamWaitEvent(s, d->group->members.at(p.rank)->*ev, 0));
+  }
+  void
+  import_ghosts(glsDist_ *d, void *src) override
+  {
+    d->group->barrier(d->world); // every member's ev_packed recorded
+    const size_t rb = row_bytes(d->op);
+    for (const Peer &p : d->peers)
+      {
+        if (p.recv_cnt == 0)
+          continue;
+        const glsDist_ *q  = d->group->members.at(p.rank);
+        const Peer     *qp = find_peer(q, d->rank);
+        if (!qp || qp->send_cnt != p.recv_cnt)
+          throw std::runtime_error("gls_dist: inconsistent exchange lists");
+        HIP_THROW(hipStreamWaitEvent(d->cs, q->ev_packed, 0));
+        HIP_THROW(hipMemcpyAsync((char *)src + p.recv_begin * rb,
+                                 (const char *)q->d_send_buf + qp->send_off * rb,
+                                 (size_t)p.recv_cnt * rb, hipMemcpyDeviceToDevice, d->cs));
+      }
+  }
+  void
+  export_ghosts(glsDist_ *d, const void *dst) override
+  {
+    d->cur_dst = const_cast<void *>(dst);
+    d->group->barrier(d->world); // every member's ev_ghosts recorded, cur_dst set
+    const size_t rb = row_bytes(d->op);
+    for (const Peer &p : d->peers)
+      {
+        if (p.send_cnt == 0)
+          continue;
+        const glsDist_ *q  = d->group->members.at(p.rank);
+        const Peer     *qp = find_peer(q, d->rank);
+        if (!qp || qp->recv_cnt != p.send_cnt)
+          throw std::runtime_error("gls_dist: inconsistent exchange lists");
+        HIP_THROW(hipStreamWaitEvent(d->cs, q->ev_ghosts, 0));
+        HIP_THROW(hipMemcpyAsync((char *)d->d_xrecv_buf + p.send_off * rb,
+                                 (const char *)q->cur_dst + qp->recv_begin * rb,
+                                 (size_t)p.send_cnt * rb, hipMemcpyDeviceToDevice, d->cs));
+      }
+  }
+  void
+  fence_send(glsDist_ *d, hipStream_t s) override
+  {
+    d->group->barrier(d->world); // the peers' last imports from this send buffer recorded
+    wait_peers(d, s, &glsDist_::ev_imported);
+  }
+  void
+  fence_ghosts(glsDist_ *d, hipStream_t s) override
+  {
+    d->group->barrier(d->world); // the peers' exports from these ghost rows recorded
+    wait_peers(d, s, &glsDist_::ev_exported);
+  }
+  void
+  allreduce(glsDist_ *d, double *buf, int64_t count, bool max, hipStream_t s) override
+  {
+    Group *g = d->group;
+    g->barrier(d->world); // the last all-reduce's ev_red_done recorded everywhere
+    for (glsDist_ *q : g->members)
+      HIP_THROW(hipStreamWaitEvent(s, q->ev_red_done, 0));
+    if (d->red_cap < count)
+      {
+        HIP_THROW(hipStreamSynchronize(s));
+        if (d->red_stage)
+          HIP_THROW(hipFree(d->red_stage));
+        HIP_THROW(hipMalloc((void **)&d->red_stage, (size_t)count * sizeof(double)));
+        d->red_cap = count;
+      }
+    if (count > 0)
+      HIP_THROW(hipMemcpyAsync(d->red_stage, buf, (size_t)count * sizeof(double),
+                               hipMemcpyDeviceToDevice, s));
+    HIP_THROW(hipEventRecord(d->ev_red_staged, s));
+    g->barrier(d->world); // every member's operand staged (and its pointer set)
+    StageArgs a{};
+    const int n = (int)g->members.size();
+    if (n > 16)
+      throw std::runtime_error("gls_dist: in-process groups of at most 16 members");
+    for (int r = 0; r < n; ++r)
+      {
+        HIP_THROW(hipStreamWaitEvent(s, g->members[r]->ev_red_staged, 0));
+        a.stage[r] = g->members[r]->red_stage;
+      }
+    if (count > 0)
+      {
+        hipLaunchKernelGGL(k_stage_reduce, dim3((unsigned)((count + 255) / 256)), dim3(256), 0,
+                           s, buf, a, n, count, max ? 1 : 0);
+        HIP_THROW(hipGetLastError());
+      }
+    HIP_THROW(hipEventRecord(d->ev_red_done, s));
+  }
+};
+
 void
 zero_ghosts(glsDist_ *d, void *dst, hipStream_t s)
 {
@@ -409,11 +618,14 @@ gls_dist_create(glsOp op, const glsDistDesc *desc, glsDist *out)
   HIP_THROW(hipEventCreateWithFlags(&d->ev_imported, hipEventDisableTiming));
   HIP_THROW(hipEventCreateWithFlags(&d->ev_ghosts, hipEventDisableTiming));
   HIP_THROW(hipEventCreateWithFlags(&d->ev_exported, hipEventDisableTiming));
+  HIP_THROW(hipEventCreateWithFlags(&d->ev_red_staged, hipEventDisableTiming));
+  HIP_THROW(hipEventCreateWithFlags(&d->ev_red_done, hipEventDisableTiming));
   if (desc->nccl_id)
     {
       ncclUniqueId id;
       std::memcpy(&id, desc->nccl_id, sizeof(id));
       NCCL_THROW(ncclCommInitRank(&d->comm, d->world, id, d->rank));
+      d->tx = std::make_unique<RcclTransport>();
     }
   else
     {
@@ -426,6 +638,7 @@ gls_dist_create(glsOp op, const glsDistDesc *desc, glsDist *out)
         throw std::runtime_error("gls_dist_create: rank already in the group");
       g->members[d->rank] = d.get();
       d->group            = g;
+      d->tx               = std::make_unique<GroupTransport>();
     }
   *out = d.release();
   GLS_CATCH
@@ -457,9 +670,11 @@ gls_dist_destroy(glsDist d)
     (void)hipEventDestroy(d->ev_packed);
   if (d->ev_imported)
     (void)hipEventDestroy(d->ev_imported);
-  for (hipEvent_t e : {d->ev_ghosts, d->ev_exported})
+  for (hipEvent_t e : {d->ev_ghosts, d->ev_exported, d->ev_red_staged, d->ev_red_done})
     if (e)
       (void)hipEventDestroy(e);
+  if (d->red_stage)
+    (void)hipFree(d->red_stage);
   if (d->cs)
     (void)hipStreamDestroy(d->cs);
   delete d;
@@ -467,18 +682,17 @@ gls_dist_destroy(glsDist d)
 
 namespace
 {
-// the partitioned vmult of one RCCL rank; rx: the damped-Jacobi step (or the
+// the partitioned vmult of one rank (RCCL, or a threaded in-process member);
+// rx: the damped-Jacobi step (or the
 // residual) fused into the local bricks and reduce on the owned rows, the
 // peers' contributions entering through the unpack (k_unpack_add)
 void
 dist_vmult(glsDist d, void *dst, void *src, hipStream_t s, const gls::RelaxStep *rx)
 {
   check_vectors(d, dst, src);
-  if (!d->comm)
-    throw std::runtime_error("gls_dist_vmult: in-process group members run gls_dist_vmult_group");
   glsOp_       *op   = d->op;
   const int     mode = gls::op_vmult_mode(op);
-  if (d->peers.empty()) // one rank: nothing to exchange
+  if (d->comm && d->peers.empty()) // one RCCL rank: nothing to exchange
     {
       gls::brick_launch(op, mode, dst, src, 0, op->n_bricks, gls::BRICK_RUN | gls::BRICK_REDUCE,
                         s, rx);
@@ -487,10 +701,11 @@ dist_vmult(glsDist d, void *dst, void *src, hipStream_t s, const gls::RelaxStep 
     }
   const int64_t ni = op->n_interior_bricks, nh = ni / 2;
   // import (comm stream) || first interior half (s)
+  d->tx->fence_send(d, s);
   pack(d, src, s);
   HIP_THROW(hipEventRecord(d->ev_packed, s));
   HIP_THROW(hipStreamWaitEvent(d->cs, d->ev_packed, 0));
-  nccl_import(d, src);
+  d->tx->import_ghosts(d, src);
   HIP_THROW(hipEventRecord(d->ev_imported, d->cs));
   gls::brick_launch(op, mode, dst, src, 0, nh, gls::BRICK_RUN, s, rx);
   // boundary units and the ghost rows they complete
@@ -501,11 +716,12 @@ dist_vmult(glsDist d, void *dst, void *src, hipStream_t s, const gls::RelaxStep 
   // compress(add) of the ghost rows (comm stream) || second interior half
   // and the owned rows' reduction (s)
   HIP_THROW(hipStreamWaitEvent(d->cs, d->ev_ghosts, 0));
-  nccl_export(d, dst, d->cs);
+  d->tx->export_ghosts(d, dst);
   HIP_THROW(hipEventRecord(d->ev_exported, d->cs));
   gls::brick_launch(op, mode, dst, src, nh, ni, gls::BRICK_RUN | gls::BRICK_REDUCE_OWNED, s, rx);
   HIP_THROW(hipStreamWaitEvent(s, d->ev_exported, 0));
   unpack(d, dst, s, rx);
+  d->tx->fence_ghosts(d, s);
   zero_ghosts(d, dst, s);
 }
 
@@ -581,15 +797,14 @@ gls_dist_update_ghost_values(glsDist d, void *vec, void *stream)
   GLS_TRY
   if (!d || !vec)
     throw std::runtime_error("gls_dist_update_ghost_values: null argument");
-  if (!d->comm)
-    throw std::runtime_error("gls_dist_update_ghost_values: RCCL ranks only");
   hipStream_t s = (hipStream_t)stream;
-  if (!d->peers.empty())
+  if (!(d->comm && d->peers.empty()))
     {
+      d->tx->fence_send(d, s);
       pack(d, vec, s);
       HIP_THROW(hipEventRecord(d->ev_packed, s));
       HIP_THROW(hipStreamWaitEvent(d->cs, d->ev_packed, 0));
-      nccl_import(d, vec);
+      d->tx->import_ghosts(d, vec);
       HIP_THROW(hipEventRecord(d->ev_imported, d->cs));
       HIP_THROW(hipStreamWaitEvent(s, d->ev_imported, 0));
     }
@@ -602,13 +817,16 @@ gls_dist_compress_add(glsDist d, void *vec, void *stream)
   GLS_TRY
   if (!d || !vec)
     throw std::runtime_error("gls_dist_compress_add: null argument");
-  if (!d->comm)
-    throw std::runtime_error("gls_dist_compress_add: RCCL ranks only");
   hipStream_t s = (hipStream_t)stream;
-  if (!d->peers.empty())
+  if (!(d->comm && d->peers.empty()))
     {
-      nccl_export(d, vec, s);
+      HIP_THROW(hipEventRecord(d->ev_ghosts, s));
+      HIP_THROW(hipStreamWaitEvent(d->cs, d->ev_ghosts, 0));
+      d->tx->export_ghosts(d, vec);
+      HIP_THROW(hipEventRecord(d->ev_exported, d->cs));
+      HIP_THROW(hipStreamWaitEvent(s, d->ev_exported, 0));
       unpack(d, vec, s);
+      d->tx->fence_ghosts(d, s);
     }
   zero_ghosts(d, vec, s);
   GLS_CATCH
@@ -631,7 +849,7 @@ gls_dist_get_max_u(glsDist d, void *vec, double *u_max, void *stream)
   double     *buf = nullptr;
   HIP_THROW(hipMallocAsync((void **)&buf, sizeof(double), s));
   HIP_THROW(hipMemcpyAsync(buf, &local, sizeof(double), hipMemcpyHostToDevice, s));
-  NCCL_THROW(ncclAllReduce(buf, buf, 1, ncclDouble, ncclMax, d->comm, s));
+  d->tx->allreduce(d, buf, 1, true, s);
   HIP_THROW(hipMemcpyAsync(u_max, buf, sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_THROW(hipFreeAsync(buf, s));
   HIP_THROW(hipStreamSynchronize(s));
@@ -679,17 +897,26 @@ k_team_sum(SumArgs a, int n, int64_t count)
     a.buf[r][i] = s;
 }
 
+// a team of one: an RCCL rank, or a member of an in-process group driven
+// from its own host thread (both through the member's Transport)
+bool
+rank_mode(glsDist const *m, int n)
+{
+  return n == 1 && m[0] && (m[0]->comm || (m[0]->group && m[0]->world > 1));
+}
+
 void
 check_team(glsDist const *m, int n)
 {
   if (!m || n < 1 || n > TEAM_MAX)
     throw std::runtime_error("gls_dist team: bad member list");
-  if (n == 1 && m[0]->comm)
+  if (rank_mode(m, n))
     return;
   for (int r = 0; r < n; ++r)
     if (!m[r] || m[r]->comm || !m[r]->group || m[r]->rank != r || m[r]->world != n)
       throw std::runtime_error("gls_dist team: an in-process group is driven with all its "
-                               "members in rank order; RCCL ranks one at a time");
+                               "members in rank order (lockstep) or one member per host thread; "
+                               "RCCL ranks one at a time");
 }
 } // namespace
 
@@ -716,7 +943,7 @@ team_vmult(glsDist const *m, void *const *dst, void *const *src, int n, hipStrea
            const RelaxStep *rx)
 {
   check_team(m, n);
-  if (m[0]->comm)
+  if (rank_mode(m, n))
     dist_vmult(m[0], dst[0], src[0], s, rx);
   else
     dist_vmult_group(m, dst, src, n, s, rx);
@@ -726,7 +953,7 @@ void
 team_update_ghosts(glsDist const *m, void *const *v, int n, hipStream_t s)
 {
   check_team(m, n);
-  if (m[0]->comm)
+  if (rank_mode(m, n))
     {
       if (gls_dist_update_ghost_values(m[0], v[0], s))
         throw std::runtime_error(gls_last_error());
@@ -745,7 +972,7 @@ void
 team_compress_add(glsDist const *m, void *const *v, int n, hipStream_t s)
 {
   check_team(m, n);
-  if (m[0]->comm)
+  if (rank_mode(m, n))
     {
       if (gls_dist_compress_add(m[0], v[0], s))
         throw std::runtime_error(gls_last_error());
@@ -767,11 +994,9 @@ team_allreduce_sum(glsDist const *m, double *const *buf, int64_t count, int n, h
   check_team(m, n);
   if (count <= 0)
     return;
-  if (m[0]->comm)
+  if (rank_mode(m, n))
     {
-      if (m[0]->world > 1)
-        NCCL_THROW(ncclAllReduce(buf[0], buf[0], (size_t)count, ncclDouble, ncclSum, m[0]->comm,
-                                 s));
+      m[0]->tx->allreduce(m[0], buf[0], count, false, s);
       return;
     }
   SumArgs a{};

@@ -20,10 +20,11 @@
 // solved redundantly on every rank by a single-domain dense-LU multigrid of
 // the whole coarse level.
 //
-// All entry points take a TEAM: the handles of the ranks this process
-// drives in lockstep — one RCCL rank (n = 1), or every member of an
-// in-process group on one device (tests: the same data movement as device
-// copies), as gls_dist_vmult / gls_dist_vmult_group.
+// All entry points take a TEAM: the handles of the ranks this call drives —
+// one rank (n = 1: an RCCL rank, or one member of an in-process group driven
+// from its own host thread, the production schedule with device copies for
+// transport), or every member of an in-process group on one device in
+// lockstep (n = world), as gls_dist_vmult / gls_dist_vmult_group.
 #include "../../include/gls_op.h"
 #include "cgs.h"
 #include "common.h"

@@ -411,6 +411,41 @@ class DistributedOperator:
         return g
 
 
+def run_threaded(world, fn):
+    """fn(rank) on `world` host threads, each with its own torch stream as
+    the current stream (the members of an in-process group driven the way
+    RCCL ranks are: one rank call sequence per thread, libglsamd's
+    production schedule with device copies as transport; ctypes releases
+    the GIL inside the calls).  Returns the results in rank order; the first
+    exception of any thread is re-raised."""
+    import threading
+    import torch
+    torch.cuda.synchronize()
+    dev = torch.cuda.current_device()
+    out, err = [None] * world, [None] * world
+
+    def body(r):
+        try:
+            torch.cuda.set_device(dev)
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                out[r] = fn(r)
+            st.synchronize()
+        except BaseException as e:  # noqa: BLE001 (re-raised below)
+            err[r] = e
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for e in err:
+        if e is not None:
+            raise e
+    torch.cuda.synchronize()
+    return out
+
+
 class LocalGroup:
     """All ranks of a partition in ONE process (one device): the same phases
     with direct buffer delivery instead of point-to-point messages.  Used to
@@ -459,6 +494,15 @@ class LocalGroup:
             v[r.n_owned_dofs:].zero_()
         self.update_ghost_values(vs)
         return vs
+
+    def vmult_threaded(self, dsts, srcs, reps=1):
+        """gls_dist_vmult per member from its own thread and stream (the
+        production two-stream schedule of an RCCL rank), `reps` times"""
+        def one(r):
+            for _ in range(reps):
+                self.native[r].vmult(dsts[r], srcs[r])
+        run_threaded(len(self.ranks), one)
+        return dsts
 
     def vmult(self, dsts, srcs):
         if self.native is not None:
@@ -895,6 +939,19 @@ class NativeGroupMultigrid:
     def gmres(self, xs, bs, **kw):
         import glsamd
         return glsamd.dist_gmres_solve(self.fine_native, self.mg, xs, bs, **kw)
+
+    # the same team calls made by one thread per member with n = 1 (the rank
+    # code path of an RCCL rank; device copies as transport)
+    def vcycle_threaded(self, dsts, srcs, reps=1):
+        def one(r):
+            for _ in range(reps):
+                type(self.mg[r]).vcycle([self.mg[r]], [dsts[r]], [srcs[r]])
+        run_threaded(self.world, one)
+
+    def gmres_threaded(self, xs, bs, **kw):
+        import glsamd
+        return run_threaded(self.world, lambda r: glsamd.dist_gmres_solve(
+            [self.fine_native[r]], [self.mg[r]], [xs[r]], [bs[r]], **kw))
 
 
 class RedundantCoarseLU:

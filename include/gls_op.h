@@ -428,7 +428,10 @@ glsStatus gls_dist_create(glsOp op, const glsDistDesc *desc, glsDist *out);
 void      gls_dist_destroy(glsDist d);
 /* vmult of the partitioned operator on the rank-local [owned | ghost]
  * vectors: src's ghost block is overwritten by the import (as deal.II's
- * update_ghost_values), dst's ghost block is zero on return (compress) */
+ * update_ghost_values), dst's ghost block is zero on return (compress).
+ * An RCCL rank, or a member of an in-process group driven from its own host
+ * thread (every member then makes the same sequence of rank calls, each on
+ * its own stream; tests) */
 glsStatus gls_dist_vmult(glsDist d, void *dst, void *src, void *stream);
 /* the same for all members of an in-process group, phases in lockstep */
 glsStatus gls_dist_vmult_group(glsDist const *members, void *const *dsts,
@@ -436,11 +439,11 @@ glsStatus gls_dist_vmult_group(glsDist const *members, void *const *dsts,
 glsStatus gls_dist_interior_bricks(glsDist d, int64_t *n_interior,
                                    int64_t *n_total);
 /* update_ghost_values of a rank-local [owned | ghost] vector (the import
- * half of gls_dist_vmult), RCCL ranks only */
+ * half of gls_dist_vmult); rank calls as gls_dist_vmult */
 glsStatus gls_dist_update_ghost_values(glsDist d, void *vec, void *stream);
 /* compress(VectorOperation::add): the ghost block's partial sums added to
  * their owners (constrained components skipped), ghost block zeroed (the
- * export half of gls_dist_vmult), RCCL ranks only */
+ * export half of gls_dist_vmult); rank calls as gls_dist_vmult */
 glsStatus gls_dist_compress_add(glsDist d, void *vec, void *stream);
 /* get_max_u of the partitioned operator (operator_ns.cc:530-568): ghost
  * import, local max (gls_op_get_max_u), RCCL all-reduce max */

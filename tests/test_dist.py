@@ -218,3 +218,35 @@ def test_local_group_gpu_two_layer(world, monkeypatch):
     torch.cuda.synchronize()
     out = g.gather(dsts).cpu().numpy()
     assert rel_err(out, _oracle_ref(c)) < 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n_ref", CASES)
+@pytest.mark.parametrize("world", [2, 4])
+def test_threaded_group_vmult(name, n_ref, world):
+    """gls_dist_vmult itself — the production schedule of an RCCL rank: pack,
+    import on the communication stream || first interior half, boundary
+    bricks + ghost-row reduce after the import event, export on the
+    communication stream || second interior half + owned-row reduce, unpack
+    after the export event — with one host thread and one stream pair per
+    member of an in-process group (device copies gated by the peers' events
+    as transport, csrc/dist.hip GroupTransport), three times back to back
+    (the send-buffer and ghost-row fences between calls), against the
+    single-domain oracle (FP64 1e-12)."""
+    import torch
+    c = deck_case(name, n_ref)
+    g = glsdist.LocalGroup(c.mesh, c.cmask, world, engine="gpu", native=True)
+    g.setup(c.params, c.u_star, c.hist, c.weights)
+    srcs = g.scatter(c.src)
+    dsts = [r.new_vector() for r in g.ranks]
+    for r, sv in zip(g.ranks, srcs):  # ghosts must come from the import
+        sv[r.n_owned_dofs:].zero_()
+    for dv in dsts:
+        dv.fill_(7.0)
+    g.vmult_threaded(dsts, srcs, reps=3)
+    torch.cuda.synchronize()
+    out = g.gather(dsts).cpu().numpy()
+    assert rel_err(out, _oracle_ref(c)) < 1e-12
+    for r, sv, dv in zip(g.ranks, srcs, dsts):
+        assert torch.equal(sv.cpu(), torch.from_numpy(c.src)[r.global_dofs.cpu()])
+        assert not dv[r.n_owned_dofs:].any()  # compress zeroes the ghosts

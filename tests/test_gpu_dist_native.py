@@ -89,3 +89,71 @@ def test_native_group_gmres(world):
     print(f"world {world}: GMRES {res['n_iterations']} vs {it_ref} iterations, x rel diff {err:.2e}")
     assert res["converged"] and abs(res["n_iterations"] - it_ref) <= 1
     assert err < 1e-8
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("prec,coarse", [("f64", -1), ("f32", -1), ("f32", 10)])
+def test_threaded_group_vcycle(world, prec, coarse):
+    """The partitioned V-cycle through the rank code path (team calls with
+    n = 1, as an RCCL rank makes them): one host thread and one stream per
+    member, every level's vmult the production dist_vmult schedule with the
+    fused relaxation (csrc/dist.hip GroupTransport: device copies gated by
+    the peers' events), the redundant direct coarse solve's all-reduce
+    through the same transport; against the single-domain V-cycle (same
+    tolerances as the lockstep group)."""
+    import torch
+    import glsamd
+    import glsdist
+    meshes, cm, params, w, u, hist = _hierarchy(1)
+    ref, _ = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision=prec,
+                              coarse_n_iterations=coarse)
+    g = glsdist.NativeGroupMultigrid(meshes, cm, world, precision=prec,
+                                     coarse_n_iterations=coarse)
+    g.setup(params, u, hist, w)
+    b = gi.rnd(11, meshes[-1].n_dofs)
+    bs = g.scatter(b)
+    xs = [torch.zeros_like(x) for x in bs]
+    g.vcycle_threaded(xs, bs, reps=2)
+    src = torch.from_numpy(b).cuda()
+    dst = torch.zeros_like(src)
+    ref.vcycle(dst, src)
+    torch.cuda.synchronize()
+    err = rel_err(g.gather(xs).cpu().numpy(), dst.cpu().numpy())
+    print(f"threaded world {world} {prec} coarse {coarse}: partitioned vs single-domain "
+          f"V-cycle {err:.2e}")
+    assert err < (1e-10 if prec == "f64" else 1e-5)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_threaded_group_gmres(world):
+    """GMRES over the rank code path (n = 1 per thread): the CGS2 partials
+    all-reduced through the in-process transport; against the single-domain
+    solve (iterations +-1, solution 1e-8)."""
+    import torch
+    import glsamd
+    import glsdist
+    meshes, cm, params, w, u, hist = _hierarchy(1)
+    mg, _ = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f64",
+                             coarse_n_iterations=-1)
+    A = glsamd.NavierStokesOperator(meshes[-1], cm[-1], "f64")
+    A.set_parameters(**params)
+    A.set_linearization_point(u)
+    A.set_previous_solution(hist, w)
+    b = gi.rnd(12, meshes[-1].n_dofs)
+    src = torch.from_numpy(b).cuda()
+    x_ref = torch.zeros_like(src)
+    solver = glsamd.LinearSolverGMRES(A, mg, relative_tolerance=1e-8, absolute_tolerance=0.0)
+    solver.solve(x_ref, src)
+    it_ref = solver.last["n_iterations"]
+    g = glsdist.NativeGroupMultigrid(meshes, cm, world, precision="f64", coarse_n_iterations=-1)
+    g.setup(params, u, hist, w)
+    bs = g.scatter(b)
+    xs = [torch.zeros_like(x) for x in bs]
+    res = g.gmres_threaded(xs, bs, relative_tolerance=1e-8, absolute_tolerance=0.0)
+    torch.cuda.synchronize()
+    err = rel_err(g.gather(xs).cpu().numpy(), x_ref.cpu().numpy())
+    its = [r["n_iterations"] for r in res]
+    print(f"threaded world {world}: GMRES {its} vs {it_ref} iterations, x rel diff {err:.2e}")
+    assert all(r["converged"] for r in res) and len(set(its)) == 1
+    assert abs(its[0] - it_ref) <= 1
+    assert err < 1e-8
