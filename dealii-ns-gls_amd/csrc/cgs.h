@@ -204,6 +204,166 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// ---- delayed CGS2 (DCGS2; Bielich, Langou, Thomas, Swirydowicz, Yamazaki,
+// Boman, "Low-synch Gram-Schmidt with delayed reorthogonalization for
+// Krylov solvers", Parallel Computing 2022): the re-orthogonalisation of the
+// tentative basis vector u_j is delayed into the next Arnoldi step and merged
+// with the projection of w_j = A M^{-1} u_j, one reduction and two basis
+// passes per step instead of three passes (krylov.hip derives the Hessenberg
+// entries).  Dots of step j, stride DCGS_W per block:
+//   [0, 32): s = Q^T u_j   [32, 64): z = Q^T w_j   64: u_j.u_j   65: u_j.w_j
+// and, on the device after the update: 66 alpha_j  67 h_jj  68 |u_{j+1}|^2.
+constexpr int DCGS_W   = 2 * CGS_MAXJ + 2;
+constexpr int DCGS_D   = DCGS_W + 3; // dots + alpha, h_jj, nu
+constexpr int DCGS_PART = CGS_BLOCKS * DCGS_W;
+
+__device__ __forceinline__ bool
+dcgs_col_used(int c, int J)
+{
+  return c >= 2 * CGS_MAXJ || (c & (CGS_MAXJ - 1)) < J;
+}
+
+// pass 1: s = Q^T u, z = Q^T w (J columns of Q), u.u, u.w (w null: only
+// s and u.u, the end of a cycle)
+__global__ void __launch_bounds__(256)
+  k_dcgs_dots(const double *__restrict__ V, int J, const double *__restrict__ u,
+              const double *__restrict__ w, double *__restrict__ part, int64_t n, int64_t ld)
+{
+  double as[CGS_MAXJ], az[CGS_MAXJ], b = 0, g = 0;
+#pragma unroll
+  for (int c = 0; c < CGS_MAXJ; ++c)
+    as[c] = az[c] = 0;
+  const int64_t per = (n + CGS_BLOCKS - 1) / CGS_BLOCKS;
+  const int64_t r0 = blockIdx.x * per, r1 = r0 + per < n ? r0 + per : n;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x)
+    {
+      double v[CGS_MAXJ];
+#pragma unroll
+      for (int c = 0; c < CGS_MAXJ; ++c)
+        v[c] = c < J ? V[(size_t)c * ld + i] : 0.0;
+      const double ui = u[i], wi = w ? w[i] : 0.0;
+#pragma unroll
+      for (int c = 0; c < CGS_MAXJ; ++c)
+        {
+          as[c] += v[c] * ui;
+          az[c] += v[c] * wi;
+        }
+      b += ui * ui;
+      g += ui * wi;
+    }
+  __shared__ double red[4][DCGS_W];
+  const int         lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < DCGS_W; ++c)
+    if (dcgs_col_used(c, J))
+      {
+        double x = c < CGS_MAXJ ? as[c] : c < 2 * CGS_MAXJ ? az[c - CGS_MAXJ] : c == 2 * CGS_MAXJ ? b : g;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+          x += __shfl_down(x, off);
+        if (lane == 0)
+          red[wv][c] = x;
+      }
+  __syncthreads();
+  for (int c = threadIdx.x; c < DCGS_W; c += blockDim.x)
+    if (dcgs_col_used(c, J))
+      part[(size_t)blockIdx.x * DCGS_W + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+}
+
+// d[c] = sum over the blocks of part[b][c] (stride `stride`) in a fixed
+// order, one workgroup per column c = blockIdx.x (unused DCGS columns: 0)
+// (J < 0: every column used.)  host: a one-column launch (the norm of the
+// new tentative vector, out at d[out]) also stores d[0, DCGS_D) into mapped
+// pinned host memory, the step's record for the host
+__global__ void __launch_bounds__(256)
+  k_dcgs_finish(const double *__restrict__ part, double *__restrict__ d, int J, int out = -1,
+                double *__restrict__ host = nullptr)
+{
+  static_assert(CGS_BLOCKS == 512, "two partials per thread");
+  __shared__ double red[4];
+  const int c = blockIdx.x, t = threadIdx.x, o = out >= 0 ? out : c;
+  if (J >= 0 && !dcgs_col_used(c, J))
+    {
+      if (t == 0)
+        d[o] = 0;
+      return;
+    }
+  double s = part[(size_t)t * DCGS_W + c] + part[(size_t)(t + 256) * DCGS_W + c];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+    s += __shfl_down(s, off);
+  if ((t & 63) == 0)
+    red[t >> 6] = s;
+  __syncthreads();
+  const double v = (red[0] + red[1]) + (red[2] + red[3]);
+  if (t == 0)
+    d[o] = v;
+  if (host)
+    for (int i = t; i < DCGS_D; i += blockDim.x)
+      host[i] = i == o ? v : d[i];
+}
+
+// pass 2: q_j = (u_j - Q s) / alpha_j, alpha_j = sqrt(u_j.u_j - |s|^2)
+// (Pythagoras), written over u_j; the next tentative vector
+// u_{j+1} = (w_j - Q z - q_j h_jj) / alpha_j with h_jj = (u_j.w_j - s.z) /
+// alpha_j, and the partials of |u_{j+1}|^2.  Block 0 stores alpha_j, h_jj
+// (d[66], d[67]).  J = 0: q_0 = u_0 / |u_0|.
+__global__ void __launch_bounds__(256)
+  k_dcgs_update(const double *__restrict__ V, int J, double *__restrict__ d, double *q,
+                const double *__restrict__ w, double *__restrict__ un,
+                double *__restrict__ part, int64_t n, int64_t ld)
+{
+  double sc[CGS_MAXJ], zc[CGS_MAXJ], s2 = 0, sz = 0;
+#pragma unroll
+  for (int c = 0; c < CGS_MAXJ; ++c)
+    {
+      sc[c] = c < J ? d[c] : 0.0;
+      zc[c] = c < J ? d[CGS_MAXJ + c] : 0.0;
+      s2 += sc[c] * sc[c];
+      sz += sc[c] * zc[c];
+    }
+  const double a2    = d[2 * CGS_MAXJ] - s2;
+  const double alpha = sqrt(a2 > 0 ? a2 : 0.0);
+  const double ia    = alpha > 0 ? 1.0 / alpha : 0.0;
+  const double hjj   = (d[2 * CGS_MAXJ + 1] - sz) * ia;
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    {
+      d[DCGS_W]     = alpha;
+      d[DCGS_W + 1] = hjj;
+    }
+  double        nu  = 0;
+  const int64_t per = (n + CGS_BLOCKS - 1) / CGS_BLOCKS;
+  const int64_t r0 = blockIdx.x * per, r1 = r0 + per < n ? r0 + per : n;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x)
+    {
+      double vr[CGS_MAXJ];
+#pragma unroll
+      for (int c = 0; c < CGS_MAXJ; ++c)
+        vr[c] = c < J ? V[(size_t)c * ld + i] : 0.0;
+      double ts = 0, tz = 0;
+#pragma unroll
+      for (int c = 0; c < CGS_MAXJ; ++c)
+        {
+          ts += vr[c] * sc[c];
+          tz += vr[c] * zc[c];
+        }
+      const double qi = (q[i] - ts) * ia;
+      const double ui = (w[i] - tz - qi * hjj) * ia;
+      q[i]            = qi;
+      un[i]           = ui;
+      nu += ui * ui;
+    }
+  __shared__ double red[4];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+    nu += __shfl_down(nu, off);
+  if ((threadIdx.x & 63) == 0)
+    red[threadIdx.x >> 6] = nu;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    part[(size_t)blockIdx.x * DCGS_W] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 // v = w / sqrt(|w|^2) with the squared norm read on the device (the
 // partitioned GMRES all-reduces |w|^2 before the root)
 __global__ void

@@ -1059,7 +1059,9 @@ gls_dist_gmres_solve(glsDist const *A, glsDistMG const *mg, int n, const glsGMRE
   HIP_THROW(hipHostMalloc((void **)&pin.p, 2 * HC * sizeof(double)));
   for (int i = 0; i < 2; ++i)
     HIP_THROW(hipEventCreateWithFlags(&pin.e[i], hipEventDisableTiming));
-  static const bool force_rocblas = getenv("GLS_GMRES_ROCBLAS") && getenv("GLS_GMRES_ROCBLAS")[0] == '1';
+  // GLS_GMRES_ORTHO=rocblas: the rocBLAS GEMV passes at every length (krylov.hip)
+  const char *ortho         = getenv("GLS_GMRES_ORTHO");
+  const bool  force_rocblas = ortho && std::string(ortho) == "rocblas";
   auto grid = [](int64_t k) { return dim3((unsigned)((k + 255) / 256)); };
   // Arnoldi step j, enqueued only
   auto arnoldi = [&](int j) {

@@ -22,6 +22,7 @@
 
 #include <rocblas/rocblas.h>
 
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 #include <string>
@@ -81,13 +82,6 @@ grid1(int64_t n)
   return dim3((unsigned)((n + 255) / 256));
 }
 
-bool
-getenv_flag(const char *name)
-{
-  const char *e = getenv(name);
-  return e && e[0] == '1';
-}
-
 void
 check(glsStatus st, const char *what)
 {
@@ -130,8 +124,9 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   // demand (a hipMalloc/hipFree of the basis per solve synchronises the
   // device and costs more than the solve's setup)
   rocblas_handle h  = blas_handle(op->device, s);
-  // dh: the two CGS passes' coefficients and |w| (HC values, one D2H copy)
-  const int      HC = 2 * (m + 1) + 1;
+  // dh: the two CGS passes' coefficients and |w| (HC values, one D2H copy),
+  // or a DCGS2 step's record (DCGS_D values)
+  const int      HC = std::max(2 * (m + 1) + 1, DCGS_D);
   // the preconditioned directions z_j = M^{-1} v_j are kept (Z, m columns):
   // the cycle's update is then x += Z y, the same iterate as deal.II's
   // x += M^{-1} (V y) (SolverGMRES, right preconditioning: solver_l.cc:62)
@@ -154,7 +149,7 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   }
   const size_t nz = zkeep ? (size_t)m * n : 0;
   // Z starts 256-byte aligned (the operator's 16-byte pack loads read it)
-  const size_t z_off = ((size_t)(m + 3) * n + HC + (size_t)CGS_BLOCKS * CGS_MAXJ + 31) / 32 * 32;
+  const size_t z_off = ((size_t)(m + 3) * n + HC + (size_t)DCGS_PART + 31) / 32 * 32;
   const size_t ws    = (z_off + nz) * sizeof(double);
   if (op->gmres_ws_bytes < ws)
     {
@@ -239,11 +234,16 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   hipEvent_t *ev = evs.e;
   for (int i = 0; i < 2; ++i)
     HIP_THROW(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
-  // GLS_GMRES_ROCBLAS=1: the rocBLAS GEMV orthogonalisation at every length
-  static const bool force_rocblas = getenv_flag("GLS_GMRES_ROCBLAS");
-  // GLS_GMRES_CGS3=1: the three explicit CGS2 passes (the second update and
-  // the norm as their own pass) instead of the Pythagorean normalisation
-  static const bool force_three_pass = getenv_flag("GLS_GMRES_CGS3");
+  // orthogonalisation: delayed CGS2 (one reduction, two basis passes per
+  // step; below) for a linear preconditioner within the fused lengths, else
+  // CGS2 (three fused passes, the second update folded into a Pythagorean
+  // normalisation), rocBLAS GEMVs beyond 31 columns.  GLS_GMRES_ORTHO =
+  // cgs2 / cgs3 (the explicit second update and norm) / rocblas selects a
+  // reference form (tests)
+  const std::string ortho        = getenv("GLS_GMRES_ORTHO") ? getenv("GLS_GMRES_ORTHO") : "";
+  const bool        force_rocblas    = ortho == "rocblas";
+  const bool        force_three_pass = ortho == "cgs3";
+  const bool        dcgs = ortho.empty() && (!mg || gls::mg_is_linear(mg)) && m + 1 < CGS_MAXJ;
   auto              arnoldi       = [&](int j) {
     precondition(zcol(j), vcol(j));
     gls::op_vmult_device(op, w.d(), zcol(j), s);
@@ -310,6 +310,162 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
                          (const double *)w.d(), (const double *)hn, n);
     HIP_THROW(hipGetLastError());
   };
+  // ---- delayed CGS2 (cgs.h).  Step j holds the TENTATIVE vector u_j
+  // (orthogonalised once) in column j of V: w_j = A M^{-1} u_j; one pass of
+  // dots s = Q^T u_j, z = Q^T w_j, u_j.u_j, u_j.w_j (Q: the final columns
+  // 0..j-1); one update pass q_j = (u_j - Q s) / alpha_j into column j and
+  // the next tentative u_{j+1} = (w_j - Q z - q_j h_jj) / alpha_j into column
+  // j+1, with |u_{j+1}|^2.  With the Arnoldi relation of the earlier columns
+  // (A M^{-1} Q_j = Q_{j+1} H_j, M linear), A M^{-1} q_j = ([z; h_jj] -
+  // H_j s_j) / alpha_j (the Q_{j+1} part) + u_{j+1}, and u_{j+1} = Q_{j+1}
+  // s_{j+1} + alpha_{j+1} q_{j+1}: column j of H is final once step j+1's
+  // s_{j+1}, alpha_{j+1} are known; until then the convergence estimate uses
+  // |u_{j+1}| for H_{j+1,j} and leaves out s_{j+1} (O(eps) terms).  The kept
+  // directions are M^{-1} u_j; with U = Q R (R_ij = s_j[i], R_jj = alpha_j),
+  // M^{-1} Q y = Z (R^{-1} y).
+  auto arnoldi_d = [&](int j) {
+    precondition(zcol(j), vcol(j));
+    gls::op_vmult_device(op, w.d(), zcol(j), s);
+    double *dd = dh.d();
+    hipLaunchKernelGGL(k_dcgs_dots, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(), j,
+                       (const double *)vcol(j), (const double *)w.d(), cpart.d(), n, n);
+    hipLaunchKernelGGL(k_dcgs_finish, dim3(DCGS_W), dim3(256), 0, s, (const double *)cpart.d(),
+                       dd, j, -1, (double *)nullptr);
+    hipLaunchKernelGGL(k_dcgs_update, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(), j,
+                       dd, vcol(j), (const double *)w.d(), vcol(j + 1), cpart.d(), n, n);
+    hipLaunchKernelGGL(k_dcgs_finish, dim3(1), dim3(256), 0, s, (const double *)cpart.d(), dd, -1,
+                       DCGS_W + 2, host_dev + (j % 2) * HC);
+    HIP_THROW(hipGetLastError());
+    HIP_THROW(hipEventRecord(ev[j % 2], s));
+  };
+  // raw (unrotated) Hessenberg, column major with m+1 rows, and R
+  std::vector<double> Hr((size_t)(m + 1) * m), Rm((size_t)m * m);
+  auto                HR = [&](int i, int c) -> double & { return Hr[(size_t)c * (m + 1) + i]; };
+  auto                RR = [&](int i, int c) -> double & { return Rm[(size_t)c * m + i]; };
+  // step j's record: column j-1 finished, column j estimated, R column j
+  auto absorb = [&](int j, const double *rc) {
+    const double *sj = rc, *zj = rc + CGS_MAXJ;
+    const double  alpha = rc[DCGS_W], hjj = rc[DCGS_W + 1], nu = rc[DCGS_W + 2];
+    if (j >= 1)
+      {
+        for (int i = 0; i < j; ++i)
+          HR(i, j - 1) += sj[i];
+        HR(j, j - 1) = alpha;
+      }
+    for (int i = 0; i <= j; ++i)
+      {
+        double t = i < j ? zj[i] : hjj;
+        for (int k = 0; k < j; ++k)
+          t -= HR(i, k) * sj[k];
+        HR(i, j) = alpha > 0 ? t / alpha : 0.0;
+      }
+    HR(j + 1, j) = std::sqrt(nu > 0 ? nu : 0.0);
+    for (int i = 0; i < j; ++i)
+      RR(i, j) = sj[i];
+    RR(j, j) = alpha;
+  };
+  // least squares min |g0 e_0 - H y| over the first jd columns (Givens QR of
+  // a copy of the raw Hessenberg): the residual estimate, and y if asked
+  std::vector<double> Hw((size_t)(m + 1) * m);
+  auto lsq = [&](int jd, double g0, double *yout) {
+    Hw = Hr;
+    auto HW = [&](int i, int c) -> double & { return Hw[(size_t)c * (m + 1) + i]; };
+    std::fill(g.begin(), g.end(), 0.0);
+    g[0] = g0;
+    for (int j = 0; j < jd; ++j)
+      {
+        for (int i = 0; i < j; ++i)
+          {
+            const double t = cs[i] * HW(i, j) + sn[i] * HW(i + 1, j);
+            HW(i + 1, j)   = -sn[i] * HW(i, j) + cs[i] * HW(i + 1, j);
+            HW(i, j)       = t;
+          }
+        const double rr = std::hypot(HW(j, j), HW(j + 1, j));
+        cs[j]           = rr > 0 ? HW(j, j) / rr : 1.0;
+        sn[j]           = rr > 0 ? HW(j + 1, j) / rr : 0.0;
+        HW(j, j)        = rr;
+        HW(j + 1, j)    = 0;
+        g[j + 1]        = -sn[j] * g[j];
+        g[j]            = cs[j] * g[j];
+      }
+    if (yout)
+      for (int i = jd - 1; i >= 0; --i)
+        {
+          double t = g[i];
+          for (int c = i + 1; c < jd; ++c)
+            t -= HW(i, c) * yout[c];
+          yout[i] = t / HW(i, i);
+        }
+    return std::fabs(g[jd]);
+  };
+  // one DCGS2 cycle from the tentative u_0 = r / beta in column 0: the
+  // update coefficients (R^{-1} y with kept directions, else y) into y;
+  // returns the number of columns
+  auto cycle_dcgs = [&](double beta) {
+    std::fill(Hr.begin(), Hr.end(), 0.0);
+    std::fill(Rm.begin(), Rm.end(), 0.0);
+    double g0      = beta;
+    int    jd      = 0;
+    bool   ahead   = false; // step jd enqueued (its record finishes column jd-1)
+    arnoldi_d(0);
+    for (int j = 0; j < m && it < desc->max_iterations; ++j)
+      {
+        ahead = j + 1 < m && it + 1 < desc->max_iterations;
+        if (ahead)
+          arnoldi_d(j + 1);
+        HIP_THROW(hipEventSynchronize(ev[j % 2]));
+        const double *rc = op->gmres_host + (j % 2) * HC;
+        absorb(j, rc);
+        if (j == 0)
+          g0 = beta * rc[DCGS_W]; // r = beta u_0 = beta alpha_0 q_0
+        ++it;
+        ++jd;
+        res = lsq(jd, g0, nullptr);
+        if (res <= tol || HR(j + 1, j) == 0)
+          break;
+      }
+    // column jd-1's re-orthogonalisation terms: the record of the step run
+    // ahead, or the dots of u_jd alone
+    if (ahead)
+      {
+        HIP_THROW(hipEventSynchronize(ev[jd % 2]));
+        const double *rc = op->gmres_host + (jd % 2) * HC;
+        for (int i = 0; i < jd; ++i)
+          HR(i, jd - 1) += rc[i];
+        HR(jd, jd - 1) = rc[DCGS_W];
+      }
+    else
+      {
+        double *dd = dh.d();
+        hipLaunchKernelGGL(k_dcgs_dots, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(),
+                           jd, (const double *)vcol(jd), (const double *)nullptr, cpart.d(), n, n);
+        hipLaunchKernelGGL(k_dcgs_finish, dim3(DCGS_W), dim3(256), 0, s,
+                           (const double *)cpart.d(), dd, jd, -1, (double *)nullptr);
+        HIP_THROW(hipGetLastError());
+        std::vector<double> rc(DCGS_W);
+        HIP_THROW(hipMemcpyAsync(rc.data(), dd, DCGS_W * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIP_THROW(hipStreamSynchronize(s));
+        double s2 = 0;
+        for (int i = 0; i < jd; ++i)
+          {
+            HR(i, jd - 1) += rc[i];
+            s2 += rc[i] * rc[i];
+          }
+        const double a2 = rc[2 * CGS_MAXJ] - s2;
+        HR(jd, jd - 1)  = std::sqrt(a2 > 0 ? a2 : 0.0);
+      }
+    res = lsq(jd, g0, y.data());
+    if (zkeep) // t = R^{-1} y
+      for (int i = jd - 1; i >= 0; --i)
+        {
+          double t = y[i];
+          for (int c = i + 1; c < jd; ++c)
+            t -= RR(i, c) * y[c];
+          y[i] = t / RR(i, i);
+        }
+    return jd;
+  };
+
   // r (in column 0 of V) = b - A x
   HIP_THROW(hipMemcpyAsync(vcol(0), b, n * sizeof(double), hipMemcpyDeviceToDevice, s));
   while (!conv && it < desc->max_iterations)
@@ -322,6 +478,10 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
       std::fill(g.begin(), g.end(), 0.0);
       g[0]   = beta;
       int jd = 0; // columns of this cycle
+      if (dcgs)
+        jd = cycle_dcgs(beta);
+      else
+        {
       // software pipeline: step j + 1 is enqueued before the host waits for
       // step j's Hessenberg column, so the device never idles through the
       // host round trip; when step j converges, the enqueued step j + 1 runs
@@ -368,6 +528,7 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
           for (int c = i + 1; c < jd; ++c)
             t -= H[(size_t)c * (m + 1) + i] * y[c];
           y[i] = t / H[(size_t)i * (m + 1) + i];
+        }
         }
       HIP_THROW(hipMemcpyAsync(dh.d(), y.data(), jd * sizeof(double), hipMemcpyHostToDevice, s));
       if (jd > 0)

@@ -182,7 +182,8 @@ def test_gmres_error_convention():
 def test_gmres_pythagorean_vs_three_pass_cgs2():
     """The default orthogonalisation (CGS2 with the second update folded into
     the normalisation, |w - V h|^2 = |w|^2 - |h|^2) against the three explicit
-    passes (GLS_GMRES_CGS3=1, read once per process: a child process) on the
+    passes (GLS_GMRES_ORTHO=cgs3) and the default delayed CGS2 (DCGS2: one
+    reduction, two basis passes per step) against CGS2 (GLS_GMRES_ORTHO=cgs2) on the
     Re3900 r1 Newton system with the FP64-level V-cycle: the same iteration
     count and solutions within the solver tolerance's class."""
     import os
@@ -220,17 +221,25 @@ print(s.last["n_iterations"])
     env["PYTHONPATH"] = os.pathsep.join([here] + sys.path)
     res = {}
     with tempfile.TemporaryDirectory() as td:
-        for tag, extra in (("pyth", {}), ("cgs3", {"GLS_GMRES_CGS3": "1"})):
+        for tag, extra in (("pyth", {"GLS_GMRES_ORTHO": "cgs2"}),
+                           ("cgs3", {"GLS_GMRES_ORTHO": "cgs3"}), ("dcgs2", {})):
             f = os.path.join(td, tag + ".npy")
             out = subprocess.run([sys.executable, "-c", code, f], env=dict(env, **extra),
                                  capture_output=True, text=True, timeout=300)
             assert out.returncode == 0, out.stderr[-2000:]
             res[tag] = (int(out.stdout.strip().splitlines()[-1]), np.load(f))
-    (ip, xp), (i3, x3) = res["pyth"], res["cgs3"]
+    (ip, xp), (i3, x3), (idc, xd) = res["pyth"], res["cgs3"], res["dcgs2"]
     diff = np.linalg.norm(xp - x3) / np.linalg.norm(x3)
-    print(f"GMRES iterations Pythagorean {ip} / three-pass {i3}, solution rel diff {diff:.2e}")
+    diff_d = np.linalg.norm(xd - xp) / np.linalg.norm(xp)
+    print(f"GMRES iterations Pythagorean {ip} / three-pass {i3} / DCGS2 {idc}, solution rel "
+          f"diff {diff:.2e} / DCGS2 vs CGS2 {diff_d:.2e}")
     assert abs(ip - i3) <= 1
     assert diff < 1e-7
+    # the same iteration count +-1 and the solution within
+    # 1e-12 of CGS2's (both meet the 1e-10 tolerance; the FP64-level V-cycle
+    # makes the preconditioner linear to round-off)
+    assert abs(idc - ip) <= 1
+    assert diff_d < 1e-12, diff_d
 
 
 def test_gmres_kept_directions_nonlinear_preconditioner(monkeypatch):
