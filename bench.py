@@ -246,9 +246,8 @@ def mg_companions(d, params, weights, n_ref, reps=20):
     (inverse diagonals + power-iteration relaxation factors, gls_mg_setup),
     one V-cycle (5 damped-Jacobi pre/post steps; coarse solve = 10
     relaxation sweeps, the substitute for the deck's Trilinos direct solver,
-    DESIGN.md A16) launched kernel by kernel and replayed from a captured
-    hipGraph, and one full right-preconditioned GMRES iteration (V-cycle + FP64
-    vmult + CGS2); event-timed medians."""
+    DESIGN.md A16), and one full right-preconditioned GMRES iteration (V-cycle
+    + FP64 vmult + delayed CGS2); event-timed medians."""
     import torch
     import glsamd
     meshes = [d.mesh(r) for r in range(n_ref + 1)]
@@ -304,9 +303,6 @@ def mg_companions(d, params, weights, n_ref, reps=20):
         return float(np.median(times)) * 1e3
 
     vc = vcycles()
-    os.environ["GLS_MG_GRAPH"] = "1"
-    vc_graph = vcycles()
-    os.environ.pop("GLS_MG_GRAPH")
     # the deck's own coarse solver ("gmg coarse grid solver": "direct",
     # multigrid.cc:448-455): the assembled r0 operator's free-dof block
     # LU-factorised and inverted once in the setup (rocSOLVER getrf/getri),
@@ -335,24 +331,6 @@ def mg_companions(d, params, weights, n_ref, reps=20):
             torch.cuda.synchronize()
             t.append(e0.elapsed_time(e1))
         lu["ms"] = float(np.median(t))
-        # the same cycle replayed from its captured hipGraph (GLS_MG_GRAPH=1;
-        # correctness: tests/test_gpu_mg.py::test_vcycle_graph_replay)
-        os.environ["GLS_MG_GRAPH"] = "1"
-        try:
-            for _ in range(3):
-                mg_lu.vcycle(x, b)
-            torch.cuda.synchronize()
-            t = []
-            for _ in range(reps):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                mg_lu.vcycle(x, b)
-                e1.record()
-                torch.cuda.synchronize()
-                t.append(e0.elapsed_time(e1))
-            lu["ms_hipgraph_replay"] = float(np.median(t))
-        finally:
-            os.environ.pop("GLS_MG_GRAPH")
         lu["gmres_iteration_ms"] = gmres_iteration(mg_lu)
         lu["coarse_dofs"] = meshes[0].n_dofs
         lu["coarse_free_dofs"] = int(sum(((c >> k) & 1 == 0).sum() for c in [cm[0]]
@@ -399,14 +377,14 @@ def mg_companions(d, params, weights, n_ref, reps=20):
                                        "note": "gls_mg_setup: inverse diagonals (direct "
                                                "element-diagonal kernel) + power iteration "
                                                "(20 steps, device reductions), wall"},
-            f"r{n_ref}_vcycle_f32_coarse_relax10": {"ms": vc, "ms_hipgraph_replay": vc_graph,
-                                                    "levels": n_ref + 1,
+            f"r{n_ref}_vcycle_f32_coarse_relax10": {"ms": vc, "levels": n_ref + 1,
                                                     "finest_dofs": meshes[-1].n_dofs,
                                                     "vcycles_per_s": 1e3 / vc},
             f"r{n_ref}_vcycle_f32_coarse_direct_lu": lu,
             f"r{n_ref}_gmres_iteration": {"ms": git,
                                           "note": "V-cycle (coarse: 10 relaxation sweeps) + "
-                                                  "FP64 vmult + CGS2 + host Hessenberg step, "
+                                                  "FP64 vmult + delayed CGS2 + host Hessenberg "
+                                                  "step, "
                                                   "wall clock; with the deck's direct coarse "
                                                   "solve: r{}_vcycle_f32_coarse_direct_lu."
                                                   "gmres_iteration_ms".format(n_ref)}}

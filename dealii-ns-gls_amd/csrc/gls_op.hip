@@ -221,8 +221,6 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
   }
   if (two_layer)
     n_split = 0; // (one dispatch generation: no tail to split)
-  if (const char *e = getenv("GLS_BRICK_SPLIT"))
-    n_split = std::atoll(e);
   if (by % 2 != 0)
     n_split = 0;
   n_split = std::max<int64_t>(0, std::min(n_split, nb_full));
@@ -251,10 +249,9 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
   // brick start(i % 8) + i / 8 of the segment (a bijection for any length).
   // Applied to the interior and the boundary segment separately (they are
   // separate launches in the partitioned vmult); the split tail keeps its
-  // LPT order.  GLS_XCD_REMAP=0 disables it.
+  // LPT order.
   {
-    const char *e     = getenv("GLS_XCD_REMAP");
-    const bool  remap = !e || std::atoi(e) != 0;
+    const bool remap = true;
     auto        xcd   = [&](int64_t b0, int64_t b1) {
       const int64_t G = b1 - b0, q = G / 8, r = G % 8;
       if (G < 16)
@@ -272,9 +269,7 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
     // XCDs' runs (Re3900 r2: 80 and 48 of 128), whose last bricks then end
     // the launch.  Each run takes a contiguous share of the curved bricks and
     // of the Cartesian ones in mesh order (lattice-plane sharing kept).
-    // GLS_CURVED_BALANCE=0 disables it.
-    const char *cb      = getenv("GLS_CURVED_BALANCE");
-    const bool  balance = remap && !(cb && cb[0] == '0') && cell_curved;
+    const bool balance = cell_curved != nullptr;
     auto        spread  = [&](int64_t b0, int64_t b1) {
       const int64_t G = b1 - b0, q = G / 8, r = G % 8;
       if (G < 16)
@@ -2197,14 +2192,10 @@ op_inverse_diagonal_device(glsOp op, void *diag, hipStream_t s)
 {
   if (!op->have_lin)
     throw std::runtime_error("compute_inverse_diagonal before set_linearization_point");
-  ApplyFn   af;
-  ProduceFn pf;
-  select(op, af, pf);
-  // GLS_DIAG_UNIT=1: the unit-vector cell applies (k_apply<DIAG>, what
-  // MatrixFreeTools::compute_diagonal does) instead of the direct evaluation
-  const char *e = getenv("GLS_DIAG_UNIT");
-  if (!(e && std::atoi(e) != 0))
-    {
+  // the element diagonals evaluated directly (k_diag) instead of
+  // MatrixFreeTools::compute_diagonal's unit-vector cell applies (1.68 ms of
+  // k_apply<DIAG> per level, round 1)
+  {
       // direct element diagonals, assembled in FP64 (in place for FP64
       // operators), inverted into the operator's precision
       double *d64 = (double *)diag;
@@ -2226,18 +2217,7 @@ op_inverse_diagonal_device(glsOp op, void *diag, hipStream_t s)
           HIP_THROW(hipFreeAsync(d64, s));
         }
       HIP_THROW(hipGetLastError());
-      return;
     }
-  HIP_THROW(hipMemsetAsync(diag, 0, (size_t)op->n_dofs * op->tsize(), s));
-  af(op, vmult_mode(op), true, diag, diag, 0, op->n_cells, s);
-  faces_diagonal(op, diag, false, s);
-  if (op->prec == GLS_F64)
-    hipLaunchKernelGGL(k_invert_diag<double>, grid1d(op->n_dofs), dim3(256), 0, s,
-                       (double *)diag, op->d_cbits, op->n_owned_dofs, op->n_dofs);
-  else
-    hipLaunchKernelGGL(k_invert_diag<float>, grid1d(op->n_dofs), dim3(256), 0, s, (float *)diag,
-                       op->d_cbits, op->n_owned_dofs, op->n_dofs);
-  HIP_THROW(hipGetLastError());
 }
 
 void

@@ -441,10 +441,7 @@ k_residual(T *__restrict__ t, const T *__restrict__ b, int64_t n)
     t[i] = b[i] - t[i];
 }
 
-// zero fill / copy of the V-cycle's own buffers: kernels by default;
-// GLS_MG_MEMNODES=1 issues hipMemsetAsync / hipMemcpyAsync instead (in a
-// captured V-cycle: memset / memcpy graph nodes).  Both are checked bit for
-// bit against the eager V-cycle (tests/test_gpu_mg.py::test_vcycle_graph_*).
+// zero fill / copy of the V-cycle's own buffers (kernels)
 __global__ void
 k_zero(uint32_t *__restrict__ x, int64_t n_words)
 {
@@ -588,31 +585,18 @@ g1(int64_t n)
   return dim3((unsigned)((n + 255) / 256));
 }
 
-bool
-mem_nodes()
-{
-  const char *e = getenv("GLS_MG_MEMNODES");
-  return e && std::atoi(e) != 0;
-}
-
 void
 zero_words(void *x, int64_t n_words, hipStream_t s)
 {
-  if (mem_nodes())
-    HIP_THROW(hipMemsetAsync(x, 0, (size_t)n_words * 4, s));
-  else
-    hipLaunchKernelGGL(k_zero, g1(n_words), dim3(256), 0, s, (uint32_t *)x, n_words);
+  hipLaunchKernelGGL(k_zero, g1(n_words), dim3(256), 0, s, (uint32_t *)x, n_words);
   HIP_THROW(hipGetLastError());
 }
 
 void
 copy_words(void *y, const void *x, int64_t n_words, hipStream_t s)
 {
-  if (mem_nodes())
-    HIP_THROW(hipMemcpyAsync(y, x, (size_t)n_words * 4, hipMemcpyDeviceToDevice, s));
-  else
-    hipLaunchKernelGGL(k_copy, g1(n_words), dim3(256), 0, s, (uint32_t *)y,
-                       (const uint32_t *)x, n_words);
+  hipLaunchKernelGGL(k_copy, g1(n_words), dim3(256), 0, s, (uint32_t *)y, (const uint32_t *)x,
+                     n_words);
   HIP_THROW(hipGetLastError());
 }
 
@@ -643,17 +627,6 @@ struct glsMG_
   bool                    setup_done = false;
   bool                    partitioned = false; // rank-local level operators
   gls::VecStage           stage; // caller layout of gls_mg_vcycle's vectors
-  // the V-cycle body (v_step on the finest level: ~80 launches between the
-  // copy_to_mg / copy_from_mg conversions, all on the multigrid's own
-  // buffers) captured once as a hipGraph and replayed on the caller's
-  // stream; re-captured after gls_mg_setup or when a level operator's state
-  // version moved (kernel arguments are captured by value).  GLS_MG_GRAPH=1
-  // enables it (off by default: measured slower, run_v_step).
-  hipGraph_t            graph      = nullptr;
-  hipGraphExec_t        graph_exec = nullptr;
-  hipStream_t           cap_stream = nullptr; // capture, then replay stream
-  hipEvent_t            ev_in = nullptr, ev_out = nullptr;
-  std::vector<uint64_t> graph_versions;
   // dense LU coarse solver (coarse_n_iterations < 0): the substitute for the
   // reference's Trilinos direct solver (multigrid.cc:448-455, 477-481)
   rocblas_handle blas   = nullptr;
@@ -1006,15 +979,6 @@ check_blas(rocblas_status st, const char *what)
   if (st != rocblas_status_success)
     throw std::runtime_error(std::string(what) + " failed (rocblas status " +
                              std::to_string((int)st) + ")");
-}
-
-// p[i] = i + 1 (LAPACK identity pivots)
-__global__ void
-k_iota1(rocblas_int *p, int64_t n)
-{
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n)
-    p[i] = (rocblas_int)(i + 1);
 }
 
 // X = the unit lower triangle of the LU factors (column major n x n):
@@ -1567,6 +1531,21 @@ assemble_free_block(glsMG_ *mg, const std::vector<int32_t> &freel, hipStream_t s
   return ok;
 }
 
+// GLS_COARSE_REFERENCE: a comma-separated list of reference forms of the
+// dense coarse solver for tests -- "columns" (A_ff assembled column by
+// column from unit-vector vmults instead of the element matrices), "getrs"
+// / "getri" (the inverse by getrs with the identity / by getri instead of
+// U^-1 L^-1), "nocond" (no static condensation)
+bool
+coarse_reference(const char *what)
+{
+  const char *e = getenv("GLS_COARSE_REFERENCE");
+  if (!e)
+    return false;
+  const std::string list = std::string(",") + e + ",";
+  return list.find(std::string(",") + what + ",") != std::string::npos;
+}
+
 // Assemble the coarse level operator into FP64 and LU-factorise it.  Only
 // the free (unconstrained) dofs take part: a constrained dof's row and
 // column of A are both the unit vector (identity rows of vmult, homogeneous
@@ -1589,17 +1568,15 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
     if (!((op->h_cmask[(size_t)(d / nc)] >> (d % nc)) & 1))
       freel.push_back((int32_t)d);
   // static condensation of the cells' interior dofs (default with the
-  // element-matrix assembly; GLS_COARSE_CONDENSE=0 off): a node with every
+  // element-matrix assembly; GLS_COARSE_REFERENCE=nocond off): a node with every
   // lattice coordinate inside (0, k) belongs to one cell only, so its dofs
   // are eliminated cell by cell (Schur complement of the element matrix) and
   // the dense inverse covers the other free dofs (Re3900 r0: 12,606 of
   // 14,206, 0.70x the factorisation flops, 0.79x the GEMV's bytes); the
   // coarse solve adds the condensed right-hand side b_B - F b_I before the
   // GEMV and x_I = C b_I - G x_B after it (k_cond_rhs / k_cond_post)
-  const char *ca      = getenv("GLS_COARSE_ASSEMBLY");
-  const bool  columns = ca && std::string(ca) == "columns";
+  const bool columns = coarse_reference("columns");
   {
-    const char *cc = getenv("GLS_COARSE_CONDENSE");
     const int   k  = op->degree, dim = op->dim, nq = op->nq;
     mg->cond_lint.clear(), mg->cond_lbnd.clear();
     for (int p = 0; p < nq; ++p)
@@ -1610,7 +1587,7 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
           (in ? mg->cond_lint : mg->cond_lbnd).push_back(p * nc + q);
       }
     const int ni = (int)mg->cond_lint.size(), nb = (int)mg->cond_lbnd.size();
-    bool      cond = !columns && !(cc && cc[0] == '0') && !mg->cond_failed && ni > 0 && ni <= COND_MAXI &&
+    bool      cond = !columns && !coarse_reference("nocond") && !mg->cond_failed && ni > 0 && ni <= COND_MAXI &&
                 nb <= 128 && nb * ni <= 1024;
     std::vector<char> is_int((size_t)n, 0);
     for (int64_t c = 0; cond && c < op->n_cells; ++c)
@@ -1703,20 +1680,9 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
     }
   HIP_THROW(hipStreamSynchronize(s));
   const auto t1 = std::chrono::steady_clock::now();
-  // GLS_COARSE_LU=npvt (measurement switch): LU without pivoting, identity
-  // pivots for getrs
-  const char *cl = getenv("GLS_COARSE_LU");
-  if (cl && std::string(cl) == "npvt")
-    {
-      check_blas(rocsolver_dgetrf_npvt(mg->blas, (rocblas_int)nf, (rocblas_int)nf, mg->d_lu,
-                                       (rocblas_int)nf, mg->d_info),
-                 "rocsolver_dgetrf_npvt");
-      hipLaunchKernelGGL(k_iota1, g1(nf), dim3(256), 0, s, mg->d_ipiv, nf);
-    }
-  else
-    check_blas(rocsolver_dgetrf(mg->blas, (rocblas_int)nf, (rocblas_int)nf, mg->d_lu,
-                                (rocblas_int)nf, mg->d_ipiv, mg->d_info),
-               "rocsolver_dgetrf");
+  check_blas(rocsolver_dgetrf(mg->blas, (rocblas_int)nf, (rocblas_int)nf, mg->d_lu,
+                              (rocblas_int)nf, mg->d_ipiv, mg->d_info),
+             "rocsolver_dgetrf");
   rocblas_int info = 0;
   HIP_THROW(hipMemcpyAsync(&info, mg->d_info, sizeof(info), hipMemcpyDeviceToHost, s));
   HIP_THROW(hipStreamSynchronize(s));
@@ -1727,16 +1693,17 @@ coarse_lu_setup_t(glsMG_ *mg, hipStream_t s)
   // the inverse from the LU factors, once: every coarse solve is then one
   // GEMV streaming the nf x nf matrix at HBM rate (the two triangular solves
   // of getrs ran 33.7 ms per V-cycle at n = 16,704 on MI355X).  Default
-  // (GLS_COARSE_INVERT unset or "trtri"): Z = U^-1 L^-1 from the unit lower
+  // Z = U^-1 L^-1 from the unit lower
   // factor inverted in place (rocsolver_dtrtri, n^3 / 3 flops) and one
   // triangular solve with U (rocblas_dtrsm, n^3): 4/3 n^3 instead of the
   // 2 n^3 of getrs with the identity, and A^-1 = Z P^T needs no column
   // permutation of the matrix: the GEMV gathers its input through free[p[i]]
-  // (d_free_in).  "getrs": the identity as right-hand side (rocsolver
-  // dgetrs); "getri": rocsolver_dgetri in place.
+  // (d_free_in).  Reference forms (GLS_COARSE_REFERENCE): "getrs", the
+  // identity as right-hand side (rocsolver dgetrs); "getri", rocsolver_dgetri
+  // in place.
   std::vector<int32_t> fin = freel; // the GEMV's input gather
-  const char *ci = getenv("GLS_COARSE_INVERT");
-  const std::string inv_mode = ci ? ci : "trtri";
+  const std::string inv_mode = coarse_reference("getri") ? "getri" :
+                               coarse_reference("getrs") ? "getrs" : "trtri";
   if (inv_mode == "getri")
     {
       check_blas(rocsolver_dgetri(mg->blas, (rocblas_int)nf, mg->d_lu, (rocblas_int)nf,
@@ -1922,19 +1889,11 @@ coarse_lu_solve_t(glsMG_ *mg, hipStream_t s)
                            (T *)mg->sol[0], (const T *)mg->def[0], xf,
                            (const int32_t *)mg->d_free_in, n, nf, ld);
       // the inverse is read once per solve and is larger than the MALL:
-      // non-temporal row loads (GLS_GEMV_NT=0: default policy)
-      static const bool nt = [] {
-        const char *e = getenv("GLS_GEMV_NT");
-        return !e || std::atoi(e) != 0;
-      }();
-      if (nt)
-        hipLaunchKernelGGL((k_gemv_rows_f32<T, true>), dim3((unsigned)((nf + 3) / 4)), dim3(256),
-                           0, s, (const float4 *)mg->d_inv32, (const float4 *)xf, (T *)mg->sol[0],
-                           (const int32_t *)mg->d_free, nf, ld);
-      else
-        hipLaunchKernelGGL((k_gemv_rows_f32<T, false>), dim3((unsigned)((nf + 3) / 4)), dim3(256),
-                           0, s, (const float4 *)mg->d_inv32, (const float4 *)xf, (T *)mg->sol[0],
-                           (const int32_t *)mg->d_free, nf, ld);
+      // non-temporal row loads (132 against 146 us with the default policy,
+      // round 3)
+      hipLaunchKernelGGL((k_gemv_rows_f32<T, true>), dim3((unsigned)((nf + 3) / 4)), dim3(256), 0,
+                         s, (const float4 *)mg->d_inv32, (const float4 *)xf, (T *)mg->sol[0],
+                         (const int32_t *)mg->d_free, nf, ld);
       HIP_THROW(hipGetLastError());
       if (mg->cond)
         cond_post_t<T>(mg, s);
@@ -2283,11 +2242,7 @@ v_step_body(glsMG_ *mg, int l, hipStream_t s)
       return;
     }
   // the last smoothing step's reduction of a level below the finest handed
-  // to the prolongation that reads its result (GLS_MG_DEFER_PROLONG=0: off)
-  static const bool defer_pro = [] {
-    const char *e = getenv("GLS_MG_DEFER_PROLONG");
-    return !(e && e[0] == '0');
-  }();
+  // to the prolongation that reads its result (GLS_MG_DEFER=0: off)
   auto hand_over = [&](int lc, const PendingReduce &p) {
     if (!p.valid)
       return;
@@ -2295,7 +2250,7 @@ v_step_body(glsMG_ *mg, int l, hipStream_t s)
     mg->pp_b = p.b, mg->pp_d = p.d, mg->pp_omega = p.omega;
   };
   const bool pro_ok = [&](int lc) {
-    return defer_pro && mg->prec == GLS_F32 && mg->dim == 3 && lc + 1 < (int)mg->ops.size() &&
+    return mg->prec == GLS_F32 && mg->dim == 3 && lc + 1 < (int)mg->ops.size() &&
            defer_reduce(mg, lc);
   }(l);
   if (l == 0)
@@ -2338,11 +2293,7 @@ v_step_body(glsMG_ *mg, int l, hipStream_t s)
       // the residual's own reduction deferred into the restriction's gather
       // (its only reader: the prolongation overwrites tmp afterwards), into
       // the slot buffer the pre-smoothing's pending slots do not occupy
-      static const bool defer_res = [] {
-        const char *e = getenv("GLS_MG_DEFER_RESIDUAL");
-        return !(e && e[0] == '0');
-      }();
-      if (defer_res && defer_reduce(mg, l) && mg->prec == GLS_F32 && mg->ops[l]->dim == 3)
+      if (defer_reduce(mg, l) && mg->prec == GLS_F32 && mg->ops[l]->dim == 3)
         {
           void *q0   = mg->qslot[0][(size_t)l], *q1 = mg->qslot[1][(size_t)l];
           rs.defer   = true;
@@ -2437,78 +2388,14 @@ power_iteration_t(glsMG_ *mg, int l, hipStream_t s)
     }
 }
 
-// v_step(top) on stream s: replayed from a captured hipGraph when possible
+// v_step(top) on stream s.  (A hipGraph replay of the whole cycle, captured
+// once per setup, measured slower than these direct launches -- 0.539 vs
+// 0.484 ms: the cycle's launches run back to back, there is no launch
+// overhead to remove -- and is on the git tag r4-graph-replay.)
 void
 run_v_step(glsMG_ *mg, int top, hipStream_t s)
 {
-  // measured (bench companion r2_vcycle_f32_coarse_relax10): the replay was
-  // slower than direct launches (0.67 vs 0.58 ms): the V-cycle is bound by
-  // the kernels' own duration, not by host launch overhead; off by default
-  const char *e   = getenv("GLS_MG_GRAPH");
-  const bool  use = (e && std::atoi(e) != 0) &&
-                   !mg->desc.coarse_iterate && // coarse GMRES syncs the host
-                   !mg->desc.coarse_amg;       // (AMG cycle: not captured)
-  if (!use)
-    {
-      v_step(mg, top, s);
-      return;
-    }
-  std::vector<uint64_t> ver;
-  for (glsOp op : mg->ops)
-    ver.push_back(op->version);
-  if (!mg->graph_exec || ver != mg->graph_versions)
-    {
-      if (mg->graph_exec)
-        HIP_THROW(hipGraphExecDestroy(mg->graph_exec));
-      if (mg->graph)
-        HIP_THROW(hipGraphDestroy(mg->graph));
-      mg->graph_exec = nullptr;
-      mg->graph      = nullptr;
-      if (!mg->cap_stream)
-        HIP_THROW(hipStreamCreateWithFlags(&mg->cap_stream, hipStreamNonBlocking));
-      HIP_THROW(hipStreamBeginCapture(mg->cap_stream, hipStreamCaptureModeThreadLocal));
-      try
-        {
-          v_step(mg, top, mg->cap_stream);
-        }
-      catch (...)
-        {
-          hipGraph_t g = nullptr;
-          (void)hipStreamEndCapture(mg->cap_stream, &g);
-          if (g)
-            (void)hipGraphDestroy(g);
-          throw;
-        }
-      HIP_THROW(hipStreamEndCapture(mg->cap_stream, &mg->graph));
-      HIP_THROW(hipGraphInstantiate(&mg->graph_exec, mg->graph, nullptr, nullptr, 0));
-      mg->graph_versions = ver;
-    }
-  if (e && std::atoi(e) == 2) // debug: captured, but run kernel by kernel
-    {
-      v_step(mg, top, s);
-      return;
-    }
-  if (e && std::atoi(e) == 3) // debug: replay on the caller's stream, synchronised
-    {
-      HIP_THROW(hipStreamSynchronize(s));
-      HIP_THROW(hipGraphLaunch(mg->graph_exec, s));
-      HIP_THROW(hipStreamSynchronize(s));
-      return;
-    }
-  // replay on the multigrid's own stream, ordered after the caller's work
-  // (copy_to_mg) and before what follows (copy_from_mg) by events: a graph
-  // launched on the legacy NULL stream was measured NOT to wait for the
-  // preceding kernel (scripts/graph_diag.py)
-  if (!mg->ev_in)
-    {
-      HIP_THROW(hipEventCreateWithFlags(&mg->ev_in, hipEventDisableTiming));
-      HIP_THROW(hipEventCreateWithFlags(&mg->ev_out, hipEventDisableTiming));
-    }
-  HIP_THROW(hipEventRecord(mg->ev_in, s));
-  HIP_THROW(hipStreamWaitEvent(mg->cap_stream, mg->ev_in, 0));
-  HIP_THROW(hipGraphLaunch(mg->graph_exec, mg->cap_stream));
-  HIP_THROW(hipEventRecord(mg->ev_out, mg->cap_stream));
-  HIP_THROW(hipStreamWaitEvent(s, mg->ev_out, 0));
+  v_step(mg, top, s);
 }
 
 } // namespace
@@ -2685,16 +2572,6 @@ gls_mg_destroy(glsMG mg)
     gls_amg_destroy(mg->amg);
   if (mg->amg_io)
     (void)hipFree(mg->amg_io);
-  if (mg->graph_exec)
-    (void)hipGraphExecDestroy(mg->graph_exec);
-  if (mg->graph)
-    (void)hipGraphDestroy(mg->graph);
-  if (mg->cap_stream)
-    (void)hipStreamDestroy(mg->cap_stream);
-  if (mg->ev_in)
-    (void)hipEventDestroy(mg->ev_in);
-  if (mg->ev_out)
-    (void)hipEventDestroy(mg->ev_out);
   mg->stage.release();
   delete mg;
 }
@@ -2831,7 +2708,6 @@ gls_mg_setup(glsMG mg, void *stream)
     }
   HIP_THROW(hipStreamSynchronize(s));
   mg->setup_done = true;
-  mg->graph_versions.clear(); // omega / diagonals changed: re-capture
   GLS_CATCH
 }
 
@@ -2928,12 +2804,9 @@ mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s)
   const int64_t n   = mg->ops[top]->n_dofs;
   const bool    cvt = mg->desc.outer_precision == GLS_F64 && mg->prec == GLS_F32;
   // copy_to_mg: folded into the finest level's first relaxation (v_step)
-  // when the V-cycle runs directly with a smoothing level on top; a captured
-  // graph would freeze src's address, the coarse-only hierarchy has no
-  // relaxation to fold into
-  const char *ge     = getenv("GLS_MG_GRAPH");
-  const bool  graph  = ge && std::atoi(ge) != 0;
-  const bool  folded = cvt && top > 0 && !graph && mg->desc.smoothing_n_iterations > 0;
+  // when the V-cycle has a smoothing level on top (the coarse-only hierarchy
+  // has no relaxation to fold into)
+  const bool folded = cvt && top > 0 && mg->desc.smoothing_n_iterations > 0;
   if (folded)
     {
       mg->top_b64   = (const double *)src;

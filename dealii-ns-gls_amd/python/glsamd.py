@@ -836,7 +836,7 @@ class Multigrid:
     def coarse_setup_times(self):
         """{assembly_ms, getrf_ms, inverse_ms, colors} of the last dense-coarse
         setup (coarse_n_iterations=-1); inverse_ms: the inverse from the LU
-        factors (trtri + trsm by default, GLS_COARSE_INVERT)."""
+        factors (trtri + trsm by default, GLS_COARSE_REFERENCE=getrs|getri)."""
         ms = (C.c_double * 3)()
         nc = C.c_int()
         _check(lib().gls_mg_coarse_setup_times(self.h, ms, C.byref(nc)))

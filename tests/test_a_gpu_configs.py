@@ -271,28 +271,22 @@ def test_coarse_assembly_element_matrices():
     """The dense coarse solver's free-dof block assembled from the level's
     element matrices (one launch + one scatter per cell colour) against the
     column-by-column assembly from unit-vector vmults
-    (GLS_COARSE_ASSEMBLY=columns), FP64 levels r0..r1: the V-cycles agree."""
+    (GLS_COARSE_REFERENCE=columns), FP64 levels r0..r1: the V-cycles agree."""
     import os
     import torch
     import glsamd
     meshes, cm, params, w, u, hist = _re3900(1)
     b = torch.from_numpy(gi.rnd(11, meshes[-1].n_dofs)).cuda()
     out = {}
-    for mode in ("columns", "elements", "getri", "npvt"):
-        if mode == "columns":
-            os.environ["GLS_COARSE_ASSEMBLY"] = "columns"
-            os.environ["GLS_COARSE_INVERT"] = "getri"
-        if mode == "getri":
-            os.environ["GLS_COARSE_INVERT"] = "getri"
-        if mode == "npvt":
-            os.environ["GLS_COARSE_LU"] = "npvt"
+    for mode in ("columns", "elements", "getri", "nocond"):
+        ref = {"columns": "columns,getri", "getri": "getri", "nocond": "nocond"}.get(mode)
+        if ref:
+            os.environ["GLS_COARSE_REFERENCE"] = ref
         try:
             mg, ops = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f64",
                                        coarse_n_iterations=-1)
         finally:
-            os.environ.pop("GLS_COARSE_ASSEMBLY", None)
-            os.environ.pop("GLS_COARSE_INVERT", None)
-            os.environ.pop("GLS_COARSE_LU", None)
+            os.environ.pop("GLS_COARSE_REFERENCE", None)
         print(mode, mg.coarse_setup_times())
         x = torch.zeros_like(b)
         mg.vcycle(x, b)
@@ -304,10 +298,10 @@ def test_coarse_assembly_element_matrices():
     # coarse system's conditioning times the different summation / solve order
     err = rel_err(out["elements"], out["columns"])
     err_inv = rel_err(out["elements"], out["getri"])
+    err_cond = rel_err(out["elements"], out["nocond"])
     print(f"element vs column coarse assembly: V-cycle rel diff {err:.2e}; "
-          f"getrs vs getri inverse {err_inv:.2e}; no-pivot LU "
-          f"{rel_err(out['npvt'], out['elements']):.2e}")
-    assert err < 1e-10 and err_inv < 1e-10
+          f"U^-1 L^-1 vs getri inverse {err_inv:.2e}; condensed vs uncondensed {err_cond:.2e}")
+    assert err < 1e-10 and err_inv < 1e-10 and err_cond < 1e-10
 
 
 # the oracle multigrid's setup at r3 (inverse diagonals by 108 unit-vector
