@@ -944,7 +944,7 @@ def main():
         # HBM bytes per vmult from the committed rocprofv3 PMC passes of this
         # workload (scripts/pmc.sh + scripts/pmc_summary.py), when they match
         traffic = None
-        tf = os.environ.get("GLS_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r04", "pmc_r2",
+        tf = os.environ.get("GLS_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r05", "pmc_r2",
                                                              "traffic.json"))
         if tf and os.path.exists(tf) and world == 1:
             with open(tf) as f:
