@@ -127,6 +127,7 @@ struct BrickArgs
   T               nu, w0, theta, stau;
   T               nu4, stau2; // 4 nu, stau^2 (delta_qwise_fast)
   int             td, cw, have_prev, have_old_grad;
+  int             det; // deterministic lattice accumulation (GLS_DETERMINISTIC): k_brick<..., DET>
   Shape<T, n>     sh;
 };
 
@@ -500,7 +501,10 @@ struct BrickOcc
   static constexpr int  waves = four || sizeof(T) == 4 ? 4 : 3;
 };
 
-template <int dim, int k, typename T, int MODE, int GEO = GEO_ANY, int ZL = 1>
+// DET: the deterministic lattice accumulation (GLS_DETERMINISTIC: the cells
+// of a round add in cell order between barriers instead of by LDS atomics;
+// its own instantiation, so the default kernels keep their registers)
+template <int dim, int k, typename T, int MODE, int GEO = GEO_ANY, int ZL = 1, bool DET = false>
 __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO, ZL>::waves))
   k_brick(BrickArgs<T, dim, k + 1> a)
 {

@@ -753,34 +753,37 @@ struct Impl
 
   // the brick kernel over n_units work units of one geometry type, one
   // workgroup per unit
-  template <int M>
+  template <int M, bool DET = false>
   static void
   launch_brick(int64_t n_units, size_t lds, int geo, hipStream_t s, const BrickArgs<T, dim, n> &a)
   {
+    if constexpr (!DET)
+      if (a.det) // the deterministic accumulation: its own instantiations
+        return launch_brick<M, true>(n_units, lds, geo, s, a);
     // two-layer bricks (3D Q2, build_bricks): two lattice chunks per thread
     if constexpr (dim == 3 && k == 2)
       if (a.L > BrickLattice<dim, k, 1>::L)
         {
           if (geo == GEO_GEN)
-            hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_GEN, 2>), dim3((unsigned)n_units),
+            hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_GEN, 2, DET>), dim3((unsigned)n_units),
                                dim3(BLOCK), lds, s, a);
           else if (geo == GEO_CART)
-            hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_CART, 2>), dim3((unsigned)n_units),
+            hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_CART, 2, DET>), dim3((unsigned)n_units),
                                dim3(BLOCK), lds, s, a);
           else
-            hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_ANY, 2>), dim3((unsigned)n_units),
+            hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_ANY, 2, DET>), dim3((unsigned)n_units),
                                dim3(BLOCK), lds, s, a);
           return;
         }
     if (geo == GEO_GEN)
-      hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_GEN>), dim3((unsigned)n_units), dim3(BLOCK),
-                         lds, s, a);
+      hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_GEN, 1, DET>), dim3((unsigned)n_units),
+                         dim3(BLOCK), lds, s, a);
     else if (geo == GEO_CART)
-      hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_CART>), dim3((unsigned)n_units), dim3(BLOCK),
-                         lds, s, a);
+      hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_CART, 1, DET>), dim3((unsigned)n_units),
+                         dim3(BLOCK), lds, s, a);
     else
-      hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_ANY>), dim3((unsigned)n_units), dim3(BLOCK),
-                         lds, s, a);
+      hipLaunchKernelGGL((k_brick<dim, k, T, M, GEO_ANY, 1, DET>), dim3((unsigned)n_units),
+                         dim3(BLOCK), lds, s, a);
   }
 
   // brick kernel over work units [b0, b1) (what & BRICK_RUN) and the
@@ -872,6 +875,7 @@ struct Impl
         a.cw            = (op->prm.flags & GLS_CELL_WISE_STAB) ? 1 : 0;
         a.have_prev     = op->have_prev ? 1 : 0;
         a.have_old_grad = (op->have_old_grad && op->prm.theta != 1.0) ? 1 : 0;
+        a.det           = (op->prm.flags & GLS_DETERMINISTIC) ? 1 : 0;
         a.sh            = make_shape<T, n>(op->basis);
         if ((what & BRICK_RUN) && b1 > b0 && mode == MODE_NEWTON)
           {
@@ -964,14 +968,30 @@ struct Impl
       for (int i = 0; i < n; ++i)
         da.D[q][i] = (T)op->basis.D[q * n + i];
     constexpr int CPB = (64 / nq > 0 ? 64 / nq : 1) * (BLOCK / 64);
-    const dim3    grid((unsigned)((op->n_cells + CPB - 1) / CPB));
     if (op->n_cells == 0)
       return;
-    if (mode == MODE_NEWTON)
-      hipLaunchKernelGGL((k_diag<dim, k, T, MODE_NEWTON>), grid, dim3(BLOCK), 0, s, da);
+    auto launch = [&](const DiagArgs<T, dim, n> &x, int64_t cells) {
+      const dim3 grid((unsigned)((cells + CPB - 1) / CPB));
+      if (mode == MODE_NEWTON)
+        hipLaunchKernelGGL((k_diag<dim, k, T, MODE_NEWTON>), grid, dim3(BLOCK), 0, s, x);
+      else
+        hipLaunchKernelGGL((k_diag<dim, k, T, MODE_FIXED>), grid, dim3(BLOCK), 0, s, x);
+      HIP_THROW(hipGetLastError());
+    };
+    if (!op_deterministic(op))
+      launch(da, op->n_cells);
     else
-      hipLaunchKernelGGL((k_diag<dim, k, T, MODE_FIXED>), grid, dim3(BLOCK), 0, s, da);
-    HIP_THROW(hipGetLastError());
+      {
+        // colour by colour: no two cells of a launch add to one node
+        op_cell_colours(const_cast<glsOp_ *>(op));
+        for (size_t c = 0; c + 1 < op->colour_off.size(); ++c)
+          {
+            DiagArgs<T, dim, n> x = da;
+            x.cells               = op->d_colour_cells + op->colour_off[c];
+            x.n_list              = op->colour_off[c + 1] - op->colour_off[c];
+            launch(x, x.n_list);
+          }
+      }
   }
 
   static void
@@ -1784,7 +1804,8 @@ gls_op_destroy(glsOp op)
                   op->d_brick_target, op->d_shared_nodes, op->d_shared_off,
                   op->d_shared_index, op->d_partial,      op->d_bgeo_cart,    op->d_bgeo_gen,
                   op->d_brick_geo,    op->d_brick_cell0,  op->d_brick_chunk0, op->d_tab_cbase,
-                  op->d_node_cmask,   op->d_inhom,        op->gmres_ws};
+                  op->d_node_cmask,   op->d_inhom,        op->gmres_ws,
+                  op->d_colour_cells};
   for (void *b : bufs)
     if (b)
       (void)hipFree(b);
@@ -2187,6 +2208,44 @@ gls_op_compute_inverse_diagonal(glsOp op, void *diag_, void *stream)
 
 namespace gls
 {
+void
+op_cell_colours(glsOp_ *op)
+{
+  if (op->d_colour_cells)
+    return;
+  const int64_t nc_ = op->n_cells;
+  const int     nq  = op->nq;
+  // per node, the colours of the cells already coloured that touch it
+  std::vector<uint64_t> used((size_t)op->n_nodes, 0);
+  std::vector<int>      colour((size_t)nc_, 0);
+  int                   n_col = 0;
+  for (int64_t c = 0; c < nc_; ++c)
+    {
+      const uint32_t *cn   = &op->h_cell_nodes[(size_t)ext_cell(op, c) * nq];
+      uint64_t        mask = 0;
+      for (int p = 0; p < nq; ++p)
+        mask |= used[cn[p]];
+      if (~mask == 0)
+        throw std::runtime_error("deterministic assembly: more than 64 cell colours");
+      const int k = __builtin_ctzll(~mask);
+      colour[(size_t)c] = k;
+      n_col             = std::max(n_col, k + 1);
+      for (int p = 0; p < nq; ++p)
+        used[cn[p]] |= 1ull << k;
+    }
+  std::vector<int32_t> list;
+  list.reserve((size_t)nc_);
+  op->colour_off.assign(1, 0);
+  for (int k = 0; k < n_col; ++k)
+    {
+      for (int64_t c = 0; c < nc_; ++c)
+        if (colour[(size_t)c] == k)
+          list.push_back((int32_t)c);
+      op->colour_off.push_back((int64_t)list.size());
+    }
+  upload((void **)&op->d_colour_cells, list);
+}
+
 void
 op_inverse_diagonal_device(glsOp op, void *diag, hipStream_t s)
 {

@@ -1134,6 +1134,9 @@ struct DiagArgs
   ApplyArgs<T, dim, n> a;
   T                    D[n][n]; // D[q][i] = phi_i'(x_q) (nodal basis derivative)
   double              *diag;    // [n_dofs] FP64 accumulator (both precisions)
+  // deterministic assembly: the cells of one colour (null: all cells)
+  const int32_t       *cells  = nullptr;
+  int64_t              n_list = 0;
 };
 
 template <int dim, int k, typename T, int MODE>
@@ -1163,8 +1166,9 @@ __global__ void __launch_bounds__(BLOCK)
   const int     p       = lane - slot * nq;
   const bool    in_wave = slot < CPW;
   const int     lc      = wave * CPW + (in_wave ? slot : 0);
-  const int64_t cell    = (int64_t)blockIdx.x * CPB + lc;
-  const bool    active  = in_wave && cell < a.cell_end;
+  const int64_t idx     = (int64_t)blockIdx.x * CPB + lc;
+  const int64_t cell    = da.cells ? (idx < da.n_list ? (int64_t)da.cells[idx] : 0) : idx;
+  const bool    active  = in_wave && (da.cells ? idx < da.n_list : cell < a.cell_end);
   const int     pa[3]   = {p % n, (p / n) % n, dim == 3 ? p / (n * n) : 0};
   if (active)
     {

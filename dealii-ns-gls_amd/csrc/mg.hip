@@ -68,6 +68,9 @@ struct TransferArgs
   const T        *p_d       = nullptr;
   T               p_omega   = T(0);
   gls::ReduceClasses p_rc{};
+  // deterministic restriction (GLS_DETERMINISTIC): the coarse cells of one
+  // colour, one workgroup each (null: workgroup c = coarse cell c)
+  const int32_t  *cells     = nullptr;
 };
 
 // the relaxation step x_prev + omega d (b - A x_prev) at shared coarse node s
@@ -293,7 +296,7 @@ __global__ void __launch_bounds__(256)
   constexpr int nl = ipow(L, dim);
   __shared__ T  v[nc][nl];
   __shared__ T  sP[L][n];
-  const int64_t c = blockIdx.x;
+  const int64_t c = a.cells ? (int64_t)a.cells[blockIdx.x] : (int64_t)blockIdx.x;
   const int     t = threadIdx.x;
   // this thread's coarse dof (node id, constraint bits) is independent of
   // the fine gather: loaded up front (blockDim >= nq * nc, k <= 2 in 3D)
@@ -749,8 +752,23 @@ transfer_t(const glsMG_ *mg, int kind, int level, void *dst, const void *src, hi
   if (kind == 0)
     hipLaunchKernelGGL((k_prolongate<dim, k, T>), grid, tb, 0, s, a, (T *)dst, (const T *)src,
                        (const T *)base);
-  else if (kind == 1)
+  else if (kind == 1 && !gls::op_deterministic(mg->ops[level - 1]))
     hipLaunchKernelGGL((k_restrict<dim, k, T>), grid, tb, 0, s, a, (T *)dst, (const T *)src);
+  else if (kind == 1)
+    {
+      // coarse cell colour by colour: no two workgroups of a launch add to
+      // one coarse node, the sums in a fixed order
+      glsOp_ *oc = const_cast<glsOp_ *>(mg->ops[level - 1]);
+      gls::op_cell_colours(oc);
+      for (size_t col = 0; col + 1 < oc->colour_off.size(); ++col)
+        {
+          auto ac  = a;
+          ac.cells = oc->d_colour_cells + oc->colour_off[col];
+          hipLaunchKernelGGL((k_restrict<dim, k, T>),
+                             dim3((unsigned)(oc->colour_off[col + 1] - oc->colour_off[col])), tb, 0,
+                             s, ac, (T *)dst, (const T *)src);
+        }
+    }
   else
     hipLaunchKernelGGL((k_interpolate<dim, k, T>), g1(a.n_cells_c * nq), dim3(256), 0, s, a,
                        (T *)dst, (const T *)src);

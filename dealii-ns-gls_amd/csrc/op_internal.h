@@ -125,6 +125,12 @@ struct glsOp_
   uint32_t *d_shared_nodes = nullptr;
   uint32_t *d_shared_off   = nullptr;
   int32_t  *d_shared_index = nullptr; // node -> shared index (-1: exclusive)
+  // cells grouped by colour (no two cells of a colour share a node; internal
+  // order): the deterministic (GLS_DETERMINISTIC) assembly of the diagonal
+  // and of the multigrid restriction, colour by colour without atomics
+  // (built on first use, op_cell_colours)
+  int32_t             *d_colour_cells = nullptr;
+  std::vector<int64_t> colour_off;
   gls::ReduceClasses reduce_classes{}; // multiplicity classes of the shared nodes
   // the shared nodes are ordered [owned | ghost]: the first n_shared_owned
   // are owned rows; classes of each part on its own (first[] relative to the
@@ -172,6 +178,17 @@ inline int64_t
 ext_cell(const glsOp_ *op, int64_t c)
 {
   return op->cell_perm.empty() ? c : op->cell_perm[(size_t)c];
+}
+
+// the operator's cells by colour (greedy over the internal order; cells of a
+// colour share no node): device list op->d_colour_cells, colour k at
+// [colour_off[k], colour_off[k+1])
+void op_cell_colours(glsOp_ *op);
+
+inline bool
+op_deterministic(const glsOp_ *op)
+{
+  return (op->prm.flags & GLS_DETERMINISTIC) != 0;
 }
 
 // fused damped-Jacobi step of the multigrid smoother (csrc/mg.hip): with it a

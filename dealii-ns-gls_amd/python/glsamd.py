@@ -19,6 +19,7 @@ _lib = None
 
 GLS_F64, GLS_F32 = 0, 1
 GLS_INCREMENT_FORM, GLS_CONSIDER_TIME_DERIVATIVE, GLS_CELL_WISE_STAB = 1, 2, 4
+GLS_DETERMINISTIC = 8
 
 # exported symbols of include/gls_op.h (checked by tests/test_abi.py)
 EXPORTS = [
@@ -382,10 +383,14 @@ class NavierStokesOperator:
 
     def set_parameters(self, nu, c1=1.0, c2=1.0, theta=1.0, w0=0.0, dt=1.0, order=0,
                        increment_form=True, consider_time_derivative=False,
-                       cell_wise_stabilization=False):
+                       cell_wise_stabilization=False, deterministic=False):
+        """deterministic: GLS_DETERMINISTIC (not a reference parameter) --
+        bitwise reproducible results run to run (ordered lattice
+        accumulation, colour-by-colour diagonal and restriction), slower"""
         flags = ((GLS_INCREMENT_FORM if increment_form else 0)
                  | (GLS_CONSIDER_TIME_DERIVATIVE if consider_time_derivative else 0)
-                 | (GLS_CELL_WISE_STAB if cell_wise_stabilization else 0))
+                 | (GLS_CELL_WISE_STAB if cell_wise_stabilization else 0)
+                 | (GLS_DETERMINISTIC if deterministic else 0))
         self.params = OpParams(nu, c1, c2, theta, w0, dt, order, flags)
         _check(lib().gls_op_set_parameters(self.h, C.byref(self.params)))
 

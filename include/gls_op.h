@@ -89,7 +89,13 @@ enum glsFlags
 {
   GLS_INCREMENT_FORM           = 1, /* Newton: increment_form, main.cc:331    */
   GLS_CONSIDER_TIME_DERIVATIVE = 2, /* consider_time_derivative (ctor arg)    */
-  GLS_CELL_WISE_STAB           = 4  /* cell_wise_stabilization (ctor arg)     */
+  GLS_CELL_WISE_STAB           = 4, /* cell_wise_stabilization (ctor arg)     */
+  /* not a reference parameter: results bitwise reproducible run to run (the
+   * brick kernels add a round's cells into the LDS lattice in cell order
+   * instead of by LDS atomics; the diagonal and the multigrid restriction
+   * assemble cell colour by colour instead of by global atomics), at some
+   * cost in speed; debugging, SURVEY §7.2.2 */
+  GLS_DETERMINISTIC            = 8
 };
 
 typedef struct

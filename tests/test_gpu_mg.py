@@ -257,8 +257,10 @@ def test_coarse_inverse_trtri_vs_getrs(prec, monkeypatch):
             monkeypatch.setenv("GLS_COARSE_REFERENCE", "getrs")
         else:
             monkeypatch.delenv("GLS_COARSE_REFERENCE", raising=False)
-        mg, _ = glsamd.build_gmg(meshes, cmasks, params, u, hist, w, precision=prec,
-                                 coarse_n_iterations=-1)
+        # deterministic mode: repeated cycles bitwise equal, so the bound
+        # below is the inverses' own difference, not run-to-run noise
+        mg, _ = glsamd.build_gmg(meshes, cmasks, dict(params, deterministic=True), u, hist, w,
+                                 precision=prec, coarse_n_iterations=-1)
         src = torch.from_numpy(b).cuda()
         ys = []
         for _ in range(2):
@@ -274,11 +276,11 @@ def test_coarse_inverse_trtri_vs_getrs(prec, monkeypatch):
           f"getrs {out['getrs'][1]}, trtri {out['trtri'][1]}")
     # FP64: two orderings of the same inverse of a coarse matrix whose FP64 LU
     # already differs from the oracle's numpy LU by ~4e-12 in the V-cycle
-    # (test_vcycle_re3900_f64_levels_tight[-1]); measured 1.15e-12.  FP32: the
-    # FP32 copies of the two inverses, under the cycle's own run-to-run FP32
-    # differences (LDS-atomic order) amplified by the saddle-point coarse
-    # solve: 20x those, at least 1e-6 (measured 2.8e-7 - 1.3e-6)
-    assert err < (5e-12 if prec == "f64" else max(1e-6, 20 * d_ee))
+    # (test_vcycle_re3900_f64_levels_tight[-1]); measured 6.2e-13 - 1.15e-12.
+    # FP32: the FP32 copies of the two inverses (measured 2.6e-7 - 2.8e-7;
+    # round 4 had to allow 20x the cycle's LDS-atomic run-to-run noise)
+    assert d_ee == 0.0
+    assert err < (5e-12 if prec == "f64" else 1e-6)
 
 
 @pytest.mark.parametrize("coarse", [10, -1])
@@ -342,3 +344,90 @@ print(s.last["n_iterations"])
           f" GMRES {it} vs {it_ref} iterations")
     assert d < max(1e-6, 20 * d_ee)
     assert abs(it - it_ref) <= 1
+
+
+def test_vcycle_deterministic_bitwise():
+    """GLS_DETERMINISTIC (SURVEY §7.2.2's deterministic mode): the brick
+    kernels add a round's cells into the LDS lattice in cell order instead of
+    by LDS atomics, the diagonal and the restriction assemble cell colour by
+    colour instead of by global atomics.  On the headline hierarchy r0..r2
+    (FP32 levels, 10 coarse sweeps): two setups give bitwise the same
+    relaxation factors, repeated V-cycles are bitwise equal, the smoother's
+    deferred shared-node reductions equal a reduction after every apply
+    (GLS_MG_DEFER=0, a child process) BITWISE -- the rebuild reproduces the
+    reduce kernel's arithmetic -- and the FP64 vmult is bitwise repeatable
+    and within 1e-12 of the oracle; the default mode stays within FP32
+    round-off of it."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    import torch
+    import glsamd
+    meshes, cmasks, params, w, u, hist = _hierarchy("input_hoffmann_3D_Re3900.json", 2)
+    pdet = dict(params, deterministic=True)
+    mg, ops = glsamd.build_gmg(meshes, cmasks, pdet, u, hist, w, precision="f32",
+                               coarse_n_iterations=10)
+    om1 = [mg.relaxation(l) for l in range(len(meshes))]
+    mg.setup()
+    om2 = [mg.relaxation(l) for l in range(len(meshes))]
+    assert om1 == om2, (om1, om2)
+    b = gi.rnd(41, meshes[-1].n_dofs)
+
+    def cycle(m):
+        x = torch.zeros(meshes[-1].n_dofs, dtype=torch.float64, device="cuda")
+        m.vcycle(x, torch.from_numpy(b).cuda())
+        torch.cuda.synchronize()
+        return _np(x)
+
+    y1, y2, y3 = cycle(mg), cycle(mg), cycle(mg)
+    assert np.array_equal(y1, y2) and np.array_equal(y1, y3)
+    code = f"""
+import sys, numpy as np, torch
+sys.path[:0] = {sys.path!r}
+import glsamd, glsinputs as gi
+from test_gpu_mg import _hierarchy
+meshes, cmasks, params, w, u, hist = _hierarchy("input_hoffmann_3D_Re3900.json", 2)
+mg, ops = glsamd.build_gmg(meshes, cmasks, dict(params, deterministic=True), u, hist, w,
+                           precision="f32", coarse_n_iterations=10)
+b = gi.rnd(41, meshes[-1].n_dofs)
+x = torch.zeros(meshes[-1].n_dofs, dtype=torch.float64, device="cuda")
+mg.vcycle(x, torch.from_numpy(b).cuda())
+torch.cuda.synchronize()
+np.save(sys.argv[1], x.cpu().numpy())
+"""
+    with tempfile.TemporaryDirectory() as td:
+        f = os.path.join(td, "eager.npy")
+        r = subprocess.run([sys.executable, "-c", code, f], env=dict(os.environ, GLS_MG_DEFER="0"),
+                           capture_output=True, text=True, timeout=180,
+                           cwd=os.path.dirname(__file__))
+        assert r.returncode == 0, r.stderr[-2000:]
+        y_eager = np.load(f)
+    n_diff = int(np.count_nonzero(y_eager != y1))
+    print(f"deterministic: deferred vs per-apply reductions differ in {n_diff} entries")
+    assert n_diff == 0
+    # the default (atomic) mode: within FP32 round-off of the deterministic cycle
+    mgd, _ = glsamd.build_gmg(meshes, cmasks, params, u, hist, w, precision="f32",
+                              coarse_n_iterations=10)
+    d = rel_err(cycle(mgd), y1)
+    print(f"default vs deterministic V-cycle {d:.1e}")
+    assert d < 1e-5
+    # FP64 vmult: bitwise repeatable, oracle parity
+    from helpers import Case
+    c = Case(meshes[-1], cmasks[-1], params, w, 1.0)
+    op = glsamd.NavierStokesOperator(meshes[-1], cmasks[-1], "f64")
+    op.set_parameters(**dict(params, deterministic=True))
+    op.set_linearization_point(u)
+    op.set_previous_solution(hist, w)
+    src = op._dev(c.src)
+    outs = []
+    for _ in range(3):
+        dst = op.initialize_dof_vector()
+        op.vmult(dst, src)
+        torch.cuda.synchronize()
+        outs.append(_np(dst))
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
+    o = c.oracle()
+    o.set_linearization_point(u)
+    o.set_previous_solution(hist, w)
+    assert rel_err(outs[0], o.vmult(c.src)) < 1e-12
