@@ -532,6 +532,59 @@ __global__ void __launch_bounds__(BLOCK, (BrickOcc<dim, k, T, MODE, GEO, ZL>::wa
     }
 }
 
+// Resident smoothing sweeps (mg.hip smooth; FP32 3D levels with deferred
+// reductions whose bricks are all resident at once, csrc/sweeps.hip): the
+// damped-Jacobi steps of one smoothing sequence in ONE launch, one
+// workgroup per brick for all of them.  A workgroup keeps its brick's node
+// ids and the iterate, b and D^{-1} at its lattice nodes in registers across
+// the sweeps.  Between sweeps no kernel boundary and no counter: a brick
+// publishes its shared nodes' partial sums as tagged granules and its
+// neighbours rebuild those nodes as soon as the tags of their slots read
+// the previous sweep.
+struct SweepArgs
+{
+  float          *vec[2];   // sweep j reads vec[j & 1], writes vec[(j + 1) & 1] (last sweep only)
+  float          *slots[2]; // the last sweep's partial slots: slots[j & 1] (plain)
+  uint64_t       *gran[2];  // the other sweeps': gran[j & 1], [slot][component] {value, tag}
+  uint32_t        gran_bytes;
+  uint32_t       *err;      // granule waits that hit the spin bound
+  uint32_t        epoch;    // tags before this launch (sweep j tags epoch + j + 1)
+  int             nsweep;
+  uint64_t       *timing;   // GLS_SWEEP_TIMING builds: [brick][sweep][6] clock stamps
+};
+#ifndef GLS_SWEEP_TIMING
+#define GLS_SWEEP_TIMING 0
+#endif
+constexpr int SWEEP_MAX_MULT = 11;      // bricks per shared node (two groups of 4 + 3)
+constexpr int SWEEP_MAX_L    = 128;     // lattice nodes per brick (a thread pair per node)
+constexpr int SWEEP_SPIN_MAX = 1 << 18; // a slot that never arrives: counted, not waited for
+
+// one node's partial sums as 8-byte {value, tag} granules, two per 16-byte
+// write-through (sc1) store (each 8-byte half is written whole)
+__device__ __forceinline__ void
+store_granules(uint64_t *base, uint32_t bytes, uint32_t slot, uint32_t tag, const float (&u)[4])
+{
+  using U4 = __attribute__((ext_vector_type(4))) unsigned int;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000);
+  const U4   g0   = {__float_as_uint(u[0]), tag, __float_as_uint(u[1]), tag};
+  const U4   g1   = {__float_as_uint(u[2]), tag, __float_as_uint(u[3]), tag};
+  __builtin_amdgcn_raw_buffer_store_b128(g0, rsrc, (int)(slot * 32u), 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(g1, rsrc, (int)(slot * 32u + 16u), 0, 16);
+}
+
+// 3 waves/SIMD (<= 168 VGPRs): the sweep loop keeps its uniform kernel
+// arguments in SGPRs across iterations (SGPR spills go to VGPR lanes); at 4
+// waves the mixed-geometry kernels spilled to scratch.  The levels it runs
+// (a few hundred bricks) fill fewer slots than 3 workgroups per CU give.
+template <int dim, int k, typename T, int MODE, int GEO = GEO_ANY, bool DET = false>
+__global__ void __launch_bounds__(BLOCK, 3)
+  k_brick_sweeps(BrickArgs<T, dim, k + 1> a, SweepArgs sw)
+{
+  constexpr int ZL = 1;
+  constexpr int G  = GEO;
+#include "brick_sweeps.inc"
+}
+
 // Sum the per-brick partials of every brick-boundary node (one contiguous
 // slot run per node); constrained components get the identity row (vmult,
 // operator_ns.cc:719-721) or zero (evaluate_residual's set_zero, :678).
@@ -694,5 +747,11 @@ __global__ void __launch_bounds__(256)
   if (out64)
     out64[(size_t)node * nc + c] = (double)sum;
 }
+
+// resident smoothing sweeps (csrc/sweeps.hip): workgroups resident at once,
+// and one launch over bricks [a.brick_begin, a.brick_end)
+int64_t sweeps_capacity(int mode, int geo, bool det, size_t lds, int device);
+void    launch_sweeps(const BrickArgs<float, 3, 3> &a, const SweepArgs &sw, int mode, int geo,
+                      bool det, size_t lds, hipStream_t s);
 
 } // namespace gls

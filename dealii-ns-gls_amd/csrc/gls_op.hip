@@ -440,6 +440,27 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
             target[(size_t)b * L + i] = SHARED_BIT | (off[s] + fill[s]++);
         }
     }
+  // resident smoothing sweeps (k_brick_sweeps): tagged-granule slot buffers
+  // for operators small enough to be resident (FP32 3D Q2 levels of a few
+  // thousand bricks of at most SWEEP_MAX_L lattice nodes) whose nodes are
+  // shared by at most SWEEP_MAX_MULT bricks
+  {
+    uint32_t max_mult = 0;
+    for (uint32_t node : shared_nodes)
+      max_mult = std::max(max_mult, mult[node]);
+    if (op->prec == GLS_F32 && dim == 3 && k == 2 && nb <= 4096 && n_slot_total > 0 &&
+        L <= SWEEP_MAX_L &&
+        max_mult <= (uint32_t)SWEEP_MAX_MULT && n_slot_total * 32 < (1ull << 31))
+      {
+        for (auto &g : op->d_sweep_gran)
+          {
+            HIP_THROW(hipMalloc(&g, (size_t)n_slot_total * 32));
+            HIP_THROW(hipMemset(g, 0, (size_t)n_slot_total * 32));
+          }
+        HIP_THROW(hipMalloc(&op->d_sweep_err, sizeof(uint32_t)));
+        HIP_THROW(hipMemset(op->d_sweep_err, 0, sizeof(uint32_t)));
+      }
+  }
   const uint32_t slot = (uint32_t)n_slot_total;
   // packed node | cmask for the gather and the reduction
   for (auto &v : bnodes)
@@ -786,6 +807,121 @@ struct Impl
                          dim3(BLOCK), lds, s, a);
   }
 
+  // the brick kernels' arguments for one apply (dst, src; rx: the fused
+  // relaxation / deferred reduction), bricks [0, 0)
+  static BrickArgs<T, dim, n>
+  brick_args(const glsOp_ *op, int mode, void *dst, const void *src, const RelaxStep *rx)
+  {
+    BrickArgs<T, dim, n> a;
+    a.brick_nodes   = op->d_brick_nodes;
+    a.brick_target  = op->d_brick_target;
+    a.brick_geo     = op->d_brick_geo;
+    a.brick_cell0   = op->d_brick_cell0;
+    a.brick_chunk0  = op->d_brick_chunk0;
+    a.tab_v         = (const typename Pack<T>::V *)op->d_tab;
+    a.geo_cart      = (const T *)op->d_bgeo_cart; // cell-indexed
+    a.geo_gen       = (const T *)op->d_bgeo_gen;  // cell-indexed
+    a.n_cells       = op->n_cells;
+    a.cellwise      = (const T *)op->d_cellwise;
+    a.old_grad      = (const T *)op->d_old_grad;
+    a.dst           = (T *)dst;
+    a.src           = (const T *)src;
+    a.partial       = (T *)(rx && rx->partial ? rx->partial : op->d_partial);
+    a.rb            = rx ? (const T *)rx->b : nullptr;
+    a.rd            = rx ? (const T *)rx->d : nullptr;
+    a.romega        = rx ? (T)rx->omega : T(0);
+    a.rkeep         = rx ? (rx->keep ? 1 : 0) : 1;
+    a.qslots        = rx ? (const T *)rx->prev_partial : nullptr;
+    a.qprev         = rx ? (const T *)rx->prev_src : nullptr;
+    a.qb            = rx ? (const T *)rx->prev_b : nullptr;
+    a.qd            = rx ? (const T *)rx->prev_d : nullptr;
+    a.qomega        = rx ? (T)rx->prev_omega : T(0);
+    a.qsrc_w        = (T *)src;
+    a.out64         = rx ? rx->out64 : nullptr;
+    if (a.out64 && (sizeof(T) != 4 || op->reduce_classes.n == 0 || mode == MODE_RESIDUAL))
+      throw std::runtime_error("fused FP64 output: FP32 brick operators with class reductions");
+    a.rc            = op->reduce_classes;
+    if (a.qslots && !(sizeof(T) == 4 && dim == 3 && op->reduce_classes.n > 0))
+      throw std::runtime_error("deferred shared-node reduction: FP32 3D brick levels only");
+    a.brick_begin   = 0;
+    a.brick_end     = 0;
+    a.bx            = op->bx;
+    a.by            = op->by;
+    a.bz            = op->bz;
+    a.L             = op->L;
+    a.Lx            = op->Lx;
+    a.Ly            = op->Ly;
+    // LDS lattice strides of 3D Q2 bricks of 4x4 cells in x, y (9 x 9
+    // nodes per layer): the widest padding the kernel's LDS budget takes
+    // at its occupancy (160 KB / workgroups per CU, one wave per SIMD
+    // each): 11 x 12 -- the x-sweep's ds_read_b128 conflict-free and the
+    // lattice accumulation's ds_add_f64 at 7 instead of 12 LDS cycles
+    // (bank model of MI355X_MICROARCH §LDS, scripts/lds_layout_search.py
+    // --lattice) -- else 9 x 11 (the 4-wave FP64 kernels: reads 5 / adds 7
+    // cycles, 297 of the 328 lattice positions their 40 KB allow), else
+    // unpadded (reads 8 / adds 12)
+    auto set_lattice = [&]() {
+      const bool four  = sizeof(T) == 8 && mode != MODE_RESIDUAL && dim == 3 && k == 2 &&
+                        op->L == 243; // BrickOcc<...>::four
+      const int  waves = four || sizeof(T) == 4 ? 4 : 3;
+      const int  nz    = op->L / (op->Lx * op->Ly);
+      const size_t budget = (size_t)160 * 1024 / waves;
+      a.PLx = op->Lx, a.PLy = op->Ly;
+      if (dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9)
+        {
+          static constexpr int pads[2][2] = {{11, 12}, {9, 11}};
+          for (const auto &pl : pads)
+            if (BrickLDS<dim, k, T>::bytes(pl[0] * pl[1] * nz) <= budget)
+              {
+                a.PLx = pl[0], a.PLy = pl[1];
+                break;
+              }
+        }
+      a.LP = a.PLx * a.PLy * nz;
+    };
+    set_lattice();
+    a.nu            = (T)op->prm.nu;
+    a.w0            = (T)op->prm.w0;
+    a.theta         = (T)op->prm.theta;
+    a.stau          = (T)(op->prm.dt == 0.0 ? 0.0 : 1.0 / op->prm.dt);
+    a.nu4           = T(4) * a.nu;
+    a.stau2         = a.stau * a.stau;
+    a.td            = ((op->prm.flags & GLS_CONSIDER_TIME_DERIVATIVE) && op->prm.order > 0);
+    a.cw            = (op->prm.flags & GLS_CELL_WISE_STAB) ? 1 : 0;
+    a.have_prev     = op->have_prev ? 1 : 0;
+    a.have_old_grad = (op->have_old_grad && op->prm.theta != 1.0) ? 1 : 0;
+    a.det           = (op->prm.flags & GLS_DETERMINISTIC) ? 1 : 0;
+    a.sh            = make_shape<T, n>(op->basis);
+    return a;
+  }
+
+  // T1 (Fields::T1) from the current tables and time weights, before a
+  // Newton brick apply
+  static void
+  ensure_t1(const glsOp_ *op, const BrickArgs<T, dim, n> &a, hipStream_t s)
+  {
+    if (!op->t1_valid || op->t1_w0 != op->prm.w0 || op->t1_td != a.td)
+      {
+        const int64_t nqc = op->n_cells * nq;
+        if (nqc > 0)
+          hipLaunchKernelGGL((k_finalize_t1<dim, T>), dim3((unsigned)((nqc + 255) / 256)),
+                             dim3(256), 0, s, (T *)op->d_tab, op->d_tab_cbase, op->tab_gs,
+                             op->n_cells, nq, (T)op->prm.w0, a.td);
+        HIP_THROW(hipGetLastError());
+        op->t1_valid = true;
+        op->t1_w0    = op->prm.w0;
+        op->t1_td    = a.td;
+      }
+  }
+
+  static int
+  brick_geo(const glsOp_ *op)
+  {
+    return op->n_curved_bricks == 0            ? GEO_CART :
+           op->n_curved_bricks == op->n_bricks ? GEO_GEN :
+                                                 GEO_ANY;
+  }
+
   // brick kernel over work units [b0, b1) (what & BRICK_RUN) and the
   // shared-node reduction (what & BRICK_REDUCE); both over all units: dst
   // fully (over)written
@@ -795,110 +931,16 @@ struct Impl
   {
     if constexpr (BrickLattice<dim, k>::fits)
       {
-        BrickArgs<T, dim, n> a;
-        a.brick_nodes   = op->d_brick_nodes;
-        a.brick_target  = op->d_brick_target;
-        a.brick_geo     = op->d_brick_geo;
-        a.brick_cell0   = op->d_brick_cell0;
-        a.brick_chunk0  = op->d_brick_chunk0;
-        a.tab_v         = (const typename Pack<T>::V *)op->d_tab;
-        a.geo_cart      = (const T *)op->d_bgeo_cart; // cell-indexed
-        a.geo_gen       = (const T *)op->d_bgeo_gen;  // cell-indexed
-        a.n_cells       = op->n_cells;
-        a.cellwise      = (const T *)op->d_cellwise;
-        a.old_grad      = (const T *)op->d_old_grad;
-        a.dst           = (T *)dst;
-        a.src           = (const T *)src;
-        a.partial       = (T *)(rx && rx->partial ? rx->partial : op->d_partial);
-        a.rb            = rx ? (const T *)rx->b : nullptr;
-        a.rd            = rx ? (const T *)rx->d : nullptr;
-        a.romega        = rx ? (T)rx->omega : T(0);
-        a.rkeep         = rx ? (rx->keep ? 1 : 0) : 1;
-        a.qslots        = rx ? (const T *)rx->prev_partial : nullptr;
-        a.qprev         = rx ? (const T *)rx->prev_src : nullptr;
-        a.qb            = rx ? (const T *)rx->prev_b : nullptr;
-        a.qd            = rx ? (const T *)rx->prev_d : nullptr;
-        a.qomega        = rx ? (T)rx->prev_omega : T(0);
-        a.qsrc_w        = (T *)src;
-        a.out64         = rx ? rx->out64 : nullptr;
-        if (a.out64 && (sizeof(T) != 4 || op->reduce_classes.n == 0 || mode == MODE_RESIDUAL))
-          throw std::runtime_error("fused FP64 output: FP32 brick operators with class reductions");
-        a.rc            = op->reduce_classes;
-        if (a.qslots && !(sizeof(T) == 4 && dim == 3 && op->reduce_classes.n > 0))
-          throw std::runtime_error("deferred shared-node reduction: FP32 3D brick levels only");
+        BrickArgs<T, dim, n> a = brick_args(op, mode, dst, src, rx);
         if (rx && rx->defer)
           what &= ~BRICK_REDUCE;
-        a.brick_begin   = b0;
-        a.brick_end     = b1;
-        a.bx            = op->bx;
-        a.by            = op->by;
-        a.bz            = op->bz;
-        a.L             = op->L;
-        a.Lx            = op->Lx;
-        a.Ly            = op->Ly;
-        // LDS lattice strides of 3D Q2 bricks of 4x4 cells in x, y (9 x 9
-        // nodes per layer): the widest padding the kernel's LDS budget takes
-        // at its occupancy (160 KB / workgroups per CU, one wave per SIMD
-        // each): 11 x 12 -- the x-sweep's ds_read_b128 conflict-free and the
-        // lattice accumulation's ds_add_f64 at 7 instead of 12 LDS cycles
-        // (bank model of MI355X_MICROARCH §LDS, scripts/lds_layout_search.py
-        // --lattice) -- else 9 x 11 (the 4-wave FP64 kernels: reads 5 / adds 7
-        // cycles, 297 of the 328 lattice positions their 40 KB allow), else
-        // unpadded (reads 8 / adds 12)
-        auto set_lattice = [&](bool) {
-          const bool four  = sizeof(T) == 8 && mode != MODE_RESIDUAL && dim == 3 && k == 2 &&
-                            op->L == 243; // BrickOcc<...>::four
-          const int  waves = four || sizeof(T) == 4 ? 4 : 3;
-          const int  nz    = op->L / (op->Lx * op->Ly);
-          const size_t budget = (size_t)160 * 1024 / waves;
-          a.PLx = op->Lx, a.PLy = op->Ly;
-          if (dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9)
-            {
-              static constexpr int pads[2][2] = {{11, 12}, {9, 11}};
-              for (const auto &pl : pads)
-                if (BrickLDS<dim, k, T>::bytes(pl[0] * pl[1] * nz) <= budget)
-                  {
-                    a.PLx = pl[0], a.PLy = pl[1];
-                    break;
-                  }
-            }
-          a.LP = a.PLx * a.PLy * nz;
-        };
-        set_lattice(false);
-        a.nu            = (T)op->prm.nu;
-        a.w0            = (T)op->prm.w0;
-        a.theta         = (T)op->prm.theta;
-        a.stau          = (T)(op->prm.dt == 0.0 ? 0.0 : 1.0 / op->prm.dt);
-        a.nu4           = T(4) * a.nu;
-        a.stau2         = a.stau * a.stau;
-        a.td            = ((op->prm.flags & GLS_CONSIDER_TIME_DERIVATIVE) && op->prm.order > 0);
-        a.cw            = (op->prm.flags & GLS_CELL_WISE_STAB) ? 1 : 0;
-        a.have_prev     = op->have_prev ? 1 : 0;
-        a.have_old_grad = (op->have_old_grad && op->prm.theta != 1.0) ? 1 : 0;
-        a.det           = (op->prm.flags & GLS_DETERMINISTIC) ? 1 : 0;
-        a.sh            = make_shape<T, n>(op->basis);
+        a.brick_begin = b0;
+        a.brick_end   = b1;
         if ((what & BRICK_RUN) && b1 > b0 && mode == MODE_NEWTON)
-          {
-            // T1 (Fields::T1) from the current tables and time weights
-            if (!op->t1_valid || op->t1_w0 != op->prm.w0 || op->t1_td != a.td)
-              {
-                const int64_t nqc = op->n_cells * nq;
-                if (nqc > 0)
-                  hipLaunchKernelGGL((k_finalize_t1<dim, T>), dim3((unsigned)((nqc + 255) / 256)),
-                                     dim3(256), 0, s, (T *)op->d_tab, op->d_tab_cbase,
-                                     op->tab_gs, op->n_cells, nq, (T)op->prm.w0, a.td);
-                HIP_THROW(hipGetLastError());
-                op->t1_valid = true;
-                op->t1_w0    = op->prm.w0;
-                op->t1_td    = a.td;
-              }
-          }
+          ensure_t1(op, a, s);
         if ((what & BRICK_RUN) && b1 > b0)
           {
-            const int geo = op->n_curved_bricks == 0            ? GEO_CART :
-                            op->n_curved_bricks == op->n_bricks ? GEO_GEN :
-                                                                  GEO_ANY;
-            set_lattice(geo != GEO_CART);
+            const int    geo = brick_geo(op);
             const size_t lds = BrickLDS<dim, k, T>::bytes(a.LP);
             if (mode == MODE_NEWTON)
               launch_brick<MODE_NEWTON>(b1 - b0, lds, geo, s, a);
@@ -1194,6 +1236,73 @@ int
 op_vmult_mode(const glsOp_ *op)
 {
   return vmult_mode(op);
+}
+
+bool
+brick_sweeps(const glsOp_ *op, int mode, void *v0, void *v1, void *slots0, void *slots1,
+             int nsweep, const RelaxStep &rx, hipStream_t s)
+{
+  using I = Impl<3, 2, float>;
+  if (nsweep < 2 || !op->d_sweep_gran[0] || !deferred_reduce_ok(op) || op->degree != 2 ||
+      op->L > SWEEP_MAX_L || !rx.b || (mode != MODE_NEWTON && mode != MODE_FIXED))
+    return false;
+  RelaxStep r     = rx;
+  r.partial       = slots0;
+  r.prev_partial  = nullptr;
+  r.defer         = true;
+  auto      a     = I::brick_args(op, mode, v1, v0, &r);
+  a.brick_begin   = 0;
+  a.brick_end     = op->n_bricks;
+  const int    geo = I::brick_geo(op);
+  const bool   det = a.det != 0;
+  const size_t lds = BrickLDS<3, 2, float>::bytes(a.LP);
+  // every brick resident at once (a brick waits for its neighbours)
+  int64_t &cap = op->sweep_cap[mode == MODE_NEWTON ? 1 : 0][geo][det ? 1 : 0];
+  if (cap < 0)
+    cap = sweeps_capacity(mode, geo, det, lds, op->device);
+  if (op->n_bricks > cap)
+    return false;
+  if (mode == MODE_NEWTON)
+    I::ensure_t1(op, a, s);
+  SweepArgs sw;
+  sw.vec[0]     = (float *)v0;
+  sw.vec[1]     = (float *)v1;
+  sw.slots[0]   = (float *)slots0;
+  sw.slots[1]   = (float *)slots1;
+  sw.gran[0]    = op->d_sweep_gran[0];
+  sw.gran[1]    = op->d_sweep_gran[1];
+  sw.gran_bytes = (uint32_t)((uint64_t)op->n_slots * 32u);
+  sw.err        = op->d_sweep_err;
+  sw.epoch      = op->sweep_epoch;
+  sw.nsweep     = nsweep;
+  sw.timing     = nullptr;
+#if GLS_SWEEP_TIMING
+  // timing builds: per-phase clock stamps of every launch appended to the
+  // file $GLS_SWEEP_TIMING_OUT (header n_bricks, nsweep; then the stamps)
+  static uint64_t *d_tim = nullptr;
+  const size_t     nst   = (size_t)op->n_bricks * nsweep * 6;
+  if (!d_tim)
+    HIP_THROW(hipMalloc(&d_tim, (size_t)4096 * 64 * 6 * sizeof(uint64_t)));
+  sw.timing = nst <= (size_t)4096 * 64 * 6 ? d_tim : nullptr;
+#endif
+  launch_sweeps(a, sw, mode, geo, det, lds, s);
+#if GLS_SWEEP_TIMING
+  if (const char *fn = getenv("GLS_SWEEP_TIMING_OUT"); fn && sw.timing)
+    {
+      std::vector<uint64_t> h(nst + 2);
+      h[0] = (uint64_t)op->n_bricks, h[1] = (uint64_t)nsweep;
+      HIP_THROW(hipStreamSynchronize(s));
+      HIP_THROW(hipMemcpy(h.data() + 2, d_tim, nst * sizeof(uint64_t), hipMemcpyDeviceToHost));
+      if (FILE *f = fopen(fn, "ab"))
+        {
+          fwrite(h.data(), sizeof(uint64_t), h.size(), f);
+          fclose(f);
+        }
+    }
+#endif
+  op->sweep_epoch += (uint32_t)(nsweep - 1);
+  op->sweep_launches++;
+  return true;
 }
 } // namespace gls
 
@@ -1805,7 +1914,8 @@ gls_op_destroy(glsOp op)
                   op->d_shared_index, op->d_partial,      op->d_bgeo_cart,    op->d_bgeo_gen,
                   op->d_brick_geo,    op->d_brick_cell0,  op->d_brick_chunk0, op->d_tab_cbase,
                   op->d_node_cmask,   op->d_inhom,        op->gmres_ws,
-                  op->d_colour_cells};
+                  op->d_colour_cells, op->d_sweep_gran[0], op->d_sweep_gran[1],
+                  op->d_sweep_err};
   for (void *b : bufs)
     if (b)
       (void)hipFree(b);
@@ -2570,6 +2680,23 @@ gls_op_brick_shape(glsOp op, int *dims)
   dims[0] = op->use_brick ? op->bx : 0;
   dims[1] = op->use_brick ? op->by : 0;
   dims[2] = op->use_brick ? op->bz : 0;
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_sweep_stats(glsOp op, uint64_t *launches, uint64_t *timeouts)
+{
+  GLS_TRY
+  if (!op || !launches || !timeouts)
+    throw std::runtime_error("gls_op_sweep_stats: null argument");
+  uint32_t h = 0;
+  if (op->d_sweep_err)
+    {
+      HIP_THROW(hipDeviceSynchronize());
+      HIP_THROW(hipMemcpy(&h, op->d_sweep_err, sizeof(h), hipMemcpyDeviceToHost));
+    }
+  *launches = op->sweep_launches;
+  *timeouts = h;
   GLS_CATCH
 }
 

@@ -865,6 +865,19 @@ defer_reduce(const glsMG_ *mg, int level)
          mg->qslot[0][(size_t)level];
 }
 
+// deferred smoothing sequences in one resident launch (k_brick_sweeps) where
+// the level qualifies: GLS_MG_DEFER unset or >= 2; 1 keeps one launch per
+// step (with deferred reductions), 0 reduces after every step
+bool
+defer_resident()
+{
+  static const bool on = [] {
+    const char *e = getenv("GLS_MG_DEFER");
+    return !e || std::atoi(e) >= 2;
+  }();
+  return on;
+}
+
 // PreconditionRelaxation::vmult (zero start) / step, `iters` iterations;
 // the result in x.  x_in (step only): the starting iterate is in tmp[level]
 // instead of x (the multigrid's out-of-place prolongation put it there).
@@ -933,6 +946,25 @@ smooth(const glsMG_ *mg, int level, void *x, const void *b, bool zero_start, int
   if (!defer || pend || it >= iters)
     out64 = nullptr;
   PendingReduce pr;
+  // the steps in one resident launch (k_brick_sweeps) where the level
+  // qualifies; the same iterates as the per-step launches below
+  if (defer && defer_resident() && iters - it >= 2)
+    {
+      void          *oth = cur == x ? tmp : x;
+      void          *s0  = mg->qslot[it % 2][(size_t)level];
+      void          *s1  = mg->qslot[(it + 1) % 2][(size_t)level];
+      gls::RelaxStep r   = rx;
+      r.out64            = out64;
+      const int      ns  = iters - it;
+      if (gls::brick_sweeps(op, gls::op_vmult_mode(op), cur, oth, s0, s1, ns, r, s))
+        {
+          // the last sweep (ns - 1) read v[(ns - 1) % 2] and wrote the other
+          const bool even = (ns - 1) % 2 == 0;
+          pr  = PendingReduce{even ? s0 : s1, even ? cur : oth, rx.b, rx.d, rx.omega, true};
+          cur = even ? oth : cur;
+          it  = iters;
+        }
+    }
   for (; it < iters; ++it)
     {
       void          *oth = cur == x ? tmp : x;

@@ -154,6 +154,17 @@ struct glsOp_
   int64_t  *d_tab_cbase = nullptr;
   int64_t   tab_gs = 0, tab_elems = 0;
   std::vector<uint32_t> brick_cell0, brick_ncell;
+  // resident smoothing sweeps (brick.h k_brick_sweeps; FP32 3D operators with
+  // few bricks): two tagged-granule slot buffers ([slot][4] {value, tag}),
+  // the waits that hit the spin bound, the last tag used (tags grow across
+  // launches; launches on one operator are stream-ordered) and the resident
+  // capacity per instantiation [Newton][geometry][deterministic] (-1: not
+  // asked yet)
+  uint64_t        *d_sweep_gran[2] = {nullptr, nullptr};
+  uint32_t        *d_sweep_err     = nullptr;
+  mutable uint32_t sweep_epoch     = 0;
+  mutable uint64_t sweep_launches  = 0;
+  mutable int64_t  sweep_cap[2][3][2] = {{{-1, -1}, {-1, -1}, {-1, -1}}, {{-1, -1}, {-1, -1}, {-1, -1}}};
 
   size_t
   tsize() const
@@ -234,6 +245,14 @@ deferred_reduce_ok(const glsOp_ *op)
 void brick_launch(const glsOp_ *op, int mode, void *dst, const void *src, int64_t b0,
                   int64_t b1, int what, hipStream_t s, const RelaxStep *rx = nullptr);
 int  op_vmult_mode(const glsOp_ *op);
+// nsweep >= 2 fused damped-Jacobi steps (rx: b, d, omega, keep, out64 for the
+// last) in one resident launch (k_brick_sweeps): sweep j reads v[j % 2] and
+// writes v[(j + 1) % 2], its partial slots slots[j % 2]; the last sweep's
+// reduction is left pending (its slots, its src) as after a deferred
+// per-launch sequence.  False (nothing launched) where the operator or the
+// device does not qualify: the caller launches the steps one by one.
+bool brick_sweeps(const glsOp_ *op, int mode, void *v0, void *v1, void *slots0, void *slots1,
+                  int nsweep, const RelaxStep &rx, hipStream_t s);
 // one V-cycle on node-major device vectors of the multigrid's outer
 // precision (gls_mg_vcycle without the caller-layout staging; GMRES calls it)
 void mg_vcycle_device(glsMG mg, void *dst, const void *src, hipStream_t s);

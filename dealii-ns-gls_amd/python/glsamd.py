@@ -36,7 +36,7 @@ EXPORTS = [
     "gls_dist_vmult_group", "gls_dist_interior_bricks", "gls_op_set_vector_layout",
     "gls_op_get_max_u", "gls_mg_set_vector_layout", "gls_dist_update_ghost_values",
     "gls_dist_get_max_u", "gls_op_compute_diagonal", "gls_op_invert_diagonal", "gls_mg_relax",
-    "gls_dist_compress_add", "gls_op_brick_shape", "gls_op_cell_permutation",
+    "gls_dist_compress_add", "gls_op_brick_shape", "gls_op_sweep_stats", "gls_op_cell_permutation",
     "gls_discover_bricks", "gls_mg_coarse_statistics", "gls_mg_coarse_setup_times",
     "gls_amg_create", "gls_amg_destroy", "gls_amg_vmult", "gls_amg_info", "gls_mg_coarse_amg",
     "gls_amg_level_matrix",
@@ -175,6 +175,7 @@ def lib():
         L.gls_mg_relax.argtypes = [vp, C.c_int, vp, vp, vp, vp, C.c_double, C.c_int, vp]
         L.gls_dist_compress_add.argtypes = [vp, vp, vp]
         L.gls_op_brick_shape.argtypes = [vp, vp]
+        L.gls_op_sweep_stats.argtypes = [vp, vp, vp]
         L.gls_op_cell_permutation.argtypes = [vp, vp]
         L.gls_op_element_matrices.argtypes = [vp, vp]
         L.gls_op_system_matrix.argtypes = [vp, C.POINTER(i64), vp, vp, vp]
@@ -368,6 +369,13 @@ class NavierStokesOperator:
         p = np.empty(self.n_cells, dtype=np.int64)
         _check(lib().gls_op_cell_permutation(self.h, p.ctypes.data))
         return p
+
+    def sweep_stats(self):
+        """(resident smoothing launches, slot waits that hit their spin
+        bound) on this multigrid level (gls_op_sweep_stats)."""
+        n, c = C.c_uint64(0), C.c_uint64(0)
+        _check(lib().gls_op_sweep_stats(self.h, C.byref(n), C.byref(c)))
+        return int(n.value), int(c.value)
 
     def __del__(self):
         try:

@@ -164,6 +164,11 @@ glsStatus gls_op_create(const glsOpDesc *desc, glsOp *out);
  * Only gls_op_vmult_cells ranges refer to the internal order; table
  * upload/download and every vector use the caller's numbering. */
 glsStatus gls_op_brick_shape(glsOp op, int *dims);
+/* Diagnostics of the multigrid's resident smoothing sweeps on this level
+ * operator since its creation: *launches = smoothing
+ * sequences run as one resident launch, *timeouts = slot waits that hit
+ * their spin bound (0 on a healthy device; synchronises the device). */
+glsStatus gls_op_sweep_stats(glsOp op, uint64_t *launches, uint64_t *timeouts);
 /* The discovery gls_op_create runs for brick = {-1,-1,-1}, on its own (host
  * only, no device call): shape = the brick shape found ({0,0,0}: none),
  * perm[internal cell] = caller cell. */

@@ -346,6 +346,92 @@ print(s.last["n_iterations"])
     assert abs(it - it_ref) <= 1
 
 
+def test_vcycle_resident_sweeps():
+    """The resident smoothing sweeps (k_brick_sweeps: a level's smoothing
+    sequence in one launch, bricks waiting only for the bricks they share a
+    node with) against one launch per step (GLS_MG_DEFER=1, a child process)
+    on the headline hierarchy r0..r2 with 10 coarse sweeps: BITWISE equal
+    V-cycles in deterministic mode, also while another stream streams a
+    large copy through the device (uneven load on the hand-offs), and no
+    neighbour wait hit its spin bound; the GMRES iteration count of the
+    default mode within 1 of the per-launch one."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    import torch
+    import glsamd
+    meshes, cmasks, params, w, u, hist = _hierarchy("input_hoffmann_3D_Re3900.json", 2)
+    pdet = dict(params, deterministic=True)
+    mg, ops = glsamd.build_gmg(meshes, cmasks, pdet, u, hist, w, precision="f32",
+                               coarse_n_iterations=10)
+    b = gi.rnd(41, meshes[-1].n_dofs)
+    bd = torch.from_numpy(b).cuda()
+
+    def cycle():
+        x = torch.zeros(meshes[-1].n_dofs, dtype=torch.float64, device="cuda")
+        mg.vcycle(x, bd)
+        torch.cuda.synchronize()
+        return _np(x)
+
+    y1 = cycle()
+    # the same cycles with a 1 GiB device copy running on another stream
+    big = torch.empty(1 << 28, dtype=torch.float32, device="cuda")
+    big2 = torch.empty_like(big)
+    side = torch.cuda.Stream()
+    ys = []
+    for _ in range(4):
+        with torch.cuda.stream(side):
+            big2.copy_(big)
+        ys.append(cycle())
+        torch.cuda.synchronize()
+    del big, big2
+    for y in ys:
+        assert np.array_equal(y, y1)
+    stats = [op.sweep_stats() for op in ops]
+    print("resident launches / spin-bound waits per level:", stats)
+    assert all(s[1] == 0 for s in stats), stats
+    # r0 (coarse sweeps) and r1 (pre- and post-smoothing) ran resident
+    assert stats[0][0] > 0 and stats[1][0] > 0, stats
+    code = f"""
+import sys, numpy as np, torch
+sys.path[:0] = {sys.path!r}
+import glsamd, glsinputs as gi
+from test_gpu_mg import _hierarchy, _re3900_gmg
+meshes, cmasks, params, w, u, hist = _hierarchy("input_hoffmann_3D_Re3900.json", 2)
+mg, ops = glsamd.build_gmg(meshes, cmasks, dict(params, deterministic=True), u, hist, w,
+                           precision="f32", coarse_n_iterations=10)
+b = gi.rnd(41, meshes[-1].n_dofs)
+x = torch.zeros(meshes[-1].n_dofs, dtype=torch.float64, device="cuda")
+mg.vcycle(x, torch.from_numpy(b).cuda())
+np.save(sys.argv[1], x.cpu().numpy())
+meshes, mg, A = _re3900_gmg(10)
+s = glsamd.LinearSolverGMRES(A, mg, relative_tolerance=1e-8, absolute_tolerance=0.0)
+x2 = torch.zeros(meshes[-1].n_dofs, dtype=torch.float64, device="cuda")
+s.solve(x2, torch.from_numpy(b).cuda())
+torch.cuda.synchronize()
+print(s.last["n_iterations"])
+"""
+    with tempfile.TemporaryDirectory() as td:
+        f = os.path.join(td, "launches.npy")
+        r = subprocess.run([sys.executable, "-c", code, f], env=dict(os.environ, GLS_MG_DEFER="1"),
+                           capture_output=True, text=True, timeout=180,
+                           cwd=os.path.dirname(__file__))
+        assert r.returncode == 0, r.stderr[-2000:]
+        y_launch = np.load(f)
+        it_launch = int(r.stdout.strip().splitlines()[-1])
+    n_diff = int(np.count_nonzero(y_launch != y1))
+    meshes2, mg2, A = _re3900_gmg(10)
+    x = torch.zeros(meshes[-1].n_dofs, dtype=torch.float64, device="cuda")
+    s = glsamd.LinearSolverGMRES(A, mg2, relative_tolerance=1e-8, absolute_tolerance=0.0)
+    s.solve(x, bd)
+    it = s.last["n_iterations"]
+    print(f"resident sweeps vs one launch per step: {n_diff} entries differ (deterministic); "
+          f"GMRES {it} vs {it_launch} iterations")
+    assert n_diff == 0
+    assert abs(it - it_launch) <= 1
+
+
 def test_vcycle_deterministic_bitwise():
     """GLS_DETERMINISTIC (SURVEY §7.2.2's deterministic mode): the brick
     kernels add a round's cells into the LDS lattice in cell order instead of
