@@ -934,6 +934,11 @@ struct Impl
         BrickArgs<T, dim, n> a = brick_args(op, mode, dst, src, rx);
         if (rx && rx->defer)
           what &= ~BRICK_REDUCE;
+#ifdef GLS_EXP_NB
+        // timing experiments only (variant builds): the first N bricks
+        if (const char *e = getenv("GLS_EXP_NB"))
+          b1 = std::min<int64_t>(b1, std::atoll(e));
+#endif
         a.brick_begin = b0;
         a.brick_end   = b1;
         if ((what & BRICK_RUN) && b1 > b0 && mode == MODE_NEWTON)
