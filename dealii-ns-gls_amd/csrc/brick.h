@@ -496,9 +496,8 @@ to_packs(const T (&x)[nc], V (&v)[NP])
 template <int dim, int k, typename T, int MODE, int GEO, int ZL = 1>
 struct BrickOcc
 {
-  static constexpr bool four  = sizeof(T) == 8 && dim == 3 && k == 2 && MODE != MODE_RESIDUAL &&
-                               ZL == 1;
-  static constexpr int  waves = four || sizeof(T) == 4 ? 4 : 3;
+  static constexpr bool four  = dim == 3 && k == 2 && MODE != MODE_RESIDUAL && ZL == 1;
+  static constexpr int  waves = four ? (sizeof(T) == 4 ? 5 : 4) : (sizeof(T) == 4 ? 4 : 3);
 };
 
 // DET: the deterministic lattice accumulation (GLS_DETERMINISTIC: the cells
@@ -581,8 +580,25 @@ __global__ void __launch_bounds__(BLOCK, 3)
   k_brick_sweeps(BrickArgs<T, dim, k + 1> a, SweepArgs sw)
 {
   constexpr int ZL = 1;
-  constexpr int G  = GEO;
+  if constexpr (GEO == GEO_ANY && BrickOcc<dim, k, T, MODE, GEO, ZL>::four)
+    {
+      // one body per brick geometry, as k_brick's (the same arithmetic)
+      if (a.brick_geo[(int)a.brick_begin + (int)blockIdx.x] & 1u)
+        {
+          constexpr int G = GEO_GEN;
 #include "brick_sweeps.inc"
+        }
+      else
+        {
+          constexpr int G = GEO_CART;
+#include "brick_sweeps.inc"
+        }
+    }
+  else
+    {
+      constexpr int G = GEO;
+#include "brick_sweeps.inc"
+    }
 }
 
 // Sum the per-brick partials of every brick-boundary node (one contiguous

@@ -861,9 +861,9 @@ struct Impl
     // cycles, 297 of the 328 lattice positions their 40 KB allow), else
     // unpadded (reads 8 / adds 12)
     auto set_lattice = [&]() {
-      const bool four  = sizeof(T) == 8 && mode != MODE_RESIDUAL && dim == 3 && k == 2 &&
-                        op->L == 243; // BrickOcc<...>::four
-      const int  waves = four || sizeof(T) == 4 ? 4 : 3;
+      const bool four  = mode != MODE_RESIDUAL && dim == 3 && k == 2 &&
+                        op->L <= 243; // BrickOcc<...>::four (one-layer bricks)
+      const int  waves = four ? (sizeof(T) == 4 ? 5 : 4) : (sizeof(T) == 4 ? 4 : 3);
       const int  nz    = op->L / (op->Lx * op->Ly);
       const size_t budget = (size_t)160 * 1024 / waves;
       a.PLx = op->Lx, a.PLy = op->Ly;
