@@ -157,26 +157,23 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
   // 4 waves x 2 cells instead of a 4-cell layer with two idle waves
   // 3D Q2 operators with many bricks: 4x4x2 bricks, 32 cells and 4 rounds
   // per workgroup (fewer shared nodes per cell, half the partial slots; the
-  // relaxation operands read at the write-out).  They pay where the launch
-  // runs several dispatch generations of the FP32 kernel (4 workgroups per
-  // CU): Re3900 r3 173 -> 162 us per FP32 vmult, but r2 (800 two-layer
-  // bricks, one generation of 4-round lives) 26.8 -> 29.5 us
-  // (profiles/r04/explore/ab_two_layer.txt).  Default: at least 4 generations
-  // of two-layer bricks; GLS_TWO_LAYER=0 / 1 forces them off / on.
-  // FP64 likewise on meshes with curved cells (the 3-wave kernels: 168
-  // VGPRs two-layer; the all-Cartesian FP64 kernel keeps its 4 waves with
-  // one-layer bricks), from 4 generations of 3 workgroups per CU
-  bool any_curved = false;
-  for (int64_t c = 0; cell_curved && c < d->n_cells && !any_curved; ++c)
-    any_curved = cell_curved[(size_t)c] != 0;
-  bool two_layer = dim == 3 && k == 2 && (op->prec == GLS_F32 || any_curved) && bx * by == 16 &&
-                   bz % 2 == 0;
+  // relaxation operands read at the write-out), run by the 4-wave FP32 /
+  // 3-wave FP64 two-layer kernels.  Against the one-layer kernels (5 waves
+  // FP32, 4 FP64 since round 5) they pay only on long launches: from 8
+  // generations of the one-layer kernel's slots on (two-layer bricks >= 8 x
+  // its workgroups per CU x CUs) -- the sphere r3 (16,384 two-layer bricks)
+  // 560 -> 530 us FP32, 918 -> 867 us FP64; below it the one-layer bricks
+  // win (Re3900 r3, 6,400: FP32 172 -> 167 us, FP64 288-294 -> 287.5 us; r2
+  // 26.8 -> 29.2 us FP32 with two layers) (profiles/r05/explore/
+  // ab_two_layer_r3.txt, ab_two_layer_r2.txt).  GLS_TWO_LAYER=0 / 1 forces
+  // them off / on.
+  bool two_layer = dim == 3 && k == 2 && bx * by == 16 && bz % 2 == 0;
   if (two_layer)
     {
       const int64_t nb2 = d->n_cells / (2 * bx * by);
-      const int     wgs = op->prec == GLS_F32 ? 4 : 3; // workgroups per CU
+      const int     wgs = op->prec == GLS_F32 ? 5 : 4; // one-layer workgroups per CU
       const int     n_cu = op_cu_count(op);
-      two_layer = n_cu > 0 && nb2 >= 4 * wgs * (int64_t)n_cu;
+      two_layer = n_cu > 0 && nb2 >= 8 * wgs * (int64_t)n_cu;
       if (const char *tl = getenv("GLS_TWO_LAYER"))
         two_layer = tl[0] == '1';
     }

@@ -199,7 +199,7 @@ def test_sphere_r3_partition_balance():
 @pytest.mark.parametrize("world", [2, 4])
 def test_local_group_gpu_two_layer(world, monkeypatch):
     """The partitioned native vmult with two-layer bricks forced
-    (GLS_TWO_LAYER=1: 4x4x2 bricks, the default only from 4 dispatch
+    (GLS_TWO_LAYER=1: 4x4x2 bricks, the default only from 8 dispatch
     generations, e.g. a rank's r3 slab at 2 ranks): interior / boundary
     segments, curved-brick balance and the ghost-row reduce on 32-cell
     bricks, against the single-domain oracle (FP64 1e-12)."""
