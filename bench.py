@@ -255,8 +255,8 @@ def mg_companions(d, params, weights, n_ref, reps=20):
     cm = [m.constraint_mask(vel, p, slip) for m in meshes]
     u = gi.linearization_point(meshes[-1].n_nodes, meshes[-1].dim, d.u_max)
     hist = gi.history(u, params["order"])
-    mg, _ = glsamd.build_gmg(meshes, cm, params, u, hist, weights, precision="f32",
-                             coarse_n_iterations=10)
+    mg, mg_ops = glsamd.build_gmg(meshes, cm, params, u, hist, weights, precision="f32",
+                                  coarse_n_iterations=10)
     setup = []
     for _ in range(5):
         torch.cuda.synchronize()
@@ -303,6 +303,8 @@ def mg_companions(d, params, weights, n_ref, reps=20):
         return float(np.median(times)) * 1e3
 
     vc = vcycles()
+    # resident smoothing launches / spin-bound waits per level (coarsest first)
+    sweeps = [list(op.sweep_stats()) for op in mg_ops]
     # the deck's own coarse solver ("gmg coarse grid solver": "direct",
     # multigrid.cc:448-455): the assembled r0 operator's free-dof block
     # LU-factorised and inverted once in the setup (rocSOLVER getrf/getri),
@@ -379,7 +381,8 @@ def mg_companions(d, params, weights, n_ref, reps=20):
                                                "(20 steps, device reductions), wall"},
             f"r{n_ref}_vcycle_f32_coarse_relax10": {"ms": vc, "levels": n_ref + 1,
                                                     "finest_dofs": meshes[-1].n_dofs,
-                                                    "vcycles_per_s": 1e3 / vc},
+                                                    "vcycles_per_s": 1e3 / vc,
+                                                    "resident_sweeps_launches_timeouts": sweeps},
             f"r{n_ref}_vcycle_f32_coarse_direct_lu": lu,
             f"r{n_ref}_gmres_iteration": {"ms": git,
                                           "note": "V-cycle (coarse: 10 relaxation sweeps) + "
