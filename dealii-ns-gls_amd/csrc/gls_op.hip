@@ -2694,6 +2694,7 @@ gls_op_sweep_stats(glsOp op, uint64_t *launches, uint64_t *timeouts)
   uint32_t h = 0;
   if (op->d_sweep_err)
     {
+      gls::DeviceScope dev(op->device);
       HIP_THROW(hipDeviceSynchronize());
       HIP_THROW(hipMemcpy(&h, op->d_sweep_err, sizeof(h), hipMemcpyDeviceToHost));
     }
