@@ -4,7 +4,7 @@ library and GLS_* switches from the environment; A/B drivers loop over
 them):  python scripts/time_vmult.py input_sphere_amg.json 3 f64 [reps]
 prints "<deck> r<n> <prec> <us per vmult> <DoF/s>"; an optional fifth
 argument "bx,by,bz" forces the brick shape (cells consecutive in the
-mesh order)."""
+mesh order); a sixth argument "det" sets GLS_DETERMINISTIC."""
 import os
 import sys
 
@@ -24,8 +24,11 @@ def main():
     cm = m.constraint_mask(*d.boundary_descriptor())
     prm, w = d.operator_parameters(2.5e-4)
     u = gi.linearization_point(m.n_nodes, m.dim, d.u_max)
-    brick = tuple(int(x) for x in sys.argv[5].split(",")) if len(sys.argv) > 5 else None
+    brick = (tuple(int(x) for x in sys.argv[5].split(","))
+             if len(sys.argv) > 5 and sys.argv[5] != "-" else None)
     op = glsamd.NavierStokesOperator(m, cm, prec, brick=brick)
+    if len(sys.argv) > 6 and sys.argv[6] == "det":
+        prm = dict(prm, deterministic=True)
     op.set_parameters(**prm)
     op.set_linearization_point(u)
     if prm["order"] > 0:
