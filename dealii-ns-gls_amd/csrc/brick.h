@@ -52,6 +52,17 @@ struct BrickLattice
   static constexpr bool fits = L <= 729;
 };
 
+// floor(i / d) for 0 <= i < 4096 and 1 <= d <= 729 from r = 1/d rounded to
+// float: (i + 1/2) / d stays >= 0.5 / 729 away from an integer, more than
+// the product's rounding error (< 4096 * 2^-23), so the truncation is exact.
+// Three VALU operations instead of the ~18 of an integer division by a
+// runtime divisor.
+__device__ __forceinline__ int
+idiv_f(int i, float r)
+{
+  return (int)(((float)i + 0.5f) * r);
+}
+
 // workgroup-scope atomic add on an LDS address (ds_add_f64 / ds_add_f32)
 template <typename T>
 __device__ __forceinline__ void
@@ -124,6 +135,8 @@ struct BrickArgs
   int             bx, by, bz;
   int             L, Lx, Ly;
   int             PLx, PLy, LP; // padded LDS lattice strides / size (>= L)
+  // reciprocals of Lx, Lx Ly, bx, bx by for exact float quotients (idiv_f)
+  float           rLx, rLxy, rbx, rbxy;
   T               nu, w0, theta, stau;
   T               nu4, stau2; // 4 nu, stau^2 (delta_qwise_fast)
   int             td, cw, have_prev, have_old_grad;

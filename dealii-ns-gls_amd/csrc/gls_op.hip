@@ -848,6 +848,10 @@ struct Impl
     a.L             = op->L;
     a.Lx            = op->Lx;
     a.Ly            = op->Ly;
+    a.rLx           = 1.0f / (float)op->Lx;
+    a.rLxy          = 1.0f / (float)(op->Lx * op->Ly);
+    a.rbx           = 1.0f / (float)op->bx;
+    a.rbxy          = 1.0f / (float)(op->bx * op->by);
     // LDS lattice strides of 3D Q2 bricks of 4x4 cells in x, y (9 x 9
     // nodes per layer): the widest padding the kernel's LDS budget takes
     // at its occupancy (160 KB / workgroups per CU, one wave per SIMD
