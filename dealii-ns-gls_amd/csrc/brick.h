@@ -569,7 +569,10 @@ struct SweepArgs
 #endif
 constexpr int SWEEP_MAX_MULT = 11;      // bricks per shared node (two groups of 4 + 3)
 constexpr int SWEEP_MAX_L    = 128;     // lattice nodes per brick (a thread pair per node)
-constexpr int SWEEP_SPIN_MAX = 1 << 18; // a slot that never arrives: counted, not waited for
+#ifndef GLS_SWEEP_SPIN_MAX
+#define GLS_SWEEP_SPIN_MAX (1 << 18)
+#endif
+constexpr int SWEEP_SPIN_MAX = GLS_SWEEP_SPIN_MAX; // a slot that never arrives: counted, not waited for
 
 // one node's partial sums as 8-byte {value, tag} granules, two per 16-byte
 // write-through (sc1) store (each 8-byte half is written whole)
