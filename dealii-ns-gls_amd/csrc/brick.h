@@ -208,23 +208,123 @@ contract_v(const V *in, const T *tab, int pa, int base, int s)
   return contract_c<n>(in, c, base, s);
 }
 
+// x contractions across lanes (3D Q2, round 6).  The lanes of a wavefront
+// hold 18 x-lines of 3 quadrature points (2 cells x 9 lines), five lines per
+// 16-lane DPP row (lane 16 r + 3 s + x; the 16th lane of every row and the
+// last 6 lanes of the wave idle: 54 of 64 busy, as before).  A contraction
+// along x, out(x) = sum_j M[x][j] in(j), then reads the line's other points
+// from the neighbouring lanes by DPP row shifts (row_shr / row_shl by 1 and
+// 2: never across a row, so never across a line's row) instead of from the
+// LDS sweep buffer: five taps k_d = M[x][x+d] (zero where x+d leaves the
+// line), applied in the order d = -2..2, which is the order j = 0..2 of the
+// LDS form -- the same FMA chain, bitwise, since the zero taps add +-0.  The
+// x sweeps of evaluate (from the src lattice), of the collocation gradient,
+// of the Dq^T test-function sweep and of the S^T sweep that feeds the
+// lattice accumulation leave LDS: per round 3 fewer dependent LDS round
+// trips and a quarter fewer LDS instructions.  Measured and NOT adopted
+// (profiles/r06/explore/ab_xline_dpp.txt): the DPP shifts cost what the LDS
+// traffic saved (FP32: 27.3 us at 4 waves, spill-free, against 26.2 us for
+// the LDS sweeps at 5 waves; FP64 needs 3 waves to avoid spills, -7 %), so
+// the kernels are not bound by LDS throughput.  GLS_XDPP_F32 / _F64 = 1
+// build the x-line kernels (parity-tested: tests/test_gpu_parity.py,
+// tests/test_a_gpu_configs.py, 44 passed).
+#ifndef GLS_XDPP_F32
+#define GLS_XDPP_F32 0
+#endif
+#ifndef GLS_XDPP_F64
+#define GLS_XDPP_F64 0
+#endif
+template <int dim, int k, typename T>
+__host__ __device__ constexpr bool
+xdpp()
+{
+  return dim == 3 && k == 2 && (sizeof(T) == 4 ? GLS_XDPP_F32 : GLS_XDPP_F64);
+}
+
+// value of lane + D (D = -2, -1, 1, 2) within the lane's 16-lane row, 0 past
+// the row's ends (DPP row_shr / row_shl, bound_ctrl: zero)
+template <int D>
+__device__ __forceinline__ float
+row_shift(float v)
+{
+  constexpr int ctrl = D < 0 ? 0x110 - D : 0x100 + D;
+  return __builtin_bit_cast(
+    float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), ctrl, 0xF, 0xF, true));
+}
+template <int D>
+__device__ __forceinline__ double
+row_shift(double v)
+{
+  typedef int I2 __attribute__((ext_vector_type(2)));
+  constexpr int ctrl = D < 0 ? 0x110 - D : 0x100 + D;
+  I2            u    = __builtin_bit_cast(I2, v);
+  u.x                = __builtin_amdgcn_update_dpp(0, u.x, ctrl, 0xF, 0xF, true);
+  u.y                = __builtin_amdgcn_update_dpp(0, u.y, ctrl, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, u);
+}
+
+// out(x) = sum_d k[d + 2] v(x + d) over the lane's x-line, every component of
+// a pack; executed by every lane of the wavefront (idle lanes hold finite
+// values: they only ever meet zero taps)
+template <typename T, typename V, int W>
+__device__ __forceinline__ V
+xline(const V &v, const T (&kk)[5])
+{
+  V r;
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+    {
+      T a = kk[0] * row_shift<-2>(v[w]);
+      a += kk[1] * row_shift<-1>(v[w]);
+      a += kk[2] * v[w];
+      a += kk[3] * row_shift<1>(v[w]);
+      a += kk[4] * row_shift<2>(v[w]);
+      r[w] = a;
+    }
+  return r;
+}
+
+// the five taps of table `tab` for a lane at x (LDS rows of 8 values: one
+// ds_read_b128 + one ds_read_b32 for FP32, two b128 + one b64 for FP64)
+constexpr int TAPS = 8;
+template <int n, typename T>
+__device__ __forceinline__ void
+taps5(const T *s_tap, int tab, int x, T (&kk)[5])
+{
+  using V      = typename Pack<T>::V;
+  constexpr int W = Pack<T>::W;
+  const T *row = s_tap + (tab * n + x) * TAPS;
+#pragma unroll
+  for (int g = 0; g < 4 / W; ++g)
+    {
+      const V v = reinterpret_cast<const V *>(row)[g];
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        kk[g * W + w] = v[w];
+    }
+  kk[4] = row[4];
+}
+
 // Sweep-buffer layout of one cell (in packs): point (x, y, z) at
 // x + PY y + PZ z, component pack kp at + kp KS, ping-pong halves A | B,
 // cells WB apart.  3D Q2 is padded (FP64: PY 4, PZ 13, KS 37, WB 151): with the
 // ds_read_b128 lane groups of MI355X_MICROARCH §LDS this takes the sweep
 // reads from 7.0 to 4.3 LDS cycles per instruction (4 = conflict free;
 // exhaustive search over PY, PZ, KS, WB of the exact lane/address map).
-template <int dim, int n, int NP>
+// With the x-line lane map (X) only the y and z sweeps read the buffers:
+// PY 3, PZ 10, KS 29 is conflict free for both precisions in the same model
+// (scripts/lds_layout_search.py --xdpp), 40 % less LDS for FP32.
+template <int dim, int n, int NP, bool X = false>
 struct BufLayout
 {
-  static constexpr bool pad  = dim == 3 && n == 3 && NP == 2;
+  static constexpr bool pad  = dim == 3 && n == 3 && NP == 2 && !X;
   // FP32 (one pack per point): same search, 6.0 -> 4.3 modelled cycles per
   // sweep read (scripts/lds_layout_search.py)
-  static constexpr bool pad1 = dim == 3 && n == 3 && NP == 1;
-  static constexpr int  PY   = pad ? 4 : pad1 ? 3 : n;
-  static constexpr int  PZ   = pad ? 13 : pad1 ? 20 : n * n;
-  static constexpr int  KS   = pad ? 37 : pad1 ? 49 : ipow(n, dim);
-  static constexpr int  WB   = pad ? 151 : pad1 ? 107 : 2 * NP * ipow(n, dim);
+  static constexpr bool pad1 = dim == 3 && n == 3 && NP == 1 && !X;
+  static constexpr int  PY   = X ? 3 : pad ? 4 : pad1 ? 3 : n;
+  static constexpr int  PZ   = X ? 10 : pad ? 13 : pad1 ? 20 : n * n;
+  static constexpr int  KS   = X ? 29 : pad ? 37 : pad1 ? 49 : ipow(n, dim);
+  static constexpr int  WB   = X ? (NP == 1 ? 61 : 125) : pad ? 151 : pad1 ? 107 : 2 * NP * ipow(n, dim);
 };
 
 // dynamic LDS of one workgroup: src lattice packs | sweep buffers |
@@ -238,14 +338,16 @@ struct BrickLDS
   static constexpr int W   = Pack<T>::W;
   static constexpr int NP  = (nc + W - 1) / W;
   static constexpr int CPW = 64 / nq > 0 ? 64 / nq : 1;
-  static constexpr int WB  = BufLayout<dim, n, NP>::WB; // per-cell sweep buffer (packs)
+  static constexpr bool X  = xdpp<dim, k, T>();
+  static constexpr int WB  = BufLayout<dim, n, NP, X>::WB; // per-cell sweep buffer (packs)
   static constexpr int WPB = BLOCK / 64;
   static constexpr int ORG = 64; // cell-origin table entries (cells per brick)
+  static constexpr int NTAP = X ? 4 * n * TAPS : 0; // x-line taps (values)
   static size_t
   bytes(int L) // L: padded LDS lattice size
   {
     return 16 * ((size_t)NP * L + (size_t)WPB * CPW * WB) + tab_offset(L) +
-           sizeof(T) * 4 * n * CoefRow<T, n>::RP + sizeof(int) * ORG;
+           sizeof(T) * (NTAP + 4 * n * CoefRow<T, n>::RP) + sizeof(int) * ORG;
   }
   __host__ __device__ static size_t
   tab_offset(int L) // accumulator bytes (FP64 for both precisions) rounded up to 16
@@ -506,11 +608,22 @@ to_packs(const T (&x)[nc], V (&v)[NP])
 // instantiations (FP64 residual, two-layer bricks, other degrees) keep the
 // earlier prefetch (issued behind the previous round's Dq^T sweeps) at 3
 // waves; the FP32 kernels fit 4 waves with it.
+// (GLS_XD_WAVES_F32 / _F64: the occupancy of the x-line kernels, brick.h
+// xline, for A/B builds)
+#ifndef GLS_XD_WAVES_F32
+#define GLS_XD_WAVES_F32 4
+#endif
+#ifndef GLS_XD_WAVES_F64
+#define GLS_XD_WAVES_F64 3
+#endif
 template <int dim, int k, typename T, int MODE, int GEO, int ZL = 1>
 struct BrickOcc
 {
   static constexpr bool four  = dim == 3 && k == 2 && MODE != MODE_RESIDUAL && ZL == 1;
-  static constexpr int  waves = four ? (sizeof(T) == 4 ? 5 : 4) : (sizeof(T) == 4 ? 4 : 3);
+  static constexpr bool X     = xdpp<dim, k, T>();
+  static constexpr int  waves = four ? (sizeof(T) == 4 ? (X ? GLS_XD_WAVES_F32 : 5) :
+                                                         (X ? GLS_XD_WAVES_F64 : 4)) :
+                                       (sizeof(T) == 4 ? 4 : 3);
 };
 
 // DET: the deterministic lattice accumulation (GLS_DETERMINISTIC: the cells
@@ -560,8 +673,11 @@ struct SweepArgs
   uint64_t       *gran[2];  // the other sweeps': gran[j & 1], [slot][component] {value, tag}
   uint32_t        gran_bytes;
   uint32_t       *err;      // granule waits that hit the spin bound
+  uint32_t       *flag;     // host-mapped word set to 1 on such a wait (the host
+                            // reads it without a synchronisation, gls::sweep_stalled)
   uint32_t        epoch;    // tags before this launch (sweep j tags epoch + j + 1)
   int             nsweep;
+  int             spin_max; // polls of a slot before the wait gives up
   uint64_t       *timing;   // GLS_SWEEP_TIMING builds: [brick][sweep][6] clock stamps
 };
 #ifndef GLS_SWEEP_TIMING
@@ -569,10 +685,8 @@ struct SweepArgs
 #endif
 constexpr int SWEEP_MAX_MULT = 11;      // bricks per shared node (two groups of 4 + 3)
 constexpr int SWEEP_MAX_L    = 128;     // lattice nodes per brick (a thread pair per node)
-#ifndef GLS_SWEEP_SPIN_MAX
-#define GLS_SWEEP_SPIN_MAX (1 << 18)
-#endif
-constexpr int SWEEP_SPIN_MAX = GLS_SWEEP_SPIN_MAX; // a slot that never arrives: counted, not waited for
+// a slot that never arrives: counted, not waited for (SweepArgs.spin_max,
+// by default SWEEP_SPIN_MAX_DEFAULT of common.h; gls_op_set_sweep_spin_bound)
 
 // one node's partial sums as 8-byte {value, tag} granules, two per 16-byte
 // write-through (sc1) store (each 8-byte half is written whole)

@@ -364,6 +364,194 @@ __global__ void __launch_bounds__(256)
     part[(size_t)blockIdx.x * DCGS_W] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// ---- wide forms of the two DCGS2 basis passes (round 6): 512-thread
+// blocks (8 waves; CGS_BLOCKS of them, the partial layout of k_dcgs_dots /
+// k_dcgs_update, so k_dcgs_finish is unchanged) and 16-byte loads, a lane
+// holding two consecutive rows.  Valid for an even row count and leading
+// dimension (16-byte aligned columns); krylov.hip takes the narrow forms
+// otherwise.
+constexpr int DCGS_WIDE = 512;
+
+// rows [r0, r1) of block b, r0 even
+__device__ __forceinline__ void
+dcgs_rows(int64_t n, int64_t &r0, int64_t &r1)
+{
+  const int64_t per = (((n + CGS_BLOCKS - 1) / CGS_BLOCKS) + 1) & ~(int64_t)1;
+  r0                = blockIdx.x * per;
+  r1                = r0 + per < n ? r0 + per : n;
+}
+
+// pass 1 (k_dcgs_dots): wave v of the block owns the columns c = v + 8 k
+// (k < 4) and keeps only their 2 x 4 accumulators (the narrow form kept all
+// 64 in every thread: 2 waves per SIMD); every wave streams u and w over
+// the block's rows (the other waves' re-reads hit the L2), so the basis is
+// read once, in 16-byte loads.  Each column's block sum comes from one wave:
+// no cross-wave reduction; u.u and u.w from wave 0.
+__global__ void __launch_bounds__(DCGS_WIDE)
+  k_dcgs_dots_wide(const double *__restrict__ V, int J, const double *__restrict__ u,
+                   const double *__restrict__ w, double *__restrict__ part, int64_t n, int64_t ld)
+{
+  using D2       = __attribute__((ext_vector_type(2))) double;
+  const int wv   = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int NW = DCGS_WIDE / 64, NK = CGS_MAXJ / NW;
+  double    as[NK], az[NK], b = 0, g = 0;
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+    as[k] = az[k] = 0;
+  int64_t r0, r1;
+  dcgs_rows(n, r0, r1);
+  for (int64_t i = r0 + 2 * lane; i < r1; i += 128)
+    {
+      const D2 u2 = *reinterpret_cast<const D2 *>(u + i);
+      const D2 w2 = w ? *reinterpret_cast<const D2 *>(w + i) : D2{0.0, 0.0};
+      D2       v2[NK];
+#pragma unroll
+      for (int k = 0; k < NK; ++k)
+        {
+          const int c = wv + NW * k;
+          v2[k]       = c < J ? *reinterpret_cast<const D2 *>(V + (size_t)c * ld + i) : D2{0.0, 0.0};
+        }
+#pragma unroll
+      for (int k = 0; k < NK; ++k)
+        {
+          as[k] += v2[k][0] * u2[0];
+          as[k] += v2[k][1] * u2[1];
+          az[k] += v2[k][0] * w2[0];
+          az[k] += v2[k][1] * w2[1];
+        }
+      if (wv == 0)
+        {
+          b += u2[0] * u2[0];
+          b += u2[1] * u2[1];
+          g += u2[0] * w2[0];
+          g += u2[1] * w2[1];
+        }
+    }
+  double *pb = part + (size_t)blockIdx.x * DCGS_W;
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+    {
+      const int c = wv + NW * k;
+      if (c >= J)
+        continue; // wave-uniform
+      double xs = as[k], xz = az[k];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1)
+        {
+          xs += __shfl_down(xs, off);
+          xz += __shfl_down(xz, off);
+        }
+      if (lane == 0)
+        {
+          pb[c]            = xs;
+          pb[CGS_MAXJ + c] = xz;
+        }
+    }
+  if (wv == 0)
+    {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1)
+        {
+          b += __shfl_down(b, off);
+          g += __shfl_down(g, off);
+        }
+      if (lane == 0)
+        {
+          pb[2 * CGS_MAXJ]     = b;
+          pb[2 * CGS_MAXJ + 1] = g;
+        }
+    }
+}
+
+// pass 2 (k_dcgs_update), wide: the step's coefficients s, z in LDS (one
+// broadcast ds_read_b128 per column instead of 64 registers), rows
+// interleaved over the 8 waves in 16-byte pairs, columns in groups of 8
+// loads in flight
+__global__ void __launch_bounds__(DCGS_WIDE)
+  k_dcgs_update_wide(const double *__restrict__ V, int J, double *__restrict__ d, double *q,
+                     const double *__restrict__ w, double *__restrict__ un,
+                     double *__restrict__ part, int64_t n, int64_t ld)
+{
+  using D2 = __attribute__((ext_vector_type(2))) double;
+  __shared__ D2     coef[CGS_MAXJ]; // {s_c, z_c}
+  __shared__ double red[DCGS_WIDE / 64];
+  __shared__ double scal[3];        // 1 / alpha, h_jj
+  if (threadIdx.x < CGS_MAXJ)
+    {
+      const int c    = threadIdx.x;
+      coef[c]        = c < J ? D2{d[c], d[CGS_MAXJ + c]} : D2{0.0, 0.0};
+    }
+  if (threadIdx.x == 0)
+    {
+      // the same arithmetic (and order) as k_dcgs_update
+      double s2 = 0, sz = 0;
+      for (int c = 0; c < CGS_MAXJ; ++c)
+        {
+          const double sc = c < J ? d[c] : 0.0, zc = c < J ? d[CGS_MAXJ + c] : 0.0;
+          s2 += sc * sc;
+          sz += sc * zc;
+        }
+      const double a2    = d[2 * CGS_MAXJ] - s2;
+      const double alpha = sqrt(a2 > 0 ? a2 : 0.0);
+      const double ia    = alpha > 0 ? 1.0 / alpha : 0.0;
+      scal[0]            = ia;
+      scal[1]            = (d[2 * CGS_MAXJ + 1] - sz) * ia;
+      if (blockIdx.x == 0)
+        {
+          d[DCGS_W]     = alpha;
+          d[DCGS_W + 1] = scal[1];
+        }
+    }
+  __syncthreads();
+  const double ia = scal[0], hjj = scal[1];
+  const int    wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double       nu = 0;
+  int64_t      r0, r1;
+  dcgs_rows(n, r0, r1);
+  for (int64_t i = r0 + 2 * (lane + 64 * wv); i < r1; i += 2 * DCGS_WIDE)
+    {
+      D2 ts = {0.0, 0.0}, tz = {0.0, 0.0};
+#pragma unroll 1
+      for (int c0 = 0; c0 < J; c0 += 8)
+        {
+          D2 v2[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            v2[k] = c0 + k < J ? *reinterpret_cast<const D2 *>(V + (size_t)(c0 + k) * ld + i)
+                               : D2{0.0, 0.0};
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            {
+              const D2 cf = coef[c0 + k < CGS_MAXJ ? c0 + k : 0];
+              const double s = c0 + k < J ? cf[0] : 0.0, z = c0 + k < J ? cf[1] : 0.0;
+              ts += v2[k] * s;
+              tz += v2[k] * z;
+            }
+        }
+      const D2 q2 = *reinterpret_cast<const D2 *>(q + i);
+      const D2 w2 = *reinterpret_cast<const D2 *>(w + i);
+      const D2 qi = (q2 - ts) * ia;
+      const D2 ui = (w2 - tz - qi * hjj) * ia;
+      *reinterpret_cast<D2 *>(q + i)  = qi;
+      *reinterpret_cast<D2 *>(un + i) = ui;
+      nu += ui[0] * ui[0];
+      nu += ui[1] * ui[1];
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+    nu += __shfl_down(nu, off);
+  if (lane == 0)
+    red[wv] = nu;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    {
+      double t = 0;
+      for (int k = 0; k < DCGS_WIDE / 64; ++k)
+        t += red[k];
+      part[(size_t)blockIdx.x * DCGS_W] = t;
+    }
+}
+
 // v = w / sqrt(|w|^2) with the squared norm read on the device (the
 // partitioned GMRES all-reduces |w|^2 before the root)
 __global__ void

@@ -67,6 +67,10 @@ enum
   BRICK_REDUCE       = BRICK_REDUCE_OWNED | BRICK_REDUCE_GHOST
 };
 
+// polls of a partial-slot granule before a resident sweep's wait gives up
+// (brick.h k_brick_sweeps; gls_op_set_sweep_spin_bound changes it per operator)
+constexpr int SWEEP_SPIN_MAX_DEFAULT = 1 << 18;
+
 // multiplicity classes of the brick-boundary nodes (k_shared_reduce_cls)
 struct ReduceClasses
 {

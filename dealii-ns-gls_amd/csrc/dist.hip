@@ -54,6 +54,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace gls
@@ -151,6 +152,9 @@ struct glsDist_
   int               rank = 0, world = 1;
   ncclComm_t        comm = nullptr;
   Group            *group = nullptr;
+  // the host thread that last drove this member in rank mode (creation: the
+  // creating thread); Group::barrier tells a lockstep misuse from slow peers
+  std::thread::id   driver = std::this_thread::get_id();
   std::unique_ptr<Transport> tx;
   // in-process all-reduce: this member's staged operand (peers read it)
   double           *red_stage = nullptr;
@@ -182,31 +186,81 @@ struct Group
   uint64_t                gen     = 0;
   bool                    broken  = false;
 
+  // per rank: the barrier generation it last arrived at
+  std::vector<uint64_t>   arrived_at;
+
+  // host barrier of the members driven one thread per member.  Fails fast
+  // (after a 10 s grace for first-launch code-object loads) when every member
+  // still missing was last driven -- or created -- by the very thread that is
+  // blocked here: the members are being driven one after another from one
+  // thread, which can never complete a rank-mode call; otherwise fails after
+  // GLS_DIST_BARRIER_TIMEOUT seconds (default 120).  Either way the group is
+  // broken for good (its members' events are mid-call).
   void
-  barrier(int world)
-  {
-    std::unique_lock<std::mutex> lk(mu);
-    if (broken)
-      throw std::runtime_error("gls_dist: in-process group broken by an earlier failure");
-    const uint64_t g = gen;
-    if (++arrived == world)
-      {
-        arrived = 0;
-        ++gen;
-        cv.notify_all();
-        return;
-      }
-    if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || broken; }) ||
-        broken)
-      {
-        broken = true;
-        cv.notify_all();
-        throw std::runtime_error("gls_dist: an in-process group member waited 120 s for its "
-                                 "peers (each member driven from its own thread makes the same "
-                                 "sequence of rank calls)");
-      }
-  }
+  barrier(glsDist_ *self);
 };
+
+double
+barrier_timeout_s()
+{
+  static const double t = [] {
+    const char *e = getenv("GLS_DIST_BARRIER_TIMEOUT");
+    const double v = e ? std::atof(e) : 0.0;
+    return v > 0 ? v : 120.0;
+  }();
+  return t;
+}
+
+void
+Group::barrier(glsDist_ *self)
+{
+  const int world = self->world;
+  std::unique_lock<std::mutex> lk(mu);
+  if (broken)
+    throw std::runtime_error("gls_dist: in-process group broken by an earlier failure");
+  const std::thread::id me = std::this_thread::get_id();
+  self->driver             = me;
+  const uint64_t g         = gen;
+  if (arrived_at.size() < (size_t)world)
+    arrived_at.resize((size_t)world, UINT64_MAX);
+  arrived_at[(size_t)self->rank] = g;
+  if (++arrived == world)
+    {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return;
+    }
+  const auto   t0    = std::chrono::steady_clock::now();
+  const double limit = barrier_timeout_s();
+  for (;;)
+    {
+      if (cv.wait_for(lk, std::chrono::milliseconds(250), [&] { return gen != g || broken; }))
+        {
+          if (broken)
+            throw std::runtime_error("gls_dist: in-process group broken by an earlier failure");
+          return;
+        }
+      const double el =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      bool lockstep = el > 10.0;
+      for (size_t r = 0; lockstep && r < members.size(); ++r)
+        if (r < arrived_at.size() && arrived_at[r] != g && members[r] && members[r]->driver != me)
+          lockstep = false;
+      if (lockstep || el > limit)
+        {
+          broken = true;
+          cv.notify_all();
+          throw std::runtime_error(
+            lockstep ? "gls_dist: rank-mode call on an in-process group driven from one thread "
+                       "(every missing member was last driven by this blocked thread); drive "
+                       "each member from its own thread, or use the *_group entry points" :
+                       "gls_dist: an in-process group member waited " + std::to_string(limit) +
+                         " s for its peers (GLS_DIST_BARRIER_TIMEOUT; each member driven from "
+                         "its own thread makes the same sequence of rank calls)");
+        }
+    }
+}
 
 size_t
 row_bytes(const glsOp_ *op)
@@ -415,7 +469,7 @@ struct GroupTransport : Transport
   void
   import_ghosts(glsDist_ *d, void *src) override
   {
-    d->group->barrier(d->world); // every member's ev_packed recorded
+    d->group->barrier(d); // every member's ev_packed recorded
     const size_t rb = row_bytes(d->op);
     for (const Peer &p : d->peers)
       {
@@ -435,7 +489,7 @@ struct GroupTransport : Transport
   export_ghosts(glsDist_ *d, const void *dst) override
   {
     d->cur_dst = const_cast<void *>(dst);
-    d->group->barrier(d->world); // every member's ev_ghosts recorded, cur_dst set
+    d->group->barrier(d); // every member's ev_ghosts recorded, cur_dst set
     const size_t rb = row_bytes(d->op);
     for (const Peer &p : d->peers)
       {
@@ -454,20 +508,20 @@ struct GroupTransport : Transport
   void
   fence_send(glsDist_ *d, hipStream_t s) override
   {
-    d->group->barrier(d->world); // the peers' last imports from this send buffer recorded
+    d->group->barrier(d); // the peers' last imports from this send buffer recorded
     wait_peers(d, s, &glsDist_::ev_imported);
   }
   void
   fence_ghosts(glsDist_ *d, hipStream_t s) override
   {
-    d->group->barrier(d->world); // the peers' exports from these ghost rows recorded
+    d->group->barrier(d); // the peers' exports from these ghost rows recorded
     wait_peers(d, s, &glsDist_::ev_exported);
   }
   void
   allreduce(glsDist_ *d, double *buf, int64_t count, bool max, hipStream_t s) override
   {
     Group *g = d->group;
-    g->barrier(d->world); // the last all-reduce's ev_red_done recorded everywhere
+    g->barrier(d); // the last all-reduce's ev_red_done recorded everywhere
     for (glsDist_ *q : g->members)
       HIP_THROW(hipStreamWaitEvent(s, q->ev_red_done, 0));
     if (d->red_cap < count)
@@ -482,7 +536,7 @@ struct GroupTransport : Transport
       HIP_THROW(hipMemcpyAsync(d->red_stage, buf, (size_t)count * sizeof(double),
                                hipMemcpyDeviceToDevice, s));
     HIP_THROW(hipEventRecord(d->ev_red_staged, s));
-    g->barrier(d->world); // every member's operand staged (and its pointer set)
+    g->barrier(d); // every member's operand staged (and its pointer set)
     StageArgs a{};
     const int n = (int)g->members.size();
     if (n > 16)

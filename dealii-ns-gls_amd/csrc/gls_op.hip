@@ -456,6 +456,10 @@ build_bricks(glsOp_ *op, const glsOpDesc *d, const char *cell_curved)
           }
         HIP_THROW(hipMalloc(&op->d_sweep_err, sizeof(uint32_t)));
         HIP_THROW(hipMemset(op->d_sweep_err, 0, sizeof(uint32_t)));
+        HIP_THROW(hipHostMalloc((void **)&op->h_sweep_flag, sizeof(uint32_t),
+                                hipHostMallocMapped | hipHostMallocCoherent));
+        *(volatile uint32_t *)op->h_sweep_flag = 0;
+        HIP_THROW(hipHostGetDevicePointer((void **)&op->d_sweep_flag, op->h_sweep_flag, 0));
       }
   }
   const uint32_t slot = (uint32_t)n_slot_total;
@@ -864,13 +868,19 @@ struct Impl
     auto set_lattice = [&]() {
       const bool four  = mode != MODE_RESIDUAL && dim == 3 && k == 2 &&
                         op->L <= 243; // BrickOcc<...>::four (one-layer bricks)
-      const int  waves = four ? (sizeof(T) == 4 ? 5 : 4) : (sizeof(T) == 4 ? 4 : 3);
+      const int  waves = four ? BrickOcc<dim, k, T, MODE_NEWTON, GEO_ANY, 1>::waves :
+                                BrickOcc<dim, k, T, MODE_RESIDUAL, GEO_ANY, 1>::waves;
       const int  nz    = op->L / (op->Lx * op->Ly);
       const size_t budget = (size_t)160 * 1024 / waves;
       a.PLx = op->Lx, a.PLy = op->Ly;
       if (dim == 3 && k == 2 && op->Lx == 9 && op->Ly == 9)
         {
-          static constexpr int pads[2][2] = {{11, 12}, {9, 11}};
+          // x-line lane map (brick.h xline): each lane reads and adds its own
+          // node only; 11 x 9 is the best model cost that fits both budgets
+          // (reads 8 / adds 7 cycles, scripts/lds_layout_search.py --xdpp)
+          static constexpr int pads_l[2][2] = {{11, 12}, {9, 11}};
+          static constexpr int pads_x[2][2] = {{11, 9}, {11, 9}};
+          const auto &pads = xdpp<dim, k, T>() ? pads_x : pads_l;
           for (const auto &pl : pads)
             if (BrickLDS<dim, k, T>::bytes(pl[0] * pl[1] * nz) <= budget)
               {
@@ -1245,10 +1255,28 @@ op_vmult_mode(const glsOp_ *op)
 }
 
 bool
+sweep_stalled(const glsOp_ *op)
+{
+  if (!op || !op->h_sweep_flag || op->sweep_reported ||
+      *(volatile const uint32_t *)op->h_sweep_flag == 0)
+    return false;
+  op->sweep_off      = true;
+  op->sweep_reported = true;
+  return true;
+}
+
+bool
 brick_sweeps(const glsOp_ *op, int mode, void *v0, void *v1, void *slots0, void *slots1,
              int nsweep, const RelaxStep &rx, hipStream_t s)
 {
   using I = Impl<3, 2, float>;
+  // after a stall (a brick's neighbour was not resident: kernels of other
+  // streams or processes held its CU) one launch per step for good
+  if (op->sweep_off || (op->h_sweep_flag && *(volatile const uint32_t *)op->h_sweep_flag))
+    {
+      op->sweep_off = true;
+      return false;
+    }
   if (nsweep < 2 || !op->d_sweep_gran[0] || !deferred_reduce_ok(op) || op->degree != 2 ||
       op->L > SWEEP_MAX_L || !rx.b || (mode != MODE_NEWTON && mode != MODE_FIXED))
     return false;
@@ -1279,8 +1307,10 @@ brick_sweeps(const glsOp_ *op, int mode, void *v0, void *v1, void *slots0, void 
   sw.gran[1]    = op->d_sweep_gran[1];
   sw.gran_bytes = (uint32_t)((uint64_t)op->n_slots * 32u);
   sw.err        = op->d_sweep_err;
+  sw.flag       = op->d_sweep_flag;
   sw.epoch      = op->sweep_epoch;
   sw.nsweep     = nsweep;
+  sw.spin_max   = op->sweep_spin_max;
   sw.timing     = nullptr;
 #if GLS_SWEEP_TIMING
   // timing builds: per-phase clock stamps of every launch appended to the
@@ -1927,6 +1957,8 @@ gls_op_destroy(glsOp op)
       (void)hipFree(b);
   if (op->gmres_host)
     (void)hipHostFree(op->gmres_host);
+  if (op->h_sweep_flag)
+    (void)hipHostFree(op->h_sweep_flag);
   op->stage.release();
   gls::faces_release(op);
   delete op;
@@ -2704,6 +2736,16 @@ gls_op_sweep_stats(glsOp op, uint64_t *launches, uint64_t *timeouts)
     }
   *launches = op->sweep_launches;
   *timeouts = h;
+  GLS_CATCH
+}
+
+glsStatus
+gls_op_set_sweep_spin_bound(glsOp op, int64_t polls)
+{
+  GLS_TRY
+  if (!op || polls < 0 || polls > (int64_t)1 << 30)
+    throw std::runtime_error("gls_op_set_sweep_spin_bound: bad arguments");
+  op->sweep_spin_max = (int)polls;
   GLS_CATCH
 }
 

@@ -243,7 +243,8 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   const std::string ortho        = getenv("GLS_GMRES_ORTHO") ? getenv("GLS_GMRES_ORTHO") : "";
   const bool        force_rocblas    = ortho == "rocblas";
   const bool        force_three_pass = ortho == "cgs3";
-  const bool        dcgs = ortho.empty() && (!mg || gls::mg_is_linear(mg)) && m + 1 < CGS_MAXJ;
+  const bool        dcgs = (ortho.empty() || ortho == "dcgs-narrow") &&
+                    (!mg || gls::mg_is_linear(mg)) && m + 1 < CGS_MAXJ;
   auto              arnoldi       = [&](int j) {
     precondition(zcol(j), vcol(j));
     gls::op_vmult_device(op, w.d(), zcol(j), s);
@@ -323,16 +324,31 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   // |u_{j+1}| for H_{j+1,j} and leaves out s_{j+1} (O(eps) terms).  The kept
   // directions are M^{-1} u_j; with U = Q R (R_ij = s_j[i], R_jj = alpha_j),
   // M^{-1} Q y = Z (R^{-1} y).
+  // the wide DCGS2 passes (cgs.h: 8-wave blocks, 16-byte row pairs) for an
+  // even row count; GLS_GMRES_ORTHO=dcgs-narrow keeps the round-5 passes
+  const bool wide = n % 2 == 0 && ortho != "dcgs-narrow";
+  auto dcgs_dots = [&](int J, const double *u, const double *wv) {
+    if (wide)
+      hipLaunchKernelGGL(k_dcgs_dots_wide, dim3(CGS_BLOCKS), dim3(DCGS_WIDE), 0, s,
+                         (const double *)V.d(), J, u, wv, cpart.d(), n, n);
+    else
+      hipLaunchKernelGGL(k_dcgs_dots, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(), J,
+                         u, wv, cpart.d(), n, n);
+  };
   auto arnoldi_d = [&](int j) {
     precondition(zcol(j), vcol(j));
     gls::op_vmult_device(op, w.d(), zcol(j), s);
     double *dd = dh.d();
-    hipLaunchKernelGGL(k_dcgs_dots, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(), j,
-                       (const double *)vcol(j), (const double *)w.d(), cpart.d(), n, n);
+    dcgs_dots(j, (const double *)vcol(j), (const double *)w.d());
     hipLaunchKernelGGL(k_dcgs_finish, dim3(DCGS_W), dim3(256), 0, s, (const double *)cpart.d(),
                        dd, j, -1, (double *)nullptr);
-    hipLaunchKernelGGL(k_dcgs_update, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(), j,
-                       dd, vcol(j), (const double *)w.d(), vcol(j + 1), cpart.d(), n, n);
+    if (wide)
+      hipLaunchKernelGGL(k_dcgs_update_wide, dim3(CGS_BLOCKS), dim3(DCGS_WIDE), 0, s,
+                         (const double *)V.d(), j, dd, vcol(j), (const double *)w.d(),
+                         vcol(j + 1), cpart.d(), n, n);
+    else
+      hipLaunchKernelGGL(k_dcgs_update, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(),
+                         j, dd, vcol(j), (const double *)w.d(), vcol(j + 1), cpart.d(), n, n);
     hipLaunchKernelGGL(k_dcgs_finish, dim3(1), dim3(256), 0, s, (const double *)cpart.d(), dd, -1,
                        DCGS_W + 2, host_dev + (j % 2) * HC);
     HIP_THROW(hipGetLastError());
@@ -437,8 +453,7 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
     else
       {
         double *dd = dh.d();
-        hipLaunchKernelGGL(k_dcgs_dots, dim3(CGS_BLOCKS), dim3(256), 0, s, (const double *)V.d(),
-                           jd, (const double *)vcol(jd), (const double *)nullptr, cpart.d(), n, n);
+        dcgs_dots(jd, (const double *)vcol(jd), (const double *)nullptr);
         hipLaunchKernelGGL(k_dcgs_finish, dim3(DCGS_W), dim3(256), 0, s,
                            (const double *)cpart.d(), dd, jd, -1, (double *)nullptr);
         HIP_THROW(hipGetLastError());
@@ -558,6 +573,10 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
     }
   op->stage.finish_out(x_, s);
   HIP_THROW(hipStreamSynchronize(s));
+  // a resident smoothing sweep that stalled poisoned a V-cycle with NaN:
+  // reported here (the multigrid continues with one launch per step)
+  if (mg)
+    gls::mg_check_stall(mg, "gls_gmres_solve");
   if (result)
     {
       result->n_iterations   = it;

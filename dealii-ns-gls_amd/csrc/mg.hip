@@ -2781,11 +2781,16 @@ gls_mg_vcycle(glsMG mg, void *dst, const void *src, void *stream)
   if (!mg || !dst || !src)
     throw std::runtime_error("gls_mg_vcycle: null argument");
   hipStream_t s = (hipStream_t)stream;
+  // a stall of an earlier (asynchronous) V-cycle is reported before this one
+  // runs; a stall of this one as soon as its flag is visible (host-layout
+  // vectors: at return)
+  gls::mg_check_stall(mg, "gls_mg_vcycle");
   const void *x = mg->stage.in_vec(src, 0, s);
   void       *y = mg->stage.out_vec(dst);
   gls::mg_vcycle_device(mg, y, x, s);
   mg->stage.finish_out(dst, s);
   mg->stage.done(s);
+  gls::mg_check_stall(mg, "gls_mg_vcycle");
   GLS_CATCH
 }
 
@@ -2837,6 +2842,23 @@ mg_check_outer(glsMG mg, const glsOp_ *op)
                              "operator's size");
   if (!mg->setup_done)
     throw std::runtime_error("gls_gmres_solve: the multigrid is not set up (gls_mg_setup)");
+}
+
+// a resident smoothing sweep of a level stalled since the last check (its
+// neighbour brick was not resident: kernels of other streams held CUs): the
+// level now runs one launch per step (gls::brick_sweeps); reported once
+void
+mg_check_stall(glsMG mg, const char *who)
+{
+  bool stalled = false;
+  for (glsOp op : mg->ops)
+    stalled = gls::sweep_stalled(op) || stalled;
+  if (stalled)
+    throw std::runtime_error(std::string(who) +
+                             ": a resident smoothing sweep timed out (co-residency of the "
+                             "level's bricks lost, INTEGRATION.md §5); the V-cycle it ran in "
+                             "returned NaN, the multigrid now runs one launch per smoothing "
+                             "step: repeat the computation");
 }
 
 bool

@@ -162,6 +162,15 @@ struct glsOp_
   // asked yet)
   uint64_t        *d_sweep_gran[2] = {nullptr, nullptr};
   uint32_t        *d_sweep_err     = nullptr;
+  // stall flag in host-mapped memory (set by a wait that hit the spin bound)
+  // and its device address; after a stall the operator runs one launch per
+  // step for the rest of its life (sweep_off) and the stall is reported once
+  // through the next multigrid / GMRES status (sweep_stalled)
+  uint32_t        *h_sweep_flag    = nullptr;
+  uint32_t        *d_sweep_flag    = nullptr;
+  mutable bool     sweep_off       = false;
+  mutable bool     sweep_reported  = false;
+  int              sweep_spin_max  = gls::SWEEP_SPIN_MAX_DEFAULT;
   mutable uint32_t sweep_epoch     = 0;
   mutable uint64_t sweep_launches  = 0;
   mutable int64_t  sweep_cap[2][3][2] = {{{-1, -1}, {-1, -1}, {-1, -1}}, {{-1, -1}, {-1, -1}, {-1, -1}}};
@@ -251,6 +260,9 @@ int  op_vmult_mode(const glsOp_ *op);
 // reduction is left pending (its slots, its src) as after a deferred
 // per-launch sequence.  False (nothing launched) where the operator or the
 // device does not qualify: the caller launches the steps one by one.
+// a resident sweep of op stalled (its stall flag is set) and this was not
+// reported yet: marks it reported and turns the resident sweeps off for op
+bool sweep_stalled(const glsOp_ *op);
 bool brick_sweeps(const glsOp_ *op, int mode, void *v0, void *v1, void *slots0, void *slots1,
                   int nsweep, const RelaxStep &rx, hipStream_t s);
 // one V-cycle on node-major device vectors of the multigrid's outer
@@ -262,6 +274,8 @@ void mg_check_outer(glsMG mg, const glsOp_ *op);
 // true when one V-cycle is a linear map of its input (no coarse solve
 // iterated to a tolerance): GMRES may then keep M^{-1} v_j (krylov.hip)
 bool mg_is_linear(glsMG mg);
+// throws (once) when a level's resident smoothing sweeps stalled
+void mg_check_stall(glsMG mg, const char *who);
 // outflow boundary-face terms (faces.hip), launched after the cell kernels
 void faces_setup(glsOp_ *op, const glsOpDesc *d);
 void faces_release(glsOp_ *op);

@@ -37,6 +37,7 @@ EXPORTS = [
     "gls_op_get_max_u", "gls_mg_set_vector_layout", "gls_dist_update_ghost_values",
     "gls_dist_get_max_u", "gls_op_compute_diagonal", "gls_op_invert_diagonal", "gls_mg_relax",
     "gls_dist_compress_add", "gls_op_brick_shape", "gls_op_sweep_stats", "gls_op_cell_permutation",
+    "gls_op_set_sweep_spin_bound",
     "gls_discover_bricks", "gls_mg_coarse_statistics", "gls_mg_coarse_setup_times",
     "gls_amg_create", "gls_amg_destroy", "gls_amg_vmult", "gls_amg_info", "gls_mg_coarse_amg",
     "gls_amg_level_matrix",
@@ -176,6 +177,7 @@ def lib():
         L.gls_dist_compress_add.argtypes = [vp, vp, vp]
         L.gls_op_brick_shape.argtypes = [vp, vp]
         L.gls_op_sweep_stats.argtypes = [vp, vp, vp]
+        L.gls_op_set_sweep_spin_bound.argtypes = [vp, C.c_int64]
         L.gls_op_cell_permutation.argtypes = [vp, vp]
         L.gls_op_element_matrices.argtypes = [vp, vp]
         L.gls_op_system_matrix.argtypes = [vp, C.POINTER(i64), vp, vp, vp]
@@ -376,6 +378,11 @@ class NavierStokesOperator:
         n, c = C.c_uint64(0), C.c_uint64(0)
         _check(lib().gls_op_sweep_stats(self.h, C.byref(n), C.byref(c)))
         return int(n.value), int(c.value)
+
+    def set_sweep_spin_bound(self, polls):
+        """Polls of a neighbour's slot before a resident sweep's wait gives
+        up (gls_op_set_sweep_spin_bound; 0 forces the stall path: tests)."""
+        _check(lib().gls_op_set_sweep_spin_bound(self.h, int(polls)))
 
     def __del__(self):
         try:

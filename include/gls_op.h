@@ -169,6 +169,14 @@ glsStatus gls_op_brick_shape(glsOp op, int *dims);
  * sequences run as one resident launch, *timeouts = slot waits that hit
  * their spin bound (0 on a healthy device; synchronises the device). */
 glsStatus gls_op_sweep_stats(glsOp op, uint64_t *launches, uint64_t *timeouts);
+/* Polls of a neighbour's partial-slot granule before a resident sweep's wait
+ * gives up (default 2^18).  A wait that gives up poisons the brick's iterate
+ * with NaN and raises the operator's stall flag; from then on the level runs
+ * one launch per smoothing step, and the next gls_mg_vcycle or
+ * gls_gmres_solve on the multigrid returns an error status once (the
+ * co-residency precondition of INTEGRATION.md §5).  Test hook: 0 makes every
+ * wait that is not satisfied at its first poll give up. */
+glsStatus gls_op_set_sweep_spin_bound(glsOp op, int64_t polls);
 /* The discovery gls_op_create runs for brick = {-1,-1,-1}, on its own (host
  * only, no device call): shape = the brick shape found ({0,0,0}: none),
  * perm[internal cell] = caller cell. */

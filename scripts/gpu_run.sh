@@ -15,6 +15,8 @@
 #                          (scripts/ab_env.sh, SPEC lines from FILE)
 #   abmg:FILE              the same for the multigrid (scripts/ab_mg.sh)
 #   py:SCRIPT[:ARGS]       python SCRIPT ARGS (colons in ARGS become spaces)
+#   prof:SCRIPT[:ARGS]     rocprofv3 --kernel-trace --stats of python SCRIPT ARGS
+#                          (prof_NAME/run_kernel_stats.csv)
 # The round's profiles/r0N/README.md names the TAG and STEPs of each file.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -82,6 +84,16 @@ for r in csv.reader(open('$OUT/stats/run_kernel_stats.csv')):
       timeout -k 10 400 python3 "$script" ${args//:/ } > "$OUT/$name.txt" 2>&1 ||
         { tail -20 "$OUT/$name.txt"; exit 1; }
       grep -v amdgpu.ids "$OUT/$name.txt" | tail -12
+      ;;
+    prof)
+      script=${arg%%:*}
+      args=
+      [ "$script" != "$arg" ] && args=${arg#*:}
+      name=$(basename "$script" .py)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run -- \
+        python3 "$script" ${args//:/ } > "$OUT/prof_$name.txt" 2>&1 || { tail -20 "$OUT/prof_$name.txt"; exit 1; }
+      grep -v amdgpu.ids "$OUT/prof_$name.txt" | tail -4
+      head -12 "$OUT/prof_$name/run_kernel_stats.csv" | cut -c1-160
       ;;
     *)
       echo "unknown step $step" >&2
