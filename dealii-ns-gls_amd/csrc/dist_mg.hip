@@ -56,6 +56,10 @@ struct glsDistMG_
   int64_t             *d_l2g = nullptr; // level-0 local node -> global node
   double              *g_buf = nullptr; // [ng0] all-reduced global vector
   void                *g_rhs = nullptr, *g_sol = nullptr; // [ng0] coarse precision
+  // agglomerated levels (glsDistMGDesc n_redundant_levels): the global
+  // operators below coarse_op (coarsest first; the caller's), coarse_mg's
+  // levels 0 .. red_ops.size() - 1
+  std::vector<glsOp>   red_ops;
   bool                 have_lin = false, setup_done = false;
   void                *outer = nullptr; // FP64 <-> level conversions: level-precision copy
   // GMRES workspace: V (m+1) n | w n | z n | y (m+1) (FP64)
@@ -361,20 +365,22 @@ coarse(Team &t, hipStream_t s)
 {
   glsDistMG_ *m0 = t.m[0];
   const int   ci = m0->desc.coarse_n_iterations;
-  if (ci > 0)
+  if (!m0->coarse_mg && ci > 0)
     {
       smooth(t, 0, true, ci, s);
       return;
     }
-  if (ci == 0)
+  if (!m0->coarse_mg && ci == 0)
     {
       for (auto *x : t.m)
         copy_vec(x->X[0], x->B[0], (size_t)x->n_dofs[0] * x->ts(), s);
       return;
     }
-  // direct: the owned coarse right-hand side scattered into a zeroed global
-  // vector, all-reduced (every global dof is owned by exactly one rank), the
-  // whole coarse level solved on every rank, the rank's local entries taken
+  // redundant (direct, or the agglomerated levels): the owned coarse
+  // right-hand side scattered into a zeroed global vector, all-reduced
+  // (every global dof is owned by exactly one rank), the whole coarse level
+  // solved -- or V-cycled over the agglomerated levels below it -- on every
+  // rank, the rank's local entries taken
   std::vector<double *> g;
   for (auto *x : t.m)
     {
@@ -581,17 +587,37 @@ gls_dist_mg_create(const glsDistMGDesc *d, const glsDist *levels, glsDistMG *out
       m->omega.assign(nl, 1.0);
       m->lambda.assign(nl, 0.0);
       HIP_THROW(hipMalloc((void **)&m->red, RED * sizeof(double)));
-      if (d->mg.coarse_n_iterations < 0)
+      const int nr = d->n_redundant_levels;
+      if (nr < 0 || (nr > 0 && (!d->redundant_ops || !d->redundant_child)))
+        throw std::runtime_error("gls_dist_mg_create: bad agglomeration arguments");
+      if (d->mg.coarse_n_iterations < 0 || nr > 0)
         {
           if (!d->coarse_global || !d->coarse_local_global)
-            throw std::runtime_error("gls_dist_mg_create: the direct coarse solver needs the "
-                                     "single-domain coarse operator and the level-0 node map");
+            throw std::runtime_error("gls_dist_mg_create: the direct coarse solver and the "
+                                     "agglomerated levels need the single-domain level-0 "
+                                     "operator and the level-0 node map");
           m->coarse_op = d->coarse_global;
           m->ng0       = d->coarse_global->n_dofs;
+          // the redundant single-domain hierarchy: the direct solve of the
+          // whole level 0 (one level), or the agglomerated levels below it
+          // plus level 0 with mg's smoother and coarse solver
           glsMGDesc cd = d->mg;
-          cd.n_levels          = 1;
+          cd.n_levels          = 1 + nr;
           cd.outer_precision   = d->coarse_global->prec;
-          check(gls_mg_create(&cd, &m->coarse_op, nullptr, &m->coarse_mg));
+          std::vector<glsOp>            rops;
+          std::vector<const uint32_t *> rch(1, nullptr);
+          for (int l = 0; l < nr; ++l)
+            {
+              if (!d->redundant_ops[l] || !d->redundant_child[l + 1] ||
+                  d->redundant_ops[l]->prec != d->coarse_global->prec)
+                throw std::runtime_error("gls_dist_mg_create: an agglomerated level is missing "
+                                         "or has another precision than level 0");
+              rops.push_back(d->redundant_ops[l]);
+              rch.push_back(d->redundant_child[l + 1]);
+            }
+          m->red_ops = rops;
+          rops.push_back(d->coarse_global);
+          check(gls_mg_create(&cd, rops.data(), nr > 0 ? rch.data() : nullptr, &m->coarse_mg));
           const int64_t nn = ops[0]->n_nodes;
           HIP_THROW(hipMalloc((void **)&m->d_l2g, std::max<int64_t>(1, nn) * 8));
           HIP_THROW(hipMemcpy(m->d_l2g, d->coarse_local_global, nn * 8, hipMemcpyHostToDevice));
@@ -761,6 +787,38 @@ gls_dist_mg_set_linearization_point(glsDistMG const *team, int n, const void *co
                     hp.push_back(gv[(size_t)r][(size_t)v]);
                   check(gls_op_set_previous_solution(cop, hp.data(), nv, weights, s));
                 }
+              // the agglomerated levels below: interpolate_to_mg on the
+              // global single-domain hierarchy (gls_mg_interpolate)
+              std::vector<void *> fine = gv[(size_t)r];
+              const int           nr   = (int)t.m[r]->red_ops.size();
+              for (int l = nr; l > 0; --l)
+                {
+                  glsOp_             *rop = t.m[r]->red_ops[(size_t)l - 1];
+                  std::vector<void *> crs;
+                  for (int v = 0; v < nv; ++v)
+                    {
+                      void *p = nullptr;
+                      HIP_THROW(hipMallocAsync(&p, std::max<size_t>(16, (size_t)rop->n_dofs *
+                                                                          rop->tsize()), s));
+                      check(gls_mg_interpolate(t.m[r]->coarse_mg, l, p, fine[(size_t)v], s));
+                      crs.push_back(p);
+                    }
+                  check(gls_op_set_linearization_point(rop, crs[0], s));
+                  if (nv > 1 && rop->prm.order > 0)
+                    {
+                      std::vector<const void *> hp(1, nullptr);
+                      for (int v = 1; v < nv; ++v)
+                        hp.push_back(crs[(size_t)v]);
+                      check(gls_op_set_previous_solution(rop, hp.data(), nv, weights, s));
+                    }
+                  if (l < nr)
+                    for (void *p : fine)
+                      HIP_THROW(hipFreeAsync(p, s));
+                  fine = crs;
+                }
+              if (nr > 0)
+                for (void *p : fine)
+                  HIP_THROW(hipFreeAsync(p, s));
               for (void *p : gv[(size_t)r])
                 HIP_THROW(hipFreeAsync(p, s));
             }
@@ -803,7 +861,9 @@ gls_dist_mg_setup(glsDistMG const *team, int n, void *stream)
       for (auto *x : t.m)
         check(gls_op_invert_diagonal(gls::dist_op(x->lv[l]), x->invd[l], s));
       const glsMGDesc &d = t.m[0]->desc;
-      if (l == 0 && nl > 1 && d.coarse_n_iterations <= 0 && d.compute_evs_n_levels <= 0)
+      // (level 0 is not smoothed: a copy or direct / redundant coarse solve)
+      if (l == 0 && (t.m[0]->coarse_mg || nl > 1) &&
+          (t.m[0]->coarse_mg || d.coarse_n_iterations <= 0) && d.compute_evs_n_levels <= 0)
         {
           for (auto *x : t.m)
             {

@@ -631,7 +631,8 @@ class PartitionedOperator:
 class DistMGDesc(C.Structure):
     _fields_ = [("mg", MGDesc), ("child", C.c_void_p), ("owned_global_nodes", C.c_void_p),
                 ("n_global_nodes", C.c_void_p), ("coarse_global", C.c_void_p),
-                ("coarse_local_global", C.c_void_p)]
+                ("coarse_local_global", C.c_void_p), ("n_redundant_levels", C.c_int),
+                ("redundant_ops", C.c_void_p), ("redundant_child", C.c_void_p)]
 
 
 def _handles(objs):
@@ -650,14 +651,19 @@ class PartitionedMultigrid:
     fine).  child[l] (l >= 1): rank-local child lattice with the global-first
     NOT_OWNER bits; owned_global_nodes[l]: global ids of the owned nodes;
     coarse_global (direct coarse solve): a NavierStokesOperator on the whole
-    coarse mesh with coarse_l2g (level-0 local node -> global node).  The
-    team methods take every handle this process drives: [self] for an RCCL
-    rank, all members of an in-process group in rank order (tests)."""
+    coarse mesh with coarse_l2g (level-0 local node -> global node).
+    Agglomeration (glsDistMGDesc n_redundant_levels): redundant_ops, the
+    global NavierStokesOperators of the levels below level 0 (coarsest
+    first), and redundant_child[l] (l = 1 .. len(redundant_ops); entry 0
+    unused) the global child lattices up to coarse_global's mesh: those
+    levels run single-domain on every rank.  The team methods take every
+    handle this process drives: [self] for an RCCL rank, all members of an
+    in-process group in rank order (tests)."""
 
     def __init__(self, levels, child, owned_global_nodes, n_global_nodes,
                  smoothing_n_iterations=5, smoothing_eig_n_iterations=20, smoothing_range=20.0,
                  coarse_n_iterations=10, outer_precision="f64", compute_evs_n_levels=0,
-                 coarse_global=None, coarse_l2g=None):
+                 coarse_global=None, coarse_l2g=None, redundant_ops=None, redundant_child=None):
         n = len(levels)
         outer = GLS_F64 if outer_precision in ("f64", GLS_F64) else GLS_F32
         md = MGDesc(n, smoothing_n_iterations, smoothing_eig_n_iterations, smoothing_range,
@@ -669,15 +675,23 @@ class PartitionedMultigrid:
         ogp = (C.c_void_p * n)(*[g.ctypes.data for g in self._own])
         self._l2g = None if coarse_l2g is None else np.ascontiguousarray(coarse_l2g, np.int64)
         self.coarse_global = coarse_global
+        nr = len(redundant_ops) if redundant_ops else 0
+        self.redundant_ops = list(redundant_ops or [])
+        self._rch = [None] + [np.ascontiguousarray(c, dtype=np.uint32)
+                              for c in (redundant_child or [None])[1:]]
+        rop = (C.c_void_p * max(nr, 1))(*[o.h.value for o in self.redundant_ops])
+        rch = (C.c_void_p * (nr + 1))(*([None] + [c.ctypes.data for c in self._rch[1:]]))
         d = DistMGDesc(md, C.cast(chp, C.c_void_p), C.cast(ogp, C.c_void_p),
                        self._ng.ctypes.data,
                        None if coarse_global is None else coarse_global.h,
-                       None if self._l2g is None else self._l2g.ctypes.data)
+                       None if self._l2g is None else self._l2g.ctypes.data, nr,
+                       C.cast(rop, C.c_void_p) if nr else None,
+                       C.cast(rch, C.c_void_p) if nr else None)
         lv = (C.c_void_p * n)(*[L.h.value for L in levels])
         h = C.c_void_p()
         _check(lib().gls_dist_mg_create(C.byref(d), C.cast(lv, C.c_void_p), C.byref(h)))
         self.h = h
-        self._ptr_keep = (chp, ogp, lv)
+        self._ptr_keep = (chp, ogp, lv, rop, rch)
         self.levels = levels
 
     def __del__(self):

@@ -855,13 +855,19 @@ class NativeGroupMultigrid:
     on the finest level's partition."""
 
     def __init__(self, meshes, cmasks, world, precision="f32", coarse_n_iterations=10,
-                 **mg_kwargs):
+                 redundant_levels=0, **mg_kwargs):
+        """redundant_levels = k > 0: level agglomeration (glsDistMGDesc
+        n_redundant_levels): levels 0 .. k-1 and a copy of level k run
+        single-domain on every rank, levels k .. are partitioned."""
         import glsamd
         self.world = world
+        k = int(redundant_levels)
         n0 = meshes[0].n_cells
         cb = coarse_bounds(n0, world)
+        all_parts = [build_partitions(m, world, [b * (m.n_cells // n0) for b in cb])
+                     for m in meshes]
         self.parts, self.ranks, self.native = [], [], []
-        for m, cm in zip(meshes, cmasks):
+        for m, cm in zip(meshes[k:], cmasks[k:]):
             ratio = m.n_cells // n0
             parts = build_partitions(m, world, [b * ratio for b in cb])
             ranks = [RankOperator(m, cm, p, precision) for p in parts]
@@ -879,19 +885,29 @@ class NativeGroupMultigrid:
             self.fine_native.append(r.eng.partitioned(r.part, group=self.fine_native[0]
                                                       if self.fine_native else None))
         self.coarse_ops = [None] * world
-        if coarse_n_iterations < 0:
-            self.coarse_ops = [glsamd.NavierStokesOperator(meshes[0], cmasks[0], precision)
+        self.redundant_ops = [[] for _ in range(world)]
+        redundant_child = None
+        if coarse_n_iterations < 0 or k > 0:
+            self.coarse_ops = [glsamd.NavierStokesOperator(meshes[k], cmasks[k], precision)
                                for _ in range(world)]
+        if k > 0:
+            self.redundant_ops = [[glsamd.NavierStokesOperator(meshes[l], cmasks[l], precision)
+                                   for l in range(k)] for _ in range(world)]
+            redundant_child = [None] + [meshes[l - 1].child_lattice(meshes[l])
+                                        for l in range(1, k + 1)]
+        nl = len(meshes) - k
         self.mg = []
         for r in range(world):
-            child = rank_child_lattices(meshes, self.parts, r)
+            child = rank_child_lattices(meshes, all_parts, r)
+            child = [None] + child[k + 1:]
             self.mg.append(glsamd.PartitionedMultigrid(
-                [self.native[l][r] for l in range(len(meshes))], child,
-                [self.parts[l][r].local_nodes[:self.parts[l][r].n_owned]
-                 for l in range(len(meshes))],
-                [m.n_nodes for m in meshes], coarse_n_iterations=coarse_n_iterations,
+                [self.native[l][r] for l in range(nl)], child,
+                [self.parts[l][r].local_nodes[:self.parts[l][r].n_owned] for l in range(nl)],
+                [m.n_nodes for m in meshes[k:]], coarse_n_iterations=coarse_n_iterations,
                 coarse_global=self.coarse_ops[r],
-                coarse_l2g=self.parts[0][r].local_nodes if coarse_n_iterations < 0 else None,
+                coarse_l2g=(self.parts[0][r].local_nodes
+                            if coarse_n_iterations < 0 or k > 0 else None),
+                redundant_ops=self.redundant_ops[r] or None, redundant_child=redundant_child,
                 **mg_kwargs))
 
     def setup(self, params, u_star, hist=None, weights=None):
@@ -905,6 +921,9 @@ class NativeGroupMultigrid:
                 r.eng.set_parameters(**params)
         for op in self.coarse_ops:
             if op is not None:
+                op.set_parameters(**params)
+        for ops in self.redundant_ops:
+            for op in ops:
                 op.set_parameters(**params)
         fine = self.ranks[-1]
         u = [r.local_from_global(u_star) for r in fine]

@@ -524,6 +524,25 @@ typedef struct
    * ghost) to global nodes; NULL otherwise */
   glsOp                  coarse_global;
   const int64_t         *coarse_local_global;
+  /* Level agglomeration (deal.II builds every global-coarsening level with its
+   * own partition, main.cc:398-400; here the levels below a threshold are
+   * gathered whole onto every rank): n_redundant_levels > 0 makes this
+   * hierarchy's level 0 the coarsest PARTITIONED level and runs the levels
+   * below it, plus a copy of level 0, redundantly and single-domain on every
+   * rank.  coarse_global is then the global operator of level 0 (with
+   * coarse_local_global as for "direct"), redundant_ops[0 .. n-1] the global
+   * operators of the n levels below it (coarsest first) and
+   * redundant_child[l] (l = 1 .. n) the child lattice of global level l-1
+   * into global level l (level n = coarse_global; entry 0 unused).  The
+   * coarse solve of the partitioned V-cycle is one single-domain V-cycle over
+   * those n + 1 global levels with mg's smoother and mg's coarse solver on
+   * the lowest one: the same cycle as the whole hierarchy, with the small
+   * levels' halo exchanges replaced by one all-reduce of level 0's
+   * right-hand side (and the resident smoothing sweeps usable there).
+   * 0: none (NULL arrays). */
+  int                    n_redundant_levels;
+  const glsOp           *redundant_ops;
+  const uint32_t *const *redundant_child;
 } glsDistMGDesc;
 glsStatus gls_dist_mg_create(const glsDistMGDesc *desc, const glsDist *levels, glsDistMG *out);
 void      gls_dist_mg_destroy(glsDistMG mg);

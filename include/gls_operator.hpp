@@ -2,7 +2,8 @@
 // libglsamd.so (include/gls_op.h): the host-side mirror of the reference's
 // OperatorBase<Number> (include/operator_base.h:13-73) and
 // PreconditionerGMG (include/multigrid.h:61-141) for the matrix-free GLS
-// Navier–Stokes operator on MI355X.
+// Navier–Stokes operator on MI355X, with the Krylov and nonlinear solvers
+// around them (solver_l.h, solver_nl.h).
 //
 // RAII handles; a nonzero status becomes gls::Error (std::runtime_error)
 // carrying gls_last_error() — the reference's AssertThrow convention.
@@ -18,6 +19,9 @@
 
 #include "gls_op.h"
 
+#include <algorithm>
+#include <cmath>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -299,5 +303,173 @@ private:
   const Multigrid  *mg;
   glsGMRESDesc      desc;
   glsGMRESResult    res{};
+};
+
+// ---- nonlinear solvers: NonLinearSolverLinearized / Newton / Picard
+// (solver_nl.h:14-95, solver_nl.cc:4-140) over the caller's vector type with
+// the reference's std::function hooks, which a driver wires as main.cc:805-864
+// does (setup_jacobian = set_linearization_point, evaluate_residual /
+// evaluate_rhs = the operator's, solve_with_jacobian = LinearSolverGMRES::
+// solve, setup_preconditioner = Multigrid::initialize).  VectorType needs
+// what deal.II's Vector offers here: reinit(const VectorType &) (same layout,
+// zero), operator=(double) (0 only), add(double, const VectorType &),
+// l2_norm() and copy construction; HostVector below is one for operators in
+// the GLS_MEM_HOST layout.  A failed convergence throws gls::Error, as the
+// reference's AssertThrow.
+template <typename VectorType>
+class NonLinearSolverBase
+{
+public:
+  virtual ~NonLinearSolverBase() = default;
+  virtual int solve(VectorType &solution) const = 0; // returns the iterations
+
+  std::function<void(const VectorType &src)>                  setup_jacobian;
+  std::function<void(const VectorType &src)>                  setup_preconditioner;
+  std::function<void(VectorType &dst, const VectorType &src)> evaluate_residual;
+  std::function<void(VectorType &dst)>                        evaluate_rhs;
+  std::function<void(VectorType &dst, const VectorType &src)> solve_with_jacobian;
+  std::function<void(const VectorType &dst)>                  postprocess;
+  // the residual l2 norm of every step (the reference's "[N] step" lines)
+  mutable std::vector<double> history;
+};
+
+// one linear solve around the current solution (solver_nl.cc:10-24)
+template <typename VectorType>
+class NonLinearSolverLinearized : public NonLinearSolverBase<VectorType>
+{
+public:
+  int
+  solve(VectorType &solution) const override
+  {
+    this->setup_jacobian(solution);
+    VectorType rhs(solution);
+    rhs.reinit(solution);
+    this->evaluate_rhs(rhs);
+    this->setup_preconditioner(solution);
+    this->solve_with_jacobian(solution, rhs);
+    return 1;
+  }
+};
+
+// Newton on the residual, the preconditioner set up at the first step only
+// when inexact (solver_nl.cc:26-89; tolerance 1e-7, at most 30 steps there)
+template <typename VectorType>
+class NonLinearSolverNewton : public NonLinearSolverBase<VectorType>
+{
+public:
+  explicit NonLinearSolverNewton(bool inexact_newton, double newton_tolerance = 1.0e-7,
+                                 int newton_max_iteration = 30)
+    : inexact_newton(inexact_newton), tol(newton_tolerance), max_it(newton_max_iteration)
+  {}
+
+  int
+  solve(VectorType &solution) const override
+  {
+    VectorType rhs(solution), inc(solution);
+    rhs.reinit(solution);
+    inc.reinit(solution);
+    this->setup_jacobian(solution);
+    this->evaluate_residual(rhs, solution);
+    double l2 = rhs.l2_norm();
+    int    it = 0;
+    this->history.assign(1, l2);
+    while (l2 > tol)
+      {
+        inc = 0.0;
+        if (it == 0 || !inexact_newton)
+          this->setup_preconditioner(solution);
+        this->solve_with_jacobian(inc, rhs);
+        solution.add(1.0, inc);
+        if (this->postprocess)
+          this->postprocess(solution);
+        this->setup_jacobian(solution);
+        this->evaluate_residual(rhs, solution);
+        l2 = rhs.l2_norm();
+        ++it;
+        this->history.push_back(l2);
+        if (it > max_it)
+          throw Error("Newton iteration did not converge. Final residual_0 is " +
+                      std::to_string(l2) + ".");
+      }
+    return it;
+  }
+
+private:
+  bool   inexact_newton;
+  double tol;
+  int    max_it;
+};
+
+// fixed-point iteration on the linearized operator, converged when the
+// update's l2 norm drops below the tolerance (solver_nl.cc:91-140)
+template <typename VectorType>
+class NonLinearSolverPicard : public NonLinearSolverBase<VectorType>
+{
+public:
+  explicit NonLinearSolverPicard(double picard_tolerance = 1.0e-7, int picard_max_iteration = 30)
+    : tol(picard_tolerance), max_it(picard_max_iteration)
+  {}
+
+  int
+  solve(VectorType &solution) const override
+  {
+    VectorType rhs(solution), tmp(solution);
+    rhs.reinit(solution);
+    double l2 = 1e10;
+    int    it = 0;
+    this->history.clear();
+    while (l2 > tol)
+      {
+        tmp = solution;
+        this->setup_jacobian(solution);
+        this->evaluate_rhs(rhs);
+        this->setup_preconditioner(solution);
+        this->solve_with_jacobian(solution, rhs);
+        tmp.add(-1.0, solution);
+        l2 = tmp.l2_norm();
+        ++it;
+        this->history.push_back(l2);
+        if (it > max_it)
+          throw Error("Picard iteration did not converge. Final residual_0 is " +
+                      std::to_string(l2) + ".");
+      }
+    return it;
+  }
+
+private:
+  double tol;
+  int    max_it;
+};
+
+// a host vector for operators in the GLS_MEM_HOST layout (the reference's
+// LinearAlgebra::distributed::Vector<double> on one rank)
+struct HostVector : std::vector<double>
+{
+  using std::vector<double>::vector;
+  void
+  reinit(const HostVector &like)
+  {
+    assign(like.size(), 0.0);
+  }
+  HostVector &
+  operator=(double s)
+  {
+    std::fill(begin(), end(), s);
+    return *this;
+  }
+  void
+  add(double a, const HostVector &v)
+  {
+    for (size_t i = 0; i < size(); ++i)
+      (*this)[i] += a * v[i];
+  }
+  double
+  l2_norm() const
+  {
+    double s = 0;
+    for (double x : *this)
+      s += x * x;
+    return std::sqrt(s);
+  }
 };
 } // namespace gls

@@ -179,6 +179,13 @@ def test_gpu_vcycle_coarse_gmres_amg(name, n_ref):
     assert rel_err(out[1e-4][0], ref.vcycle(b)) < 5e-3
     info, setup_ms = mg.coarse_amg()
     assert info["levels"] >= 1 and setup_ms > 0
+    if name == "input_turek_2D_Re20_stat.json":
+        # the deck default: ML's coarse max size keeps the
+        # Re20 iso-Q1 coarse system in ONE dense level, so the coarse GMRES
+        # converges in a single iteration (a forced multilevel hierarchy
+        # stalls: profiles/r05/amg/re20_forced_multilevel_diagnosis.txt)
+        assert info["levels"] == 1, info
+        assert out[1e-4][1] <= 2 and out[1e-6][1] <= 2, (out[1e-4][1], out[1e-6][1])
     # the relaxation-sweep substitute of earlier rounds reaches the same V-cycle
     # (iteration counts of both: bench.py amg_companions)
     if d.simulation == "sphere":
