@@ -234,6 +234,16 @@ contract_v(const V *in, const T *tab, int pa, int base, int s)
 #ifndef GLS_XDPP_F64
 #define GLS_XDPP_F64 0
 #endif
+// L2 prefetch of the next round's tables (round 6 experiment): in the
+// prologue every wave of a FOUR kernel pulls the cache lines of its round-1
+// Newton table chunk into the L2 with one LDS-DMA dword load per line
+// (global_load_lds_dword into a 256-byte landing area nobody reads: no
+// registers held), so the round's LATE loads hit the L2 instead of the MALL /
+// HBM.  GLS_TAB_PREFETCH=1 builds it (A/B: profiles/r06/explore).
+#ifndef GLS_TAB_PREFETCH
+#define GLS_TAB_PREFETCH 0
+#endif
+
 template <int dim, int k, typename T>
 __host__ __device__ constexpr bool
 xdpp()
@@ -343,11 +353,12 @@ struct BrickLDS
   static constexpr int WPB = BLOCK / 64;
   static constexpr int ORG = 64; // cell-origin table entries (cells per brick)
   static constexpr int NTAP = X ? 4 * n * TAPS : 0; // x-line taps (values)
+  static constexpr int PF   = GLS_TAB_PREFETCH ? 256 : 0; // L2-prefetch landing bytes
   static size_t
   bytes(int L) // L: padded LDS lattice size
   {
     return 16 * ((size_t)NP * L + (size_t)WPB * CPW * WB) + tab_offset(L) +
-           sizeof(T) * (NTAP + 4 * n * CoefRow<T, n>::RP) + sizeof(int) * ORG;
+           sizeof(T) * (NTAP + 4 * n * CoefRow<T, n>::RP) + sizeof(int) * ORG + PF;
   }
   __host__ __device__ static size_t
   tab_offset(int L) // accumulator bytes (FP64 for both precisions) rounded up to 16

@@ -980,6 +980,13 @@ dist_op(glsDist d)
   return d->op;
 }
 
+// a member of an in-process group (several partitions on one device)
+bool
+dist_in_process(glsDist d)
+{
+  return d && d->group != nullptr;
+}
+
 int
 dist_rank(glsDist d)
 {

@@ -617,6 +617,14 @@ gls_dist_mg_create(const glsDistMGDesc *d, const glsDist *levels, glsDistMG *out
             }
           m->red_ops = rops;
           rops.push_back(d->coarse_global);
+          // the members of an in-process group share one device and run
+          // their redundant cycles at the same time: a resident smoothing
+          // launch per member could not keep all its bricks resident (the
+          // co-residency precondition), so those levels
+          // take one launch per step there; one rank per GPU keeps them
+          if (gls::dist_in_process(levels[0]))
+            for (glsOp o : rops)
+              o->sweep_off = true;
           check(gls_mg_create(&cd, rops.data(), nr > 0 ? rch.data() : nullptr, &m->coarse_mg));
           const int64_t nn = ops[0]->n_nodes;
           HIP_THROW(hipMalloc((void **)&m->d_l2g, std::max<int64_t>(1, nn) * 8));

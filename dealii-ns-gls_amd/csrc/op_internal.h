@@ -295,6 +295,8 @@ fused_relax_ok(const glsOp_ *op)
 // one process drives in lockstep — one RCCL rank, or all members of an
 // in-process group (rank order)
 glsOp_ *dist_op(glsDist d);
+// a member of an in-process group (several partitions on one device)
+bool    dist_in_process(glsDist d);
 int     dist_rank(glsDist d);
 int     dist_world(glsDist d);
 // rx: per member, the damped-Jacobi step / residual fused on the owned rows
