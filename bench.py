@@ -647,6 +647,25 @@ def dist_gmres_companion(d, params, weights, n_ref, dist, rank, world, reps=10):
             "ms": t_ngm / its * 1e3, "n_gpus": world,
             "note": "gls_dist_mg_vcycle + gls_dist_gmres_solve (native team calls, "
                     "RCCL all-reduced CGS2), wall clock max over ranks"}
+        # level agglomeration: r0, r1 single-domain on every rank (one
+        # all-reduce of the r1 right-hand side), r2 partitioned
+        if n_ref >= 2:
+            amg_ = dmg.native(params, u, hist, weights, redundant_levels=n_ref - 1)
+            glsamd.PartitionedMultigrid.vcycle([amg_], [x], [b])
+            t_avc = wall(lambda: glsamd.PartitionedMultigrid.vcycle([amg_], [x], [b]), reps)
+
+            def agmres():
+                try:
+                    glsamd.dist_gmres_solve([fine_h], [amg_], [x], [b], n_max_iterations=28,
+                                            relative_tolerance=0.0, absolute_tolerance=0.0)
+                except glsamd.GlsError:
+                    pass
+            agmres()
+            t_agm = wall(agmres, 2)
+            out[f"r{n_ref}_dist_native_vcycle_f32_agglomerated"] = {
+                "ms": t_avc / reps * 1e3, "redundant_levels": n_ref - 1}
+            out[f"r{n_ref}_dist_native_gmres_iteration_agglomerated"] = {
+                "ms": t_agm / its * 1e3, "n_gpus": world}
     except Exception as e:  # reported, never fatal
         out[f"r{n_ref}_dist_native_gmres_iteration"] = {"error": str(e)}
     return out

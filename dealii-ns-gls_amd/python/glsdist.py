@@ -582,6 +582,7 @@ class DistributedMultigrid:
         self._fine = (meshes[-1], cmasks[-1], engine, native)
         self._n_global_nodes = [m.n_nodes for m in meshes]
         self._coarse_mesh = (meshes[0], cmasks[0], precision)
+        self._meshes = (list(meshes), list(cmasks), precision)
         self.levels = []
         for m, cm in zip(meshes, cmasks):
             if m.n_cells % n0:
@@ -624,33 +625,49 @@ class DistributedMultigrid:
             gd = torch.from_numpy(_dofs(D.r.part.local_nodes[:D.r.part.n_owned], D.r.nc))
             self._global_dof.append(gd.to(D.r.device))
 
-    def native(self, params, u_star, hist=None, weights=None):
+    def native(self, params, u_star, hist=None, weights=None, redundant_levels=0):
         """This rank's native partitioned multigrid over the same level
         operators (glsamd.PartitionedMultigrid, gls_dist_mg_*: the V-cycle
         with its halo exchanges, relaxation and coarse solve inside the
         library, one team call per rank) with its linearization point and
         setup done; the GMRES over it is glsamd.dist_gmres_solve([fine
         operator's native handle], [mg], ...).  Needs the native level
-        operators (engine "gpu")."""
+        operators (engine "gpu").  redundant_levels = k > 0: levels 0 .. k-1
+        and a global copy of level k run single-domain on this rank (level
+        agglomeration, glsDistMGDesc n_redundant_levels); the partitioned
+        hierarchy starts at level k."""
         import glsamd
-        hs = [D.native for D in self.levels]
+        k = int(redundant_levels)
+        levels = self.levels[k:]
+        hs = [D.native for D in levels]
         if any(h is None for h in hs):
             raise ValueError("native(): the level operators have no native handles")
-        coarse, l2g = None, None
-        if self._coarse_direct:
-            m0, cm0, prec = self._coarse_mesh
-            coarse = glsamd.NavierStokesOperator(m0, cm0, prec)
+        coarse, l2g, rops, rch = None, None, None, None
+        keep = []
+        if self._coarse_direct or k > 0:
+            meshes, cmasks, prec = self._meshes
+            coarse = glsamd.NavierStokesOperator(meshes[k], cmasks[k], prec)
             coarse.set_parameters(**params)
-            l2g = self.levels[0].r.part.local_nodes
+            l2g = levels[0].r.part.local_nodes
+            keep.append(coarse)
+            if k > 0:
+                rops = [glsamd.NavierStokesOperator(meshes[l], cmasks[l], prec)
+                        for l in range(k)]
+                for o in rops:
+                    o.set_parameters(**params)
+                rch = [None] + [meshes[l - 1].child_lattice(meshes[l]) for l in range(1, k + 1)]
+                keep += rops
         mg = glsamd.PartitionedMultigrid(
-            hs, self.child, [D.r.part.local_nodes[:D.r.part.n_owned] for D in self.levels],
-            self._n_global_nodes, smoothing_n_iterations=self.n_smooth,
+            hs, [None] + list(self.child[k + 1:]),
+            [D.r.part.local_nodes[:D.r.part.n_owned] for D in levels],
+            self._n_global_nodes[k:], smoothing_n_iterations=self.n_smooth,
             smoothing_eig_n_iterations=self.n_eig, smoothing_range=self.range,
             coarse_n_iterations=self.coarse_iters, compute_evs_n_levels=self.evs_levels,
-            coarse_global=coarse, coarse_l2g=l2g)
-        for D in self.levels:
+            coarse_global=coarse, coarse_l2g=l2g, redundant_ops=rops, redundant_child=rch)
+        mg._keep_ops = keep
+        for D in levels:
             D.r.eng.set_parameters(**params)
-        top = self.levels[-1].r
+        top = levels[-1].r
         u = [top.local_from_global(u_star)]
         h = None
         if hist is not None and params.get("order", 0) > 0:
