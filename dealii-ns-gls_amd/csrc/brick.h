@@ -239,7 +239,9 @@ contract_v(const V *in, const T *tab, int pa, int base, int s)
 // Newton table chunk into the L2 with one LDS-DMA dword load per line
 // (global_load_lds_dword into a 256-byte landing area nobody reads: no
 // registers held), so the round's LATE loads hit the L2 instead of the MALL /
-// HBM.  GLS_TAB_PREFETCH=1 builds it (A/B: profiles/r06/explore).
+// HBM.  Measured and NOT adopted: 6-13 % slower, FP64 and FP32
+// (profiles/r06/explore/ab_l2_prefetch.txt): round 1's tables are not the
+// critical path.  GLS_TAB_PREFETCH=1 builds it.
 #ifndef GLS_TAB_PREFETCH
 #define GLS_TAB_PREFETCH 0
 #endif
