@@ -381,26 +381,32 @@ dcgs_rows(int64_t n, int64_t &r0, int64_t &r1)
   r1                = r0 + per < n ? r0 + per : n;
 }
 
-// pass 1 (k_dcgs_dots): wave v of the block owns the columns c = v + 8 k
-// (k < 4) and keeps only their 2 x 4 accumulators (the narrow form kept all
-// 64 in every thread: 2 waves per SIMD); every wave streams u and w over
-// the block's rows (the other waves' re-reads hit the L2), so the basis is
-// read once, in 16-byte loads.  Each column's block sum comes from one wave:
-// no cross-wave reduction; u.u and u.w from wave 0.
+// pass 1 (k_dcgs_dots), wide: the 8 waves of a block split its rows in two
+// halves and the columns in four groups (wave v: row half v / 4, columns
+// c = v % 4 + 4 k, k < 8), each keeping 2 x 8 accumulators (the narrow form
+// kept all 64 in every thread: 2 waves per SIMD) and streaming u and w over
+// its half (each read by 4 waves, the re-reads L2 hits), the basis once, in
+// 16-byte loads; the two halves' sums of a column meet in LDS.  u.u and u.w
+// from the column-group-0 waves.
 __global__ void __launch_bounds__(DCGS_WIDE)
   k_dcgs_dots_wide(const double *__restrict__ V, int J, const double *__restrict__ u,
                    const double *__restrict__ w, double *__restrict__ part, int64_t n, int64_t ld)
 {
-  using D2       = __attribute__((ext_vector_type(2))) double;
-  const int wv   = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  constexpr int NW = DCGS_WIDE / 64, NK = CGS_MAXJ / NW;
+  using D2         = __attribute__((ext_vector_type(2))) double;
+  constexpr int NG = 4, NK = CGS_MAXJ / NG; // column groups, columns per group
+  __shared__ double red[2][DCGS_W];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int cg = wv % NG, half = wv / NG;
   double    as[NK], az[NK], b = 0, g = 0;
 #pragma unroll
   for (int k = 0; k < NK; ++k)
     as[k] = az[k] = 0;
   int64_t r0, r1;
   dcgs_rows(n, r0, r1);
-  for (int64_t i = r0 + 2 * lane; i < r1; i += 128)
+  // the block's row pairs split in two contiguous halves
+  const int64_t np = (r1 - r0 + 1) / 2, hp = (np + 1) / 2;
+  const int64_t h0 = r0 + 2 * (half * hp), h1 = half ? r1 : (r0 + 2 * hp < r1 ? r0 + 2 * hp : r1);
+  for (int64_t i = h0 + 2 * lane; i < h1; i += 128)
     {
       const D2 u2 = *reinterpret_cast<const D2 *>(u + i);
       const D2 w2 = w ? *reinterpret_cast<const D2 *>(w + i) : D2{0.0, 0.0};
@@ -408,7 +414,7 @@ __global__ void __launch_bounds__(DCGS_WIDE)
 #pragma unroll
       for (int k = 0; k < NK; ++k)
         {
-          const int c = wv + NW * k;
+          const int c = cg + NG * k;
           v2[k]       = c < J ? *reinterpret_cast<const D2 *>(V + (size_t)c * ld + i) : D2{0.0, 0.0};
         }
 #pragma unroll
@@ -419,7 +425,7 @@ __global__ void __launch_bounds__(DCGS_WIDE)
           az[k] += v2[k][0] * w2[0];
           az[k] += v2[k][1] * w2[1];
         }
-      if (wv == 0)
+      if (cg == 0)
         {
           b += u2[0] * u2[0];
           b += u2[1] * u2[1];
@@ -427,11 +433,10 @@ __global__ void __launch_bounds__(DCGS_WIDE)
           g += u2[1] * w2[1];
         }
     }
-  double *pb = part + (size_t)blockIdx.x * DCGS_W;
 #pragma unroll
   for (int k = 0; k < NK; ++k)
     {
-      const int c = wv + NW * k;
+      const int c = cg + NG * k;
       if (c >= J)
         continue; // wave-uniform
       double xs = as[k], xz = az[k];
@@ -443,11 +448,11 @@ __global__ void __launch_bounds__(DCGS_WIDE)
         }
       if (lane == 0)
         {
-          pb[c]            = xs;
-          pb[CGS_MAXJ + c] = xz;
+          red[half][c]            = xs;
+          red[half][CGS_MAXJ + c] = xz;
         }
     }
-  if (wv == 0)
+  if (cg == 0)
     {
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1)
@@ -457,10 +462,15 @@ __global__ void __launch_bounds__(DCGS_WIDE)
         }
       if (lane == 0)
         {
-          pb[2 * CGS_MAXJ]     = b;
-          pb[2 * CGS_MAXJ + 1] = g;
+          red[half][2 * CGS_MAXJ]     = b;
+          red[half][2 * CGS_MAXJ + 1] = g;
         }
     }
+  __syncthreads();
+  double *pb = part + (size_t)blockIdx.x * DCGS_W;
+  for (int c = threadIdx.x; c < DCGS_W; c += blockDim.x)
+    if (dcgs_col_used(c, J))
+      pb[c] = red[0][c] + red[1][c];
 }
 
 // pass 2 (k_dcgs_update), wide: the step's coefficients s, z in LDS (one

@@ -450,7 +450,11 @@ void      gls_dist_destroy(glsDist d);
  * update_ghost_values), dst's ghost block is zero on return (compress).
  * An RCCL rank, or a member of an in-process group driven from its own host
  * thread (every member then makes the same sequence of rank calls, each on
- * its own stream; tests) */
+ * its own stream; tests).  An in-process member waits for its peers at host
+ * barriers: it fails after GLS_DIST_BARRIER_TIMEOUT seconds (default 120),
+ * or after 10 s when every missing member was last driven by the waiting
+ * thread itself (members driven one after another from one thread), and the
+ * group is then broken for good. */
 glsStatus gls_dist_vmult(glsDist d, void *dst, void *src, void *stream);
 /* the same for all members of an in-process group, phases in lockstep */
 glsStatus gls_dist_vmult_group(glsDist const *members, void *const *dsts,
