@@ -982,8 +982,13 @@ def main():
         # HBM bytes per vmult from the committed rocprofv3 PMC passes of this
         # workload (scripts/pmc.sh + scripts/pmc_summary.py), when they match
         traffic = None
-        tf = os.environ.get("GLS_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r05", "pmc_r2",
-                                                             "traffic.json"))
+        # the newest round's PMC record of the headline kernel pair
+        tf = os.environ.get("GLS_TRAFFIC_JSON")
+        if tf is None:
+            for rnd in ("r06", "r05"):
+                tf = os.path.join(ROOT, "profiles", rnd, "pmc_r2", "traffic.json")
+                if os.path.exists(tf):
+                    break
         if tf and os.path.exists(tf) and world == 1:
             with open(tf) as f:
                 tj = json.load(f)
