@@ -1023,6 +1023,49 @@ class RedundantCoarseLU:
         return x
 
 
+class RedundantBottomMG:
+    """Level agglomeration for the host-driven DistributedMultigrid (the
+    native twin is glsDistMGDesc.n_redundant_levels): built over the global
+    meshes 0 .. k and passed as the coarse_solver of a DistributedMultigrid
+    over meshes k .. L with coarse_n_iterations = -1, it runs levels 0 .. k
+    single-domain on every rank -- one V-cycle per coarse solve, the same
+    smoother and the given coarse solver at the bottom -- after the level-k
+    right-hand side arrives all-gathered.  Its linearization point and history
+    are level k's, interpolated down the global levels (build_gmg).  The
+    V-cycle of the whole hierarchy, with the small levels' halo exchanges
+    replaced by one gather (deal.II re-partitions such levels instead,
+    main.cc:398-400)."""
+
+    def __init__(self, meshes, cmasks, precision, coarse_n_iterations=10, **mg_kwargs):
+        self.meshes, self.cmasks, self.precision = list(meshes), list(cmasks), precision
+        self.coarse_n_iterations, self.mg_kwargs = coarse_n_iterations, mg_kwargs
+        self.mg = self.ops = None
+
+    def __call__(self, mesh, cmask, precision):
+        # the coarse_solver factory protocol: level 0 of the partitioned
+        # hierarchy must be this bottom's finest level
+        if mesh.n_cells != self.meshes[-1].n_cells or precision != self.precision:
+            raise ValueError("RedundantBottomMG: the partitioned hierarchy must start at the "
+                             "bottom's finest level, in its precision")
+        return self
+
+    def setup(self, params, u, hist, weights):
+        import glsamd
+        import torch
+        h = None if hist is None or params.get("order", 0) == 0 else list(hist)
+        self.mg, self.ops = glsamd.build_gmg(self.meshes, self.cmasks, params, u, h, weights,
+                                             precision=self.precision,
+                                             coarse_n_iterations=self.coarse_n_iterations,
+                                             outer_precision=self.precision, **self.mg_kwargs)
+        torch.cuda.synchronize()
+
+    def solve(self, b):
+        import torch
+        x = torch.zeros_like(b)
+        self.mg.vcycle(x, b)
+        return x
+
+
 def gmres_solve(apply_A, apply_P, b, x, n_owned, allreduce, max_n_tmp_vectors=30,
                 max_iterations=10000, relative_tolerance=1e-8, absolute_tolerance=1e-12):
     """LinearSolverGMRES::solve (solver_l.cc:45-74) on rank-local vectors of a

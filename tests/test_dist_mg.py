@@ -316,3 +316,133 @@ def test_native_mg_plan(world):
         # the claiming rank owns the node (local index in the owned prefix)
         assert (loc[own] < pf.n_owned).all()
     assert (claims == 1).all()
+
+
+def _worker_agglomerated(rank, world, port, name, n_ref, k, q):
+    """A rank of the host-driven partitioned multigrid with level agglomeration
+    (glsdist.RedundantBottomMG's protocol): levels k .. partitioned, levels
+    0 .. k single-domain on every rank behind one gather (here an oracle
+    multigrid as the bottom, the CPU engine of the tests)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "dealii-ns-gls_amd", "python"), os.path.join(root, "oracle"),
+              os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    import glsdist as gd
+    from dist_engines import OracleEngine, OracleTransfers
+    from mg_ref import OracleGMG
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        meshes, cm, params, w, u, hist, b = _hierarchy(name, n_ref)
+
+        class OracleBottom:
+            def __call__(self, mesh, cmask, precision):
+                return self
+
+            def setup(self, prm, u0, h0, wts):
+                self.g = OracleGMG(meshes[:k + 1], cm[:k + 1], prm, u0.numpy(),
+                                   None if h0 is None else [h.numpy() for h in h0], wts,
+                                   coarse_iters=10)
+                self.g.setup_omega()
+
+            def solve(self, rhs):
+                return torch.from_numpy(self.g.vcycle(rhs.double().numpy()))
+
+        dmg = gd.DistributedMultigrid(meshes[k:], cm[k:], "f64", dist, rank, world,
+                                      engine=OracleEngine,
+                                      transfers=lambda m: OracleTransfers(m, meshes[k:]),
+                                      coarse_n_iterations=-1, coarse_solver=OracleBottom())
+        top = dmg.levels[-1]
+        dmg.set_linearization_point(params, top.scatter_global(u),
+                                    [top.scatter_global(h) for h in hist], w)
+        dmg.setup()
+        bl = top.scatter_global(b)
+        xl = top.new_vector()
+        dmg.vmult(xl, bl)
+        vc = top.gather_global(xl).numpy()
+        if rank == 0:
+            q.put((list(dmg.omega), vc))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_vcycle_agglomerated():
+    """Level agglomeration on the host-driven path at world size 2 (gloo, the
+    oracle as every rank's operator): 2D Turek Re100 r0..r2 with r2
+    partitioned and r0, r1 single-domain on every rank (the coarse_solver
+    protocol glsdist.RedundantBottomMG implements on the GPU) -- the V-cycle
+    of the single-domain three-level hierarchy to 1e-10, the partitioned
+    level's relaxation factor to 1e-10 (the native
+    twin: tests/test_gpu_dist_native.py::test_native_group_vcycle_agglomerated)."""
+    import socket
+    import torch.multiprocessing as mp
+    from mg_ref import OracleGMG
+    name, n_ref, k = "input_turek_2D_Re100.json", 2, 1
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_agglomerated, args=(r, 2, port, name, n_ref, k, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    meshes, cm, params, w, u, hist, b = _hierarchy(name, n_ref)
+    ref = OracleGMG(meshes, cm, params, u, hist, w, coarse_iters=10)
+    ref.setup_omega()
+    vc_ref = ref.vcycle(b)
+    omega, vc = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert abs(omega[-1] - ref.omega[-1]) < 1e-10 * ref.omega[-1], (omega, ref.omega)
+    err = rel_err(vc, vc_ref)
+    print(f"gloo world 2, {k + 1} of {n_ref + 1} levels agglomerated: V-cycle vs single-domain "
+          f"{err:.2e}")
+    assert err < 1e-10
+
+
+@pytest.mark.gpu
+def test_rccl_world1_agglomerated_bottom():
+    """glsdist.RedundantBottomMG on the product path at world 1 (RCCL): the
+    host-driven partitioned multigrid over Re3900 r1..r2 whose coarse solve is
+    the single-domain r0..r1 V-cycle on every rank, against the single-domain
+    r0..r2 GPU V-cycle (FP32 levels)."""
+    import torch
+    import torch.distributed as dist
+    import glsamd
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        meshes, cm, params, w, u, hist, b = _hierarchy("input_hoffmann_3D_Re3900.json", 2)
+        bottom = glsdist.RedundantBottomMG(meshes[:2], cm[:2], "f32", coarse_n_iterations=10)
+        dmg = glsdist.DistributedMultigrid(meshes[1:], cm[1:], "f32", dist, 0, 1,
+                                           coarse_n_iterations=-1, coarse_solver=bottom)
+        top = dmg.levels[-1]
+        dmg.set_linearization_point(params, top.scatter_global(u),
+                                    [top.scatter_global(h) for h in hist], w)
+        dmg.setup()
+        mg, ops = glsamd.build_gmg(meshes, cm, params, u, hist, w, precision="f32",
+                                   coarse_n_iterations=10)
+        wd, lam = mg.relaxation(2)
+        assert abs(dmg.omega[-1] - wd) < 1e-4 * wd, (dmg.omega, wd)
+        bd = torch.from_numpy(b).cuda()
+        x1 = torch.zeros_like(bd)
+        dmg.vmult(x1, top.scatter_global(b).double())
+        x2 = torch.zeros_like(bd)
+        mg.vcycle(x2, bd)
+        torch.cuda.synchronize()
+        err = rel_err(top.gather_global(x1).cpu().numpy(), x2.cpu().numpy())
+        print(f"world 1 host-driven, r0..r1 agglomerated: V-cycle vs single-domain {err:.2e}")
+        assert err < 1e-3  # FP32 levels, different omega rounding (as the test above)
+    finally:
+        dist.destroy_process_group()
