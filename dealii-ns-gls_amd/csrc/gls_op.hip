@@ -2141,6 +2141,46 @@ gls_op_vmult(glsOp op, void *dst, const void *src, void *stream)
   GLS_CATCH
 }
 
+// NavierStokesOperator::vmult_interface_down (operator_ns.cc:734-753): the
+// cell loop over src with dst zeroed, then dst = src on the constrained dofs.
+// The refinement-edge dofs (edge_constrained_indices, .cc:131-152) exist only
+// on locally refined level meshes; every mesh this library takes is a whole
+// level of a globally refined hierarchy, so the set is empty and the result
+// is the vmult's (whose edge save / restore, .cc:691-731, is then a no-op).
+glsStatus
+gls_op_vmult_interface_down(glsOp op, void *dst, const void *src, void *stream)
+{
+  GLS_TRY
+  if (!op || !dst || !src)
+    throw std::runtime_error("gls_op_vmult_interface_down: null argument");
+  if (dst == src)
+    throw std::runtime_error("gls_op_vmult_interface_down: dst and src must not alias");
+  hipStream_t s = (hipStream_t)stream;
+  const void *x = op->stage.in_vec(src, 0, s);
+  void       *y = op->stage.out_vec(dst);
+  gls::op_vmult_device(op, y, x, s);
+  op->stage.finish_out(dst, s);
+  op->stage.done(s);
+  GLS_CATCH
+}
+
+// NavierStokesOperator::vmult_interface_up (operator_ns.cc:755-787): with no
+// edge-constrained dofs (has_edge_constrained_indices == false, above) the
+// reference sets dst = 0 and returns.
+glsStatus
+gls_op_vmult_interface_up(glsOp op, void *dst, const void *src, void *stream)
+{
+  GLS_TRY
+  if (!op || !dst || !src)
+    throw std::runtime_error("gls_op_vmult_interface_up: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  void       *y = op->stage.out_vec(dst);
+  HIP_THROW(hipMemsetAsync(y, 0, (size_t)op->n_dofs * op->tsize(), s));
+  op->stage.finish_out(dst, s);
+  op->stage.done(s);
+  GLS_CATCH
+}
+
 } // extern "C"
 
 // constraints_inhomogeneous.distribute(tmp) on a copy of src (src NULL: a

@@ -25,7 +25,8 @@ GLS_DETERMINISTIC = 8
 EXPORTS = [
     "gls_op_create", "gls_op_destroy", "gls_op_set_parameters", "gls_op_m",
     "gls_op_precision", "gls_op_set_linearization_point", "gls_op_set_previous_solution",
-    "gls_op_vmult", "gls_op_vmult_cells", "gls_op_vmult_init", "gls_op_apply_identity_rows",
+    "gls_op_vmult", "gls_op_vmult_interface_down", "gls_op_vmult_interface_up",
+    "gls_op_vmult_cells", "gls_op_vmult_init", "gls_op_apply_identity_rows",
     "gls_op_evaluate_residual", "gls_op_evaluate_residual_plain", "gls_op_evaluate_rhs",
     "gls_op_set_constraint_values", "gls_gmres_solve",
     "gls_op_compute_inverse_diagonal", "gls_op_upload_tables", "gls_op_download_tables",
@@ -136,6 +137,8 @@ def lib():
         L.gls_op_set_linearization_point.argtypes = [vp, vp, vp]
         L.gls_op_set_previous_solution.argtypes = [vp, vp, C.c_int, vp, vp]
         L.gls_op_vmult.argtypes = [vp, vp, vp, vp]
+        L.gls_op_vmult_interface_down.argtypes = [vp, vp, vp, vp]
+        L.gls_op_vmult_interface_up.argtypes = [vp, vp, vp, vp]
         L.gls_op_vmult_cells.argtypes = [vp, vp, vp, i64, i64, vp]
         L.gls_op_vmult_init.argtypes = [vp, vp, vp, vp]
         L.gls_op_apply_identity_rows.argtypes = [vp, vp, vp, vp]
@@ -446,6 +449,18 @@ class NavierStokesOperator:
     def Tvmult(self, dst, src):
         """OperatorBase::Tvmult forwards to vmult (operator_base.cc:12-18)."""
         self.vmult(dst, src)
+
+    def vmult_interface_down(self, dst, src):
+        """OperatorBase::vmult_interface_down (operator_ns.cc:734-753): on a
+        globally refined level (no refinement-edge dofs) the vmult."""
+        _check(lib().gls_op_vmult_interface_down(self.h, _vptr(dst), _vptr(src), _stream()))
+        return dst
+
+    def vmult_interface_up(self, dst, src):
+        """OperatorBase::vmult_interface_up (operator_ns.cc:755-787): dst = 0
+        without refinement-edge dofs (has_edge_constrained_indices false)."""
+        _check(lib().gls_op_vmult_interface_up(self.h, _vptr(dst), _vptr(src), _stream()))
+        return dst
 
     def invalidate_system(self):
         """OperatorBase::invalidate_system (operator_ns.cc:229-232): the

@@ -22,6 +22,12 @@
  *                                      operator_base.h:32-33, operator_ns.cc:234-320
  *   gls_op_vmult                     OperatorBase::vmult
  *                                      operator_base.h:45-46, operator_ns.cc:684-732
+ *   gls_op_vmult_interface_down /
+ *   gls_op_vmult_interface_up        OperatorBase::vmult_interface_down / _up
+ *                                      operator_base.h:51-58, operator_ns.cc:734-787
+ *                                      (local-smoothing interface matrices;
+ *                                      globally refined levels: down = vmult,
+ *                                      up = 0)
  *   gls_op_vmult_init /
  *   gls_op_vmult_cells /
  *   gls_op_apply_identity_rows       the pieces of vmult around the ghost
@@ -212,6 +218,15 @@ glsStatus gls_op_set_previous_solution(glsOp op, const void *const *history,
                                        void *stream);
 
 glsStatus gls_op_vmult(glsOp op, void *dst, const void *src, void *stream);
+/* the local-smoothing interface matrices of OperatorBase (operator_ns.cc:
+ * 734-787).  Their edge-constrained dofs (operator_ns.cc:131-152) sit on the
+ * refinement edges of a locally refined level; the meshes this library takes
+ * are whole levels of a globally refined hierarchy, where that set is empty:
+ * interface_down is then the vmult (cell loop, dst = src on the constrained
+ * dofs) and interface_up sets dst = 0 -- what the reference computes on such
+ * a mesh.  Same vector layout and errors as gls_op_vmult. */
+glsStatus gls_op_vmult_interface_down(glsOp op, void *dst, const void *src, void *stream);
+glsStatus gls_op_vmult_interface_up(glsOp op, void *dst, const void *src, void *stream);
 /* cells [cell_begin, cell_end): dst += cell contributions (no zeroing) */
 glsStatus gls_op_vmult_cells(glsOp op, void *dst, const void *src,
                              int64_t cell_begin, int64_t cell_end,

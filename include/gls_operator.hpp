@@ -185,6 +185,20 @@ public:
     vmult(dst, src, stream);
   }
 
+  // OperatorBase::vmult_interface_down / _up (operator_ns.cc:734-787); on the
+  // globally refined levels this library takes: the vmult / zero
+  void
+  vmult_interface_down(void *dst, const void *src, void *stream = nullptr) const
+  {
+    check(gls_op_vmult_interface_down(h, dst, src, stream), "vmult_interface_down");
+  }
+
+  void
+  vmult_interface_up(void *dst, const void *src, void *stream = nullptr) const
+  {
+    check(gls_op_vmult_interface_up(h, dst, src, stream), "vmult_interface_up");
+  }
+
   // OperatorBase::get_system_matrix (operator_ns.cc:1407-1430) as CSR over
   // the node-major dofs; constrained rows / columns carry their unit diagonal
   struct SparseMatrix

@@ -61,6 +61,32 @@ def test_get_max_u(prec):
         assert abs(got - ref) < (1e-13 if prec == "f64" else 1e-6) * ref
 
 
+@pytest.mark.parametrize("layout", ["device", "host"])
+def test_vmult_interface_down_up(layout):
+    """vmult_interface_down / _up (operator_ns.cc:734-787) on a globally
+    refined level, where no dof sits on a refinement edge: down is the vmult
+    (the oracle's, identity rows included), up overwrites dst with zeros."""
+    import torch
+    case = deck_case("input_hoffmann_3D_Re3900.json", 1)
+    ref = case.oracle().vmult(case.src)
+    op = case.gpu("f64")
+    if layout == "host":
+        op.set_vector_layout("host", None)
+        src, down, up = case.src.copy(), np.full(case.n_dofs, 7.0), np.full(case.n_dofs, 7.0)
+        op.vmult_interface_down(down, src)
+        op.vmult_interface_up(up, src)
+    else:
+        src = op._dev(case.src)
+        down = op.initialize_dof_vector().fill_(7.0)
+        up = op.initialize_dof_vector().fill_(7.0)
+        op.vmult_interface_down(down, src)
+        op.vmult_interface_up(up, src)
+        torch.cuda.synchronize()
+        down, up = down.cpu().numpy(), up.cpu().numpy()
+    assert rel_err(down, ref) < 1e-12
+    assert not np.any(up)
+
+
 def test_multigrid_and_gmres_host_permuted():
     import torch
     import glsamd
