@@ -1,0 +1,1 @@
+bash scripts/gpu_run.sh r6h py:scripts/clock_probe.py
