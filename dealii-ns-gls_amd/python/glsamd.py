@@ -222,7 +222,15 @@ def _check(rc):
 
 
 def _stream():
+    """torch's current stream on the current device, as the C ABI's stream
+    argument.  torch._C._cuda_getCurrentRawStream returns the handle without
+    building a Stream object (3.0 us per call on the box for the public
+    form, profiles/r06/explore/host_overhead.txt); the public form where it
+    is absent."""
     import torch
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if raw is not None:
+        return C.c_void_p(raw(torch.cuda.current_device()))
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 

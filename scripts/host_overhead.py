@@ -58,6 +58,9 @@ def main():
     out = {"call_us": busy_cpu(lambda: op.vmult(dst, src)),
            "parts_us": {
                "current_stream": busy_cpu(lambda: torch.cuda.current_stream().cuda_stream, 200),
+               "raw_stream": busy_cpu(lambda: torch._C._cuda_getCurrentRawStream(
+                   torch.cuda.current_device()), 200),
+               "glsamd_stream": busy_cpu(glsamd._stream, 200),
                "two_data_ptr": busy_cpu(lambda: (dst.data_ptr(), src.data_ptr()), 200),
                "c_abi_call": busy_cpu(lambda: lib.gls_op_vmult(h, pd, ps, sp)),
                "event_record": busy_cpu(lambda: torch.cuda.Event(enable_timing=True).record(),
