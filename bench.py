@@ -736,6 +736,10 @@ def main():
                     help="launch plumbing only (gloo, no GPU): the CPU test of --gpus N")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle-ms", type=float, default=200.0,
+                    help="untimed back-to-back steps for about this long before the W "
+                         "warm-up steps, so the timed region runs at the sustained clock "
+                         "(0: off; reported as 'settle' in the line)")
     ap.add_argument("--nref", type=int, default=None)
     ap.add_argument("--precision", default="f64")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -885,6 +889,30 @@ def main():
         region_events = True
 
     torch.cuda.synchronize()
+    # clock settle, untimed, before the W warm-up steps: after the setup's
+    # seconds of GPU idleness the first ~20 ms of vmults run at a lower clock
+    # (profiles/r06/explore/clock_probe.txt: 38.6 -> 34.2 us per step over 600
+    # back-to-back vmults after 3 s idle; this loop's W + K pattern 36.1-36.5
+    # us with no settle, 33.1-33.8 us after 100 ms of vmults).  A solver runs
+    # the operator at the sustained clock.  Every rank runs the same number of
+    # steps (the partitioned step is collective): ten timed steps, then the
+    # count for settle_ms from the slowest rank.
+    settle = None
+    if args.settle_ms > 0:
+        t_settle = time.perf_counter()
+        for _ in range(10):
+            apply_fn()
+        torch.cuda.synchronize()
+        per = torch.tensor([(time.perf_counter() - t_settle) / 10], dtype=torch.float64,
+                           device="cuda")
+        if dist is not None:
+            dist.all_reduce(per, op=dist.ReduceOp.MAX)
+        n_settle = 10 + max(0, int(args.settle_ms * 1e-3 / max(float(per.item()), 1e-6)) - 10)
+        for _ in range(n_settle - 10):
+            apply_fn()
+        torch.cuda.synchronize()
+        settle = {"steps": n_settle, "ms": (time.perf_counter() - t_settle) * 1e3,
+                  "target_ms": args.settle_ms}
     for _ in range(args.warmup):
         apply_fn()
     torch.cuda.synchronize()
@@ -1014,6 +1042,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            # untimed steps before the warm-up (the sustained clock, see above)
+            "settle": settle,
             "ms_per_step": ms,
             "higher_is_better": True,
             "scaling": "strong",

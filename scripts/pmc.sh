@@ -9,7 +9,7 @@ i=0
 while read -r counters; do
   [ -z "$counters" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $counters --output-format csv -d gpurun_out/pmc/p$i -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-companions ${BENCH_ARGS:-} > gpurun_out/pmc/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $counters --output-format csv -d gpurun_out/pmc/p$i -o run -- python3 bench.py --steps 10 --warmup 2 --settle-ms 0 --no-cpu-baseline --no-companions ${BENCH_ARGS:-} > gpurun_out/pmc/p$i.log 2>&1
   rc=$?; echo "pass $i ($counters) rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done <<'LIST'
