@@ -63,7 +63,7 @@ def main():
             if settle:
                 t0 = time.perf_counter()
                 n = 0
-                while (time.perf_counter() - t0) * 1e3 < SETTLE_MS:
+                while (time.perf_counter() - t0) * 1e3 < SETTLE_MS:  # noqa: F821
                     for _ in range(20):
                         op.vmult(dst, src)
                     n += 20
@@ -83,8 +83,15 @@ def main():
                         "events_us_per_step": round(e0.elapsed_time(e1) * 1e3 / K, 2)})
         return res
 
-    out["bench_pattern"] = pattern(False)
-    out["bench_settled"] = pattern(True)
+    global SETTLE_MS
+    if len(sys.argv) > 1:
+        # settle lengths to compare: bench's pattern after each
+        for ms in (float(x) for x in sys.argv[1].split(",")):
+            SETTLE_MS = ms
+            out[f"bench_settled_{int(ms)}ms"] = pattern(ms > 0)
+    else:
+        out["bench_pattern"] = pattern(False)
+        out["bench_settled"] = pattern(True)
     print(json.dumps(out, indent=1))
 
 
