@@ -56,14 +56,14 @@ def main():
     out["chain_after_idle_us_per_step"] = [round(evs[r].elapsed_time(evs[r + 1]) * 1e3 / K, 2)
                                            for r in range(30)]
 
-    def pattern(settle):
+    def pattern(settle, settle_ms=SETTLE_MS):
         res = []
         for _ in range(REPS):
             time.sleep(IDLE_S)
             if settle:
                 t0 = time.perf_counter()
                 n = 0
-                while (time.perf_counter() - t0) * 1e3 < SETTLE_MS:  # noqa: F821
+                while (time.perf_counter() - t0) * 1e3 < settle_ms:
                     for _ in range(20):
                         op.vmult(dst, src)
                     n += 20
@@ -83,12 +83,10 @@ def main():
                         "events_us_per_step": round(e0.elapsed_time(e1) * 1e3 / K, 2)})
         return res
 
-    global SETTLE_MS
     if len(sys.argv) > 1:
         # settle lengths to compare: bench's pattern after each
         for ms in (float(x) for x in sys.argv[1].split(",")):
-            SETTLE_MS = ms
-            out[f"bench_settled_{int(ms)}ms"] = pattern(ms > 0)
+            out[f"bench_settled_{int(ms)}ms"] = pattern(ms > 0, ms)
     else:
         out["bench_pattern"] = pattern(False)
         out["bench_settled"] = pattern(True)
