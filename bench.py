@@ -919,17 +919,23 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    # the opening event is enqueued before the clock starts (instrumentation,
-    # ~5 us of host time per record; the GPU stamps it at once, idle, so the
-    # region events still span the whole first step)
+    # region events (instrumentation: created and the opening one enqueued
+    # before the clock starts -- creating and recording them inside it cost
+    # ~50 us of host time per region, profiles/r06/explore/sync_probe.txt).
+    # ev_region[0]: stamped at once (idle GPU), so [0]..[2] also holds the
+    # first step's launch from an idle queue; ev_region[1]: after step 1, when
+    # the host is ahead of the GPU, so [1]..[2] holds steps 2..K back to back
+    # -- the kernels' own average duration, what rocprofv3 averages
     if region_events:
-        ev_region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev_region = tuple(torch.cuda.Event(enable_timing=True) for _ in range(3))
         ev_region[0].record()
     t_start = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         apply_fn()
+        if region_events and i == 0:
+            ev_region[1].record()
     if region_events:
-        ev_region[1].record()
+        ev_region[2].record()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -943,8 +949,8 @@ def main():
 
     # average duration of the dominant kernel pair (k_brick + reduce), HIP
     # events on the stream it is launched on (torch's current stream): single
-    # GPU, the events around the timed region / K (the vmults back to back, as
-    # rocprofv3 sees them); partitioned, the rank-local cell loop between its
+    # GPU, the region events after step 1 / (K - 1) (the vmults back to back,
+    # as rocprofv3 sees them); partitioned, the rank-local cell loop between its
     # own events.  kernel_ms_event_pairs: one event pair around each of K more
     # vmults (the event packets between the launches add ~3 us per vmult)
     kernel_ms = kernel_ms_pairs = None
@@ -956,8 +962,11 @@ def main():
         torch.cuda.synchronize()
         kernel_ms_pairs = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
         kernel_ms = kernel_ms_pairs
+    kernel_ms_region = None
     if region_events:
-        kernel_ms = ev_region[0].elapsed_time(ev_region[1]) / args.steps
+        kernel_ms_region = ev_region[0].elapsed_time(ev_region[2]) / args.steps
+        kernel_ms = (ev_region[1].elapsed_time(ev_region[2]) / (args.steps - 1)
+                     if args.steps > 1 else kernel_ms_region)
 
     dist_comp = None
     if use_dist and not args.no_companions:
@@ -1065,6 +1074,8 @@ def main():
                          "kernel": "vmult = gls::k_brick<3,2,double,MODE_NEWTON> + "
                                    "gls::k_shared_reduce_cls (both inside the events)",
                          "kernel_ms": kernel_ms, "kernel_ms_event_pairs": kernel_ms_pairs,
+                         # the whole region / K (first launch from an idle queue included)
+                         "kernel_ms_region": kernel_ms_region,
                          "algorithmic_bytes": bytes_per_vmult,
                          "streamed_bytes": op.vmult_bytes(),
                          # the same launch time against what the kernel reads
