@@ -16,7 +16,8 @@ HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics \
             -Wall -Wno-unused-parameter -Wno-unused-function
 
 # rocsolver/rocblas: dense LU of the coarse multigrid level only; rccl: ghost exchange
-AMD_LIBS := -L/opt/rocm/lib -lrocsolver -lrocblas -lrccl -Wl,-rpath,/opt/rocm/lib
+# rocprofiler-sdk-roctx: the timer sections' roctx ranges (trace.cc)
+AMD_LIBS := -L/opt/rocm/lib -lrocsolver -lrocblas -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
 
 MESH_SRC := $(PKG)/host/mesh.cc
 AMD_SRC  := $(wildcard $(PKG)/csrc/*.hip) $(wildcard $(PKG)/csrc/*.cc)

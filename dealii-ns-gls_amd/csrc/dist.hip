@@ -41,6 +41,7 @@
 // group from one thread in lockstep on one stream.
 #include "../../include/gls_op.h"
 #include "common.h"
+#include "trace.h"
 #include "kernels.h"
 #include "op_internal.h"
 
@@ -832,6 +833,7 @@ glsStatus
 gls_dist_vmult(glsDist d, void *dst, void *src, void *stream)
 {
   GLS_TRY
+  gls::Section sec_("ns::vmult", (hipStream_t)stream);
   dist_vmult(d, dst, src, (hipStream_t)stream, nullptr);
   GLS_CATCH
 }

@@ -28,6 +28,7 @@
 #include "../../include/gls_op.h"
 #include "cgs.h"
 #include "common.h"
+#include "trace.h"
 #include "op_internal.h"
 
 #include <rocblas/rocblas.h>
@@ -918,6 +919,7 @@ gls_dist_mg_vcycle(glsDistMG const *team, int n, void *const *dst, const void *c
                    void *stream)
 {
   GLS_TRY
+  gls::Section sec_("gmg::vmult", (hipStream_t)stream);
   Team        t = make_team(team, n);
   hipStream_t s = (hipStream_t)stream;
   if (!dst || !src)
@@ -972,6 +974,7 @@ gls_dist_gmres_solve(glsDist const *A, glsDistMG const *mg, int n, const glsGMRE
                      void *const *x, const void *const *b, glsGMRESResult *result, void *stream)
 {
   GLS_TRY
+  gls::Section sec_("gmres::solve", (hipStream_t)stream);
   if (!A || !desc || !x || !b || n < 1 || n > TEAM_MAX)
     throw std::runtime_error("gls_dist_gmres_solve: bad arguments");
   if (desc->max_n_tmp_vectors < 3)

@@ -5,6 +5,7 @@
 #include "../../include/gls_op.h"
 #include "brick.h"
 #include "common.h"
+#include "trace.h"
 #include "kernels.h"
 #include "op_internal.h"
 
@@ -2006,6 +2007,7 @@ glsStatus
 gls_op_set_linearization_point(glsOp op, const void *vec, void *stream)
 {
   GLS_TRY
+  gls::Section sec_("ns::set_linearization_point", (hipStream_t)stream);
   if (!op || !vec)
     throw std::runtime_error("gls_op_set_linearization_point: null argument");
   ApplyFn     af;
@@ -2027,6 +2029,7 @@ gls_op_set_previous_solution(glsOp op, const void *const *hist, int n_hist,
                              const double *weights, void *stream)
 {
   GLS_TRY
+  gls::Section sec_("ns::set_previous_solution", (hipStream_t)stream);
   if (!op)
     throw std::runtime_error("gls_op_set_previous_solution: null operator");
   const int order = op->prm.order;
@@ -2128,6 +2131,7 @@ glsStatus
 gls_op_vmult(glsOp op, void *dst, const void *src, void *stream)
 {
   GLS_TRY
+  gls::Section sec_("ns::vmult", (hipStream_t)stream);
   if (!op || !dst || !src)
     throw std::runtime_error("gls_op_vmult: null argument");
   if (dst == src)
@@ -2151,6 +2155,7 @@ glsStatus
 gls_op_vmult_interface_down(glsOp op, void *dst, const void *src, void *stream)
 {
   GLS_TRY
+  gls::Section sec_("ns::vmult_interface_down", (hipStream_t)stream);
   if (!op || !dst || !src)
     throw std::runtime_error("gls_op_vmult_interface_down: null argument");
   if (dst == src)
@@ -2171,6 +2176,7 @@ glsStatus
 gls_op_vmult_interface_up(glsOp op, void *dst, const void *src, void *stream)
 {
   GLS_TRY
+  gls::Section sec_("ns::vmult_interface_up", (hipStream_t)stream);
   if (!op || !dst || !src)
     throw std::runtime_error("gls_op_vmult_interface_up: null argument");
   hipStream_t s = (hipStream_t)stream;
@@ -2275,6 +2281,7 @@ glsStatus
 gls_op_evaluate_rhs(glsOp op, void *dst, void *stream)
 {
   GLS_TRY
+  gls::Section sec_("ns::evaluate_rhs", (hipStream_t)stream);
   if (!op || !dst)
     throw std::runtime_error("gls_op_evaluate_rhs: null argument");
   if (!op->have_lin)
@@ -2292,6 +2299,7 @@ glsStatus
 gls_op_evaluate_residual(glsOp op, void *dst, const void *src, void *stream)
 {
   GLS_TRY
+  gls::Section sec_("ns::evaluate_residual", (hipStream_t)stream);
   if (!op || !dst || !src || dst == src)
     throw std::runtime_error("gls_op_evaluate_residual: bad arguments");
   if (!op->have_lin)
@@ -2311,6 +2319,7 @@ glsStatus
 gls_op_evaluate_residual_plain(glsOp op, void *dst, const void *src, void *stream)
 {
   GLS_TRY
+  gls::Section sec_("ns::evaluate_residual", (hipStream_t)stream);
   if (!op || !dst || !src || dst == src)
     throw std::runtime_error("gls_op_evaluate_residual_plain: bad arguments");
   if (!op->have_lin)
@@ -2383,6 +2392,7 @@ glsStatus
 gls_op_compute_inverse_diagonal(glsOp op, void *diag_, void *stream)
 {
   GLS_TRY
+  gls::Section sec_("ns::compute_inverse_diagonal", (hipStream_t)stream);
   if (!op || !diag_)
     throw std::runtime_error("gls_op_compute_inverse_diagonal: null argument");
   hipStream_t s = (hipStream_t)stream;
@@ -2667,6 +2677,7 @@ glsStatus
 gls_op_system_matrix(glsOp op, int64_t *nnz, int64_t *row_ptr, int64_t *cols, double *vals)
 {
   GLS_TRY
+  gls::Section sec_("ns::initialize_system_matrix", nullptr);
   if (!op || !nnz)
     throw std::runtime_error("gls_op_system_matrix: null argument");
   if (op->n_owned_nodes != op->n_nodes)

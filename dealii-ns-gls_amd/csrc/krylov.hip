@@ -18,6 +18,7 @@
 #include "../../include/gls_op.h"
 #include "cgs.h"
 #include "common.h"
+#include "trace.h"
 #include "op_internal.h"
 
 #include <rocblas/rocblas.h>
@@ -96,6 +97,7 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
                 glsGMRESResult *result, void *stream)
 {
   GLS_TRY
+  gls::Section sec_("gmres::solve", (hipStream_t)stream);
   if (!op || !desc || !x_ || !b_)
     throw std::runtime_error("gls_gmres_solve: null argument");
   if (op->prec != GLS_F64)
@@ -196,7 +198,10 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   auto    zcol = [&](int j) { return zkeep ? Zd + (size_t)j * n : z.d(); };
   auto precondition = [&](double *dst, const double *src) {
     if (mg)
-      gls::mg_vcycle_device(mg, dst, src, s);
+      {
+        gls::Section sc("gmg::vmult", s);
+        gls::mg_vcycle_device(mg, dst, src, s);
+      }
     else
       HIP_THROW(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, s));
   };
@@ -247,7 +252,10 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
                     (!mg || gls::mg_is_linear(mg)) && m + 1 < CGS_MAXJ;
   auto              arnoldi       = [&](int j) {
     precondition(zcol(j), vcol(j));
-    gls::op_vmult_device(op, w.d(), zcol(j), s);
+    {
+      gls::Section sc("ns::vmult", s);
+      gls::op_vmult_device(op, w.d(), zcol(j), s);
+    }
     double *hn        = dh.d() + 2 * (m + 1);
     bool    unit_done = false;
     if (j + 1 < CGS_MAXJ && !force_rocblas && !force_three_pass)
@@ -337,7 +345,10 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
   };
   auto arnoldi_d = [&](int j) {
     precondition(zcol(j), vcol(j));
-    gls::op_vmult_device(op, w.d(), zcol(j), s);
+    {
+      gls::Section sc("ns::vmult", s);
+      gls::op_vmult_device(op, w.d(), zcol(j), s);
+    }
     double *dd = dh.d();
     dcgs_dots(j, (const double *)vcol(j), (const double *)w.d());
     hipLaunchKernelGGL(k_dcgs_finish, dim3(DCGS_W), dim3(256), 0, s, (const double *)cpart.d(),
@@ -565,7 +576,10 @@ gls_gmres_solve(glsOp op, glsMG mg, const glsGMRESDesc *desc, void *x_, const vo
         break;
       // restart: true residual r = b - A x into column 0
       ++n_rst;
-      gls::op_vmult_device(op, vcol(0), x, s);
+      {
+        gls::Section sc("ns::vmult", s);
+        gls::op_vmult_device(op, vcol(0), x, s);
+      }
       hipLaunchKernelGGL(k_residual, grid1(n), dim3(256), 0, s, vcol(0), b, n);
       HIP_THROW(hipGetLastError());
       res  = nrm2(vcol(0));

@@ -17,6 +17,7 @@
 #include "kernels.h"
 #include "op_internal.h"
 #include "cgs.h"
+#include "trace.h"
 
 #include <chrono>
 #include <string>
@@ -27,6 +28,7 @@
 #include <algorithm>
 #include <type_traits>
 #include <cmath>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -609,6 +611,9 @@ copy_words(void *y, const void *x, int64_t n_words, hipStream_t s)
 struct glsMG_
 {
   glsMGDesc          desc{};
+  // timer-section names of the V-cycle phases per level (multigrid.cc:550-583:
+  // gmg::vmult::level_<l>::<phase>; [l][5] = the coarse solve's plain name)
+  std::vector<std::vector<std::string>> sec;
   std::vector<glsOp> ops;
   int                prec = GLS_F32, dim = 3, degree = 2, nc = 4;
   std::vector<uint32_t *> d_child;  // level l >= 1: [cells(l-1)][nl]
@@ -2283,8 +2288,10 @@ v_step(glsMG_ *mg, int l, hipStream_t s)
 void
 v_step_body(glsMG_ *mg, int l, hipStream_t s)
 {
+  const std::vector<std::string> &sec = mg->sec[(size_t)l];
   if (l == 0 && mg->desc.coarse_iterate)
     {
+      gls::Section sc(sec[5], s);
       if (mg->prec == GLS_F64)
         coarse_gmres_t<double>(mg, s);
       else
@@ -2305,6 +2312,7 @@ v_step_body(glsMG_ *mg, int l, hipStream_t s)
   }(l);
   if (l == 0)
     {
+      gls::Section  sc(sec[5], s);
       PendingReduce pc;
       coarse_apply(mg, s, pro_ok ? &pc : nullptr);
       hand_over(0, pc);
@@ -2319,16 +2327,21 @@ v_step_body(glsMG_ *mg, int l, hipStream_t s)
   fr.zero_words = (int64_t)((size_t)mg->ops[l - 1]->n_dofs * mg->ts() / 4);
   fr.b64        = l == (int)mg->ops.size() - 1 ? mg->top_b64 : nullptr;
   PendingReduce pend;
-  const bool folded = smooth(mg, l, mg->sol[l], mg->def[l], true, nit, s, false, &fr, &pend);
-  if (!folded && fr.b64)
-    {
-      const int64_t n = mg->ops[l]->n_dofs;
-      hipLaunchKernelGGL((k_convert<double, float>), g1(n), dim3(256), 0, s,
-                         (float *)mg->def[l], fr.b64, n);
-      HIP_THROW(hipGetLastError());
-    }
+  bool          folded;
+  {
+    gls::Section sc(sec[0], s);
+    folded = smooth(mg, l, mg->sol[l], mg->def[l], true, nit, s, false, &fr, &pend);
+    if (!folded && fr.b64)
+      {
+        const int64_t n = mg->ops[l]->n_dofs;
+        hipLaunchKernelGGL((k_convert<double, float>), g1(n), dim3(256), 0, s,
+                           (float *)mg->def[l], fr.b64, n);
+        HIP_THROW(hipGetLastError());
+      }
+  }
   // residual t = defect - A solution (fused into the brick vmult's write-out
   // and shared-node reduction for brick operators)
+  std::unique_ptr<gls::Section> sc_res(new gls::Section(sec[1], s));
   if (gls::fused_relax_ok(mg->ops[l]))
     {
       gls::RelaxStep rs;
@@ -2359,30 +2372,40 @@ v_step_body(glsMG_ *mg, int l, hipStream_t s)
       gls::op_vmult_device(mg->ops[l], mg->tmp[l], mg->sol[l], s);
       residual(mg, l, mg->tmp[l], mg->def[l], s);
     }
+  sc_res.reset();
   // restrict
-  if (!folded)
-    {
-      const int64_t w = (int64_t)((size_t)mg->ops[l - 1]->n_dofs * mg->ts() / 4);
-      zero_words(mg->def[l - 1], w, s);
-    }
-  transfer(mg, 1, l, mg->def[l - 1], mg->tmp[l], s);
+  {
+    gls::Section sc(sec[2], s);
+    if (!folded)
+      {
+        const int64_t w = (int64_t)((size_t)mg->ops[l - 1]->n_dofs * mg->ts() / 4);
+        zero_words(mg->def[l - 1], w, s);
+      }
+    transfer(mg, 1, l, mg->def[l - 1], mg->tmp[l], s);
+  }
   mg->rq_level = -1;
   v_step(mg, l - 1, s);
   // prolongate and add the coarse correction; with an odd number of fused
   // smoothing steps to follow it goes out of place into tmp, so the
   // ping-pong ends in sol without a copy
   const bool odd = gls::fused_relax_ok(mg->ops[l]) && nit % 2 == 1;
-  if (odd)
-    transfer(mg, 0, l, mg->tmp[l], mg->sol[l - 1], s, mg->sol[l]);
-  else
-    transfer(mg, 0, l, mg->sol[l], mg->sol[l - 1], s);
+  {
+    gls::Section sc(sec[3], s);
+    if (odd)
+      transfer(mg, 0, l, mg->tmp[l], mg->sol[l - 1], s, mg->sol[l]);
+    else
+      transfer(mg, 0, l, mg->sol[l], mg->sol[l - 1], s);
+  }
   mg->pp_level = -1;
   // post-smoothing (MGSmootherPrecondition::smooth -> step); on the finest
   // level its last step also writes the FP64 result (copy_from_mg folded)
   bool          wrote = false;
   PendingReduce pp;
-  smooth(mg, l, mg->sol[l], mg->def[l], false, nit, s, odd, nullptr, pro_ok ? &pp : nullptr,
-         l == (int)mg->ops.size() - 1 ? mg->top_out64 : nullptr, &wrote);
+  {
+    gls::Section sc(sec[4], s);
+    smooth(mg, l, mg->sol[l], mg->def[l], false, nit, s, odd, nullptr, pro_ok ? &pp : nullptr,
+           l == (int)mg->ops.size() - 1 ? mg->top_out64 : nullptr, &wrote);
+  }
   if (l == (int)mg->ops.size() - 1)
     mg->top_out64_done = wrote;
   hand_over(l, pp);
@@ -2572,6 +2595,13 @@ gls_mg_create(const glsMGDesc *desc, const glsOp *levels, const uint32_t *const 
     }
   mg->omega.assign(nl_levels, 1.0);
   mg->lambda.assign(nl_levels, 0.0);
+  for (int l = 0; l < nl_levels; ++l)
+    {
+      const std::string b = "gmg::vmult::level_" + std::to_string(l);
+      mg->sec.push_back({b + "::0_pre_smoother_step", b + "::1_residual_step",
+                         b + "::2_restriction", b + "::3_prolongation",
+                         b + "::5_post_smoother_step", b});
+    }
   int64_t acc_total = 0;
   for (int l = 0; l < nl_levels; ++l)
     {
@@ -2639,6 +2669,7 @@ gls_mg_setup(glsMG mg, void *stream)
   // on the levels' device; the caller's current device is restored
   gls::DeviceScope dev(mg->ops[0]->device);
   hipStream_t      s  = (hipStream_t)stream;
+  gls::Section     sec_("gmg::initialize", s);
   const size_t     nl = mg->ops.size();
   // the smoother's slot buffers for deferred reductions (smooth)
   for (int q = 0; q < 2; ++q)
@@ -2675,7 +2706,10 @@ gls_mg_setup(glsMG mg, void *stream)
       hipStream_t  ls = mg->side[l];
       HIP_THROW(hipStreamWaitEvent(ls, fork, 0));
       // compute_inverse_diagonal (multigrid.cc:290-293)
-      gls::op_inverse_diagonal_device(mg->ops[l], mg->invdiag[l], ls);
+      {
+        gls::Section sc("gmg::initialize::smoother::init0", ls);
+        gls::op_inverse_diagonal_device(mg->ops[l], mg->invdiag[l], ls);
+      }
       // relaxation = 0: omega from the power-iteration estimate of
       // lambda_max(D^-1 A) (power_iteration_t), estimated on the levels
       // above the coarsest one (multigrid.cc:355-358 with
@@ -2690,6 +2724,7 @@ gls_mg_setup(glsMG mg, void *stream)
         }
       else
         {
+          gls::Section sc("gmg::initialize::smoother::init1", ls);
           if (mg->prec == GLS_F64)
             power_iteration_t<double>(mg, (int)l, ls);
           else
@@ -2731,6 +2766,7 @@ gls_mg_setup(glsMG mg, void *stream)
       // the coarse level's system matrix (FP64, constrained rows / columns
       // identity) and the AMG hierarchy on it
       HIP_THROW(hipStreamSynchronize(s));
+      gls::Section sc("gmg::initialize::amg", s);
       const auto t0   = std::chrono::steady_clock::now();
       glsOp      op0  = mg->ops[0];
       int64_t    nnz  = 0;
@@ -2751,6 +2787,7 @@ gls_mg_setup(glsMG mg, void *stream)
     }
   else if (mg->desc.coarse_n_iterations < 0)
     {
+      gls::Section sc("gmg::initialize::direct", s);
       if (mg->prec == GLS_F64)
         coarse_lu_setup_t<double>(mg, s);
       else
@@ -2781,6 +2818,7 @@ gls_mg_vcycle(glsMG mg, void *dst, const void *src, void *stream)
   if (!mg || !dst || !src)
     throw std::runtime_error("gls_mg_vcycle: null argument");
   hipStream_t s = (hipStream_t)stream;
+  gls::Section sec_("gmg::vmult", s);
   // a stall of an earlier (asynchronous) V-cycle is reported before this one
   // runs; a stall of this one as soon as its flag is visible (host-layout
   // vectors: at return)

@@ -39,6 +39,8 @@ EXPORTS = [
     "gls_dist_get_max_u", "gls_op_compute_diagonal", "gls_op_invert_diagonal", "gls_mg_relax",
     "gls_dist_compress_add", "gls_op_brick_shape", "gls_op_sweep_stats", "gls_op_cell_permutation",
     "gls_op_set_sweep_spin_bound",
+    "gls_timer_enable", "gls_timer_reset", "gls_timer_n_sections", "gls_timer_section",
+    "gls_timer_report",
     "gls_discover_bricks", "gls_mg_coarse_statistics", "gls_mg_coarse_setup_times",
     "gls_amg_create", "gls_amg_destroy", "gls_amg_vmult", "gls_amg_info", "gls_mg_coarse_amg",
     "gls_amg_level_matrix",
@@ -208,12 +210,57 @@ def lib():
         L.gls_dist_gmres_solve.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp]
         L.gls_discover_bricks.argtypes = [C.c_int, C.c_int, i64, vp, vp, vp]
         L.gls_last_error.restype = C.c_char_p
+        L.gls_timer_enable.argtypes = [C.c_int, C.POINTER(C.c_int)]
+        L.gls_timer_reset.argtypes = []
+        L.gls_timer_n_sections.argtypes = []
+        L.gls_timer_n_sections.restype = i64
+        L.gls_timer_section.argtypes = [i64, C.c_char_p, i64, C.POINTER(i64),
+                                        C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.gls_timer_report.argtypes = [C.c_char_p, i64]
+        L.gls_timer_report.restype = i64
         _lib = L
     return _lib
 
 
 class GlsError(RuntimeError):
     pass
+
+
+# ---- timer sections (gls_timer_*: MyTimerOutput / MyScope, timer.h:194-413)
+def timer_enable(on=True):
+    """Tally the library's timer sections (host wall time and GPU time
+    between events on each section's stream); returns the previous state.
+    Sections are roctx ranges either way."""
+    was = C.c_int(0)
+    _check(lib().gls_timer_enable(1 if on else 0, C.byref(was)))
+    return bool(was.value)
+
+
+def timer_reset():
+    _check(lib().gls_timer_reset())
+
+
+def timer_sections():
+    """{name: {"calls", "host_ms", "gpu_ms"}} (gpu_ms None without events);
+    reading waits for the sections' pending events."""
+    L = lib()
+    out = {}
+    name = C.create_string_buffer(256)
+    for i in range(L.gls_timer_n_sections()):
+        calls, hms, gms = C.c_int64(0), C.c_double(0), C.c_double(0)
+        _check(L.gls_timer_section(i, name, 256, C.byref(calls), C.byref(hms), C.byref(gms)))
+        out[name.value.decode()] = {"calls": calls.value, "host_ms": hms.value,
+                                    "gpu_ms": gms.value if gms.value >= 0 else None}
+    return out
+
+
+def timer_report():
+    """The tally as TimerOutput-style text (print_wall_time_statistics)."""
+    L = lib()
+    n = L.gls_timer_report(None, 0)
+    buf = C.create_string_buffer(int(n))
+    L.gls_timer_report(buf, n)
+    return buf.value.decode()
 
 
 def _check(rc):

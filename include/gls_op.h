@@ -53,6 +53,11 @@
  *                                      relaxation smoother (multigrid.cc:281-351),
  *                                      MGTwoLevelTransfer (main.cc:538-563),
  *                                      V-cycle apply (multigrid.cc:202-220)
+ *   gls_timer_*                      MyTimerOutput / MyScope sections and
+ *                                      TimerOutput wall-time statistics
+ *                                      (timer.h:194-338, 342-413): the
+ *                                      reference's section names as roctx
+ *                                      ranges, optional per-section tally
  *
  * Conventions
  *   - Vectors are DEVICE pointers in the operator's precision (double for
@@ -590,6 +595,32 @@ glsStatus gls_dist_gmres_solve(glsDist const *A, glsDistMG const *mg, int n,
 
 
 const char *gls_last_error(void);
+
+/* ---- timer sections (timer.h:194-413 MyTimerOutput / MyScope).  Every
+ * entry point and V-cycle phase opens a section named as the reference's
+ * (ns::vmult, ns::compute_inverse_diagonal, ns::set_linearization_point,
+ * ns::set_previous_solution, ns::evaluate_rhs, ns::evaluate_residual,
+ * ns::vmult_interface_down / _up, ns::initialize_system_matrix,
+ * gmres::solve, gmg::initialize, gmg::initialize::smoother::init0 / init1,
+ * gmg::initialize::direct / amg, gmg::vmult, and per level
+ * gmg::vmult::level_<l>::0_pre_smoother_step / 1_residual_step /
+ * 2_restriction / 3_prolongation / 5_post_smoother_step, gmg::vmult::level_0
+ * for the coarse solve: multigrid.cc:550-583).  A section is always a roctx
+ * range (rocprofv3 --marker-trace shows them); with timing on (this call or
+ * GLS_TIMING=1 in the environment) it also adds its host wall time and the
+ * GPU time between two events on its stream to a process-wide tally.  The
+ * events are read when the tally is (no synchronisation inside the timed
+ * calls).  Sections nest: a V-cycle's time is also inside gmres::solve. */
+glsStatus gls_timer_enable(int on, int *was_on);
+glsStatus gls_timer_reset(void);
+int64_t   gls_timer_n_sections(void);
+/* section i: its name (truncated to name_len - 1 characters), calls, host ms
+ * and GPU ms summed over the calls (-1 when no call had events) */
+glsStatus gls_timer_section(int64_t i, char *name, int64_t name_len, int64_t *calls,
+                            double *host_ms, double *gpu_ms);
+/* the tally as a text table (print_wall_time_statistics); returns the
+ * length needed including the terminating NUL (snprintf semantics) */
+int64_t   gls_timer_report(char *buf, int64_t len);
 
 #ifdef __cplusplus
 }

@@ -42,6 +42,25 @@ check(glsStatus s, const char *what)
     throw Error(std::string(what) + ": " + gls_last_error());
 }
 
+// the library's timer sections (MyTimerOutput, timer.h:194-338): tally on /
+// off (returns the previous state) and TimerOutput-style statistics
+inline bool
+timer_enable(bool on)
+{
+  int was = 0;
+  check(gls_timer_enable(on ? 1 : 0, &was), "timer_enable");
+  return was != 0;
+}
+
+inline std::string
+timer_report()
+{
+  std::string s((size_t)gls_timer_report(nullptr, 0), '\0');
+  gls_timer_report(&s[0], (int64_t)s.size());
+  s.resize(s.size() - 1);
+  return s;
+}
+
 // the scalars NavierStokesOperator / TimeIntegratorData feed the cell kernel
 // (operator_ns.h:102-114, time_integration.h:10-36)
 struct Parameters
