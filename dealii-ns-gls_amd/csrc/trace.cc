@@ -199,6 +199,28 @@ gls_timer_reset(void)
   GLS_CATCH
 }
 
+// caller-opened sections (the reference's MyScope around its own code:
+// newton::solve, richardson::solve, direct::solve, solver_nl.cc / solver_l.cc)
+glsStatus
+gls_timer_begin(const char *name, void *stream, void **token)
+{
+  GLS_TRY
+  if (!name || !token)
+    throw std::runtime_error("gls_timer_begin: null argument");
+  *token = new gls::Section(name, (hipStream_t)stream);
+  GLS_CATCH
+}
+
+glsStatus
+gls_timer_end(void *token)
+{
+  GLS_TRY
+  if (!token)
+    throw std::runtime_error("gls_timer_end: null token");
+  delete static_cast<gls::Section *>(token);
+  GLS_CATCH
+}
+
 int64_t
 gls_timer_n_sections(void)
 {

@@ -40,7 +40,7 @@ EXPORTS = [
     "gls_dist_compress_add", "gls_op_brick_shape", "gls_op_sweep_stats", "gls_op_cell_permutation",
     "gls_op_set_sweep_spin_bound",
     "gls_timer_enable", "gls_timer_reset", "gls_timer_n_sections", "gls_timer_section",
-    "gls_timer_report",
+    "gls_timer_report", "gls_timer_begin", "gls_timer_end",
     "gls_discover_bricks", "gls_mg_coarse_statistics", "gls_mg_coarse_setup_times",
     "gls_amg_create", "gls_amg_destroy", "gls_amg_vmult", "gls_amg_info", "gls_mg_coarse_amg",
     "gls_amg_level_matrix",
@@ -216,6 +216,8 @@ def lib():
         L.gls_timer_n_sections.restype = i64
         L.gls_timer_section.argtypes = [i64, C.c_char_p, i64, C.POINTER(i64),
                                         C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.gls_timer_begin.argtypes = [C.c_char_p, vp, C.POINTER(vp)]
+        L.gls_timer_end.argtypes = [vp]
         L.gls_timer_report.argtypes = [C.c_char_p, i64]
         L.gls_timer_report.restype = i64
         _lib = L
@@ -252,6 +254,35 @@ def timer_sections():
         out[name.value.decode()] = {"calls": calls.value, "host_ms": hms.value,
                                     "gpu_ms": gms.value if gms.value >= 0 else None}
     return out
+
+
+class timer_scope:
+    """MyScope (timer.h:342-413) around the caller's own code: a timer
+    section (roctx range; tallied when timing is on) on torch's current
+    stream, e.g. `with glsamd.timer_scope("newton::solve"): ...`."""
+
+    def __init__(self, name, stream=None):
+        self.name, self.stream = name.encode(), stream
+        self.tok = C.c_void_p()
+
+    def __enter__(self):
+        s = self.stream if self.stream is not None else _stream_or_null()
+        _check(lib().gls_timer_begin(self.name, s, C.byref(self.tok)))
+        return self
+
+    def __exit__(self, *exc):
+        _check(lib().gls_timer_end(self.tok))
+        return False
+
+
+def _stream_or_null():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return _stream()
+    except ImportError:
+        pass
+    return None
 
 
 def timer_report():

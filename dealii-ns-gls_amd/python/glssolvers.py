@@ -56,6 +56,10 @@ class NonLinearSolverNewton(NonLinearSolverBase):
         self.newton_max_iteration = newton_max_iteration
 
     def solve(self, solution):
+        with glsamd.timer_scope("newton::solve"):  # solver_nl.cc:38
+            return self._solve(solution)
+
+    def _solve(self, solution):
         import torch
         rhs = torch.zeros_like(solution)
         inc = torch.zeros_like(solution)

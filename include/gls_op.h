@@ -612,6 +612,11 @@ const char *gls_last_error(void);
  * events are read when the tally is (no synchronisation inside the timed
  * calls).  Sections nest: a V-cycle's time is also inside gmres::solve. */
 glsStatus gls_timer_enable(int on, int *was_on);
+/* a section around the caller's own code (MyScope in solver_nl.cc /
+ * solver_l.cc: newton::solve, ...): begin returns a token, end closes it;
+ * sections close in reverse order of opening (roctx ranges nest) */
+glsStatus gls_timer_begin(const char *name, void *stream, void **token);
+glsStatus gls_timer_end(void *token);
 glsStatus gls_timer_reset(void);
 int64_t   gls_timer_n_sections(void);
 /* section i: its name (truncated to name_len - 1 characters), calls, host ms

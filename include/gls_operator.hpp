@@ -52,6 +52,23 @@ timer_enable(bool on)
   return was != 0;
 }
 
+// MyScope (timer.h:342-413) for the caller's code: a timer section for the
+// lifetime of the object
+class Scope
+{
+public:
+  explicit Scope(const char *name, void *stream = nullptr)
+  {
+    check(gls_timer_begin(name, stream, &token), "timer Scope");
+  }
+  ~Scope() { (void)gls_timer_end(token); }
+  Scope(const Scope &)            = delete;
+  Scope &operator=(const Scope &) = delete;
+
+private:
+  void *token = nullptr;
+};
+
 inline std::string
 timer_report()
 {
@@ -398,6 +415,7 @@ public:
   int
   solve(VectorType &solution) const override
   {
+    Scope      scope("newton::solve"); // solver_nl.cc:38
     VectorType rhs(solution), inc(solution);
     rhs.reinit(solution);
     inc.reinit(solution);

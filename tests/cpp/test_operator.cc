@@ -522,7 +522,8 @@ run(int argc, char **argv)
   const bool timed = rep.find("ns::vmult ") != std::string::npos &&
                      (gm_its == 0 ||
                       (rep.find("gmres::solve ") != std::string::npos &&
-                       rep.find("gmg::vmult::level_1::0_pre_smoother_step") != std::string::npos));
+                       rep.find("gmg::vmult::level_1::0_pre_smoother_step") != std::string::npos)) &&
+                     (n_newton == 0 || rep.find("newton::solve ") != std::string::npos);
   // 1/d amplifies the round-off of near-cancelling diagonal entries:
   // 10x the FP64 bound, as tests/test_gpu_parity.py
   return (timed && e0 < 1e-12 && e1 < 1e-12 && e2 < 1e-11 && e3 < 1e-12 && e4 < 1e-12 && e5 < 1e-11 &&

@@ -15,3 +15,23 @@ def test_timer_abi_cpu():
         assert glsamd.timer_enable(False) is False
     finally:
         glsamd.timer_enable(was)
+
+
+def test_timer_scope_cpu():
+    """A caller-opened section (MyScope: gls_timer_begin / _end) is tallied
+    under its name, nested sections separately."""
+    was = glsamd.timer_enable(True)
+    try:
+        glsamd.timer_reset()
+        with glsamd.timer_scope("newton::solve"):
+            with glsamd.timer_scope("direct::solve"):
+                pass
+        with glsamd.timer_scope("newton::solve"):
+            pass
+        t = glsamd.timer_sections()
+        assert t["newton::solve"]["calls"] == 2 and t["direct::solve"]["calls"] == 1
+        assert t["newton::solve"]["host_ms"] >= t["direct::solve"]["host_ms"] >= 0
+        assert "newton::solve" in glsamd.timer_report()
+    finally:
+        glsamd.timer_enable(was)
+        glsamd.timer_reset()
