@@ -23,7 +23,10 @@ MESH_SRC := $(PKG)/host/mesh.cc
 AMD_SRC  := $(wildcard $(PKG)/csrc/*.hip) $(wildcard $(PKG)/csrc/*.cc)
 AMD_HDR  := $(wildcard $(PKG)/csrc/*.h) $(wildcard $(PKG)/csrc/*.inc) $(wildcard $(PKG)/csrc/*.cuh) include/gls_op.h
 
-all: mesh amd oracle cpptest
+all: mesh amd oracle cpptest tools
+
+tools: $(LIBDIR)/libglsamd.so $(LIBDIR)/libglsmesh.so
+	$(MAKE) -C tools all
 
 mesh: $(LIBDIR)/libglsmesh.so
 amd: $(LIBDIR)/libglsamd.so
@@ -62,5 +65,5 @@ clean:
 	rm -rf $(OBJDIR)
 	$(MAKE) -C oracle clean
 
-.PHONY: all mesh amd oracle cpptest clean
+.PHONY: all mesh amd oracle cpptest tools clean
 
