@@ -391,16 +391,21 @@ delta_otf()
 // the table fields a brick vmult / residual of MODE streams: Newton U, grad U,
 // T1 and h (or delta_1/2); fixed-point U and delta_1/2; residual also
 // Ut_old.  Groups of 16 bytes with none of these are not loaded.
+// (GLS_EXP_NO_UGU: timing-only build that skips U and grad U -- wrong
+// results; the bound on what recomputing them in the kernel could gain)
+#ifndef GLS_EXP_NO_UGU
+#define GLS_EXP_NO_UGU 0
+#endif
 template <int dim, int MODE, int k = 2>
 __host__ __device__ constexpr bool
 field_read(int f)
 {
   using F         = Fields<dim>;
   const bool d12  = f == F::D1 || f == F::D2;
-  const bool u    = f >= F::U && f < F::U + dim;
+  const bool u    = !GLS_EXP_NO_UGU && f >= F::U && f < F::U + dim;
   const bool h    = f == F::H;
   const bool ut   = f >= F::UT && f < F::UT + dim;
-  const bool gu   = f >= F::GU && f < F::GU + dim * dim;
+  const bool gu   = !GLS_EXP_NO_UGU && f >= F::GU && f < F::GU + dim * dim;
   const bool t1   = f >= F::T1 && f < F::T1 + dim;
   return (delta_otf<k, MODE>() ? h : d12) || u || (MODE == MODE_NEWTON && (gu || t1)) ||
          (MODE == MODE_RESIDUAL && ut);
