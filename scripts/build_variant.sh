@@ -19,5 +19,5 @@ done
 wait
 others=$(ls $P/build/*.o | grep -v -e '/gls_op.hip.o' -e '/sweeps.hip.o')
 /opt/rocm/bin/hipcc $HIPFLAGS -shared -o $P/lib/var/$NAME.so $OBJ/gls_op.o $OBJ/sweeps.o $others \
-  -L/opt/rocm/lib -lrocsolver -lrocblas -lrccl -Wl,-rpath,/opt/rocm/lib
+  -L/opt/rocm/lib -lrocsolver -lrocblas -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
 echo "built $P/lib/var/$NAME.so"
