@@ -143,7 +143,7 @@ def survey_bytes(op, td=True, cell_wise=False):
 
 def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src, reps=50):
     """The rest of SURVEY §8d's timing protocol, beside the headline line:
-    cold (MALL flushed by a 1 GiB scratch write between reps) vs warm FP64
+    cold (MALL flushed by a 1 GiB scratch read between reps) vs warm FP64
     at r2, the FP32 level operator (the smoother's hot path) on the same
     mesh, the HBM-bound r+1 mesh (Turek-3D size at r2 = 3) and the
     unstructured sphere deck at r3 (17.1 M DoFs, all geometry per q).  Medians of
@@ -151,8 +151,16 @@ def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src,
     import torch
     import glsamd
     out = {}
-    scratch = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
-    flush = lambda: scratch.fill_(1)  # noqa: E731
+    # cold = the operator's data out of the MALL (256 MB) and the L2s: a 1 GiB
+    # READ between reps, which leaves clean lines of another buffer.  A 1 GiB
+    # WRITE (the flush of rounds 1-6, kept as *_cold_write_flush) leaves dirty
+    # lines whose write-back the timed vmult's own reads trigger: +16.6 us per
+    # r2 vmult inside its events (profiles/r06/explore/cold_probe.txt)
+    scratch = torch.zeros(1 << 30, dtype=torch.uint8, device="cuda")
+    scratch_f32 = scratch.view(torch.float32)
+    sink = torch.zeros((), dtype=torch.float32, device="cuda")
+    flush = lambda: torch.sum(scratch_f32, dim=0, out=sink)  # noqa: E731
+    flush_write = lambda: scratch.fill_(1)  # noqa: E731
 
     def line(op, dst, src, fl=None, prec="f64"):
         for _ in range(5):
@@ -179,6 +187,10 @@ def companions(d, mesh, cmask, params, weights, n_ref, hot_op, hot_dst, hot_src,
 
     out[f"r{n_ref}_f64_warm"] = line(hot_op, hot_dst, hot_src)
     out[f"r{n_ref}_f64_cold"] = line(hot_op, hot_dst, hot_src, flush)
+    out[f"r{n_ref}_f64_cold"]["flush"] = "1 GiB read between reps"
+    out[f"r{n_ref}_f64_cold_write_flush"] = line(hot_op, hot_dst, hot_src, flush_write)
+    out[f"r{n_ref}_f64_cold_write_flush"]["flush"] = (
+        "1 GiB write between reps (its dirty lines written back inside the timed vmult)")
 
     def build(m, cm, prec, dk=d, prm=params, w=weights):
         u_star = gi.linearization_point(m.n_nodes, m.dim, dk.u_max)
@@ -1082,10 +1094,14 @@ def main():
                          # (16 instead of SURVEY's 20 table values per q)
                          "frac_streamed": op.vmult_bytes() / (kernel_ms * 1e-3) / HBM_PEAK,
                          # SURVEY §8d's cold r2 figure (MALL flushed by a 1 GiB
-                         # write between vmults; the warm 133 MB working set fits
-                         # the 256 MB MALL) and the HBM-bound r+1 mesh back to
-                         # back, from the companions below (null without them)
+                         # read between vmults, one synchronize per call; the
+                         # warm 133 MB working set fits the 256 MB MALL), the
+                         # rounds-1-6 write flush beside it, and the HBM-bound
+                         # r+1 mesh back to back, from the companions below
+                         # (null without them)
                          "frac_cold": _comp_get(comp, f"r{n_ref}_f64_cold", "roofline_frac"),
+                         "frac_cold_write_flush": _comp_get(comp, f"r{n_ref}_f64_cold_write_flush",
+                                                            "roofline_frac"),
                          "frac_r3": _comp_get(comp, f"r{n_ref + 1}_f64_warm",
                                               "roofline_frac_back_to_back")},
             "cpu_baseline": cpu,

@@ -245,6 +245,14 @@ contract_v(const V *in, const T *tab, int pa, int base, int s)
 #ifndef GLS_TAB_PREFETCH
 #define GLS_TAB_PREFETCH 0
 #endif
+// Non-temporal stores of the brick write-out (dst rows and partial slots;
+// round 6 experiment): the 20 MB an r2 FP64 vmult writes stream out instead of
+// staying dirty in the L2s until the kernel's end.  Measured and NOT adopted
+// (profiles/r06/explore/ab_nt_store.txt): r2 FP64 33.0 -> 36.9 us, r3 FP64
+// 238 -> 345 us, FP32 r2 23.0 -> 24.0 us.  GLS_NT_STORE=1 builds it.
+#ifndef GLS_NT_STORE
+#define GLS_NT_STORE 0
+#endif
 
 template <int dim, int k, typename T>
 __host__ __device__ constexpr bool

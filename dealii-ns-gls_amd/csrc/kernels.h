@@ -174,6 +174,23 @@ store_node<float, 4>(float *__restrict__ v, uint32_t node, const float (&u)[4])
   *reinterpret_cast<float4 *>(v + (size_t)node * 4) = make_float4(u[0], u[1], u[2], u[3]);
 }
 
+// the same 4-value row as non-temporal 16-byte stores (the brick write-out
+// under GLS_NT_STORE, an A/B build switch)
+template <typename T>
+__device__ __forceinline__ void
+store_node_nt(T *__restrict__ v, uint32_t node, const T (&u)[4])
+{
+  typedef T V2 __attribute__((ext_vector_type(16 / sizeof(T))));
+  V2 *p = reinterpret_cast<V2 *>(v + (size_t)node * 4);
+  if constexpr (sizeof(T) == 8)
+    {
+      __builtin_nontemporal_store(V2{u[0], u[1]}, p);
+      __builtin_nontemporal_store(V2{u[2], u[3]}, p + 1);
+    }
+  else
+    __builtin_nontemporal_store(V2{u[0], u[1], u[2], u[3]}, p);
+}
+
 // 1D contraction along an axis with stride `s` (n points):
 //   forward:   out[p] = sum_j M[pa][j] in[base + j s]
 //   transpose: out[p] = sum_j M[j][pa] in[base + j s]
